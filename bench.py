@@ -1,0 +1,258 @@
+"""Benchmark: bellman_TRM! subproblems/sec on the BASELINE roofline config (C4) -- MI355X.
+
+A "step" is one pass of the hot path over one batch of synthetic input: per rank, `--batch`
+independent subproblems (default 1), each a full bellman_TRM! (DP over nt=65536 steps x 4096 levels
+x B+1=257 budget rows) followed by eval_u_TRM! (backtrack), inputs already resident in HBM.
+Multi-GPU (torchrun, one process per GPU): the problem descriptor is broadcast once over RCCL, each
+rank solves its own restarts (weak scaling, no data-path collective) and the controls (as uint16
+level ranks) plus Φ* are gathered to rank 0 over RCCL at the end of every step.
+
+Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel, measured with HIP events on
+the library's stream; `roofline_valu` gives the FP64-VALU view (the p=1 sweep is VALU-bound);
+`cpu_baseline` times the C restatement of the reference loop (oracle/) on a bounded sample.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md
+FP64_VALU_PEAK_TOPS = 39.3     # 256 CU x 64 FP64 lanes/clk x 2.4 GHz (78.6 TFLOP/s counts an FMA as 2)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--p", default=None, help="override p: 1 or inf")
+    ap.add_argument("--batch", type=int, default=1, help="subproblems per rank per step")
+    ap.add_argument("--nt", type=int, default=None, help="truncate nt (profiling passes only; not a bench line)")
+    ap.add_argument("--variant", default="pinf", help="extra p=Inf line on the same config ('' to skip)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=5, help="recursion steps timed for the CPU baseline")
+    return ap.parse_args()
+
+
+def candidates_per_step(levels, uo, B):
+    """Exact N_cand = sum_l L * max(0, B+1-b̃(l,i)) per step (SURVEY §8 d), averaged over steps."""
+    nv = levels.nuval
+    tot = 0
+    nt = uo.shape[1]
+    for s in range(0, nt - 1, 2048):
+        e = min(nt - 1, s + 2048)
+        bt = np.abs(nv[:, :, None] - uo[None, :, s:e]).sum(axis=1)  # L x steps
+        tot += np.maximum(0, B + 1 - bt).sum()
+    return levels.L * tot / max(1, nt - 1)
+
+
+def run(args, rank, world, device, dist, torch):
+    from mioc import native
+    from mioc.synth import CONFIGS, make_inputs
+
+    cfg = CONFIGS[args.config]
+    p = cfg.p if args.p is None else (math.inf if args.p == "inf" else float(args.p))
+    nt = cfg.nt if args.nt is None else args.nt
+    levels = cfg.levels()
+    B = cfg.B
+
+    # descriptor: broadcast once from rank 0 (RCCL) -- seeds, sizes, parameters
+    desc = torch.tensor([cfg.seed_df, cfg.seed_u, nt, B, cfg.dt, cfg.beta, p if p != math.inf else -1.0],
+                        dtype=torch.float64, device=device)
+    if world > 1:
+        dist.broadcast(desc, src=0)
+    seed_df, seed_u, nt, B, dt, beta, pv = desc.tolist()
+    nt, B = int(nt), int(B)
+    p = math.inf if pv < 0 else pv
+
+    ctx = native.Context(device)
+    ctx.set_levels(levels)
+    ctx.set_cost(p, beta)
+    ctx.set_option(native.MIOC_OPT_TIMING, 1)
+
+    K = args.batch
+    nsets = args.warmup + args.steps
+    dfs, uos = [], []
+    for s in range(nsets):
+        for b in range(K):
+            k = (s * world + rank) * K + b
+            _, df, uo = make_inputs(cfg, k=k, nt=nt, levels=levels)
+            dfs.append(df)
+            uos.append(uo)
+    d_df = torch.tensor(np.stack([d.T for d in dfs]), dtype=torch.float64, device=device).reshape(nsets, K, nt, -1)
+    d_uo = torch.tensor(np.stack([d.T for d in uos]), dtype=torch.float64, device=device).reshape(nsets, K, nt, -1)
+    d_u = torch.empty((K, nt, levels.M), dtype=torch.float64, device=device)
+    d_phi = torch.empty(K, dtype=torch.float64, device=device)
+    d_st = torch.empty(K, dtype=torch.int32, device=device)
+    nuval = torch.tensor(levels.nuval, dtype=torch.float64, device=device)
+    gather_buf = [torch.empty((K, nt), dtype=torch.int16, device=device) for _ in range(world)] if rank == 0 else None
+
+    def step(s):
+        ctx.bellman_batch_device(K, d_df[s].data_ptr(), d_uo[s].data_ptr(), levels.M, nt, B, dt)
+        ctx.backtrack_batch_device(B, d_u.data_ptr(), d_phi.data_ptr(), d_st.data_ptr())
+        if world > 1:
+            ctx.synchronize()
+            # controls as level ranks (uint16 payload) + Φ*, gathered to rank 0 over RCCL
+            ranks = (d_u.reshape(K * nt, 1, -1) == nuval.reshape(1, *nuval.shape)).all(dim=2).int().argmax(dim=1)
+            payload = ranks.to(torch.int16).reshape(K, nt)
+            dist.gather(payload, gather_buf, dst=0)
+            phis = [torch.empty_like(d_phi) for _ in range(world)] if rank == 0 else None
+            dist.gather(d_phi, phis, dst=0)
+
+    for s in range(args.warmup):
+        step(s)
+    ctx.synchronize()
+    torch.cuda.synchronize(device)
+    ctx.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for s in range(args.warmup, nsets):
+        step(s)
+    ctx.synchronize()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    st = d_st.cpu().numpy()
+    if np.any(st != 0):
+        raise RuntimeError(f"rank {rank}: infeasible subproblem status {st}")
+
+    dom_ms, dom_n, dom_name = ctx.kernel_stats(0)
+    walk_ms, walk_n, walk_name = ctx.kernel_stats(1)
+    algo = ctx.last_algo()
+    res = dict(elapsed=elapsed, K=K, nt=nt, B=B, p=p, algo=algo, dom_ms=dom_ms, dom_n=dom_n, dom_name=dom_name,
+               walk_ms=walk_ms, walk_n=walk_n, walk_name=walk_name, levels=levels, uo=uos[-1],
+               phi=d_phi.cpu().numpy().tolist())
+    ctx.close()
+    return res
+
+
+def roofline_of(res, args):
+    """Algorithmic bytes / flops of the dominant kernel per launch (SURVEY §8 d), over its HIP-event time."""
+    lv, B, K, nt = res["levels"], res["B"], res["K"], res["nt"]
+    L = lv.L
+    avg_s = (res["dom_ms"] / 1e3) / max(1, res["dom_n"])
+    if res["dom_name"] == "k_generic_step":
+        # front in + front out (fp64) + compact U (uint16/uint8) per step, per subproblem
+        ub = 1 if L <= 256 else 2
+        bytes_per_launch = K * (B + 1) * L * (8 + 8 + ub)
+        ncand = K * candidates_per_step(lv, res["uo"], B)
+        ops = 2.0 * ncand  # one v_add_f64 + one v_min_f64 per candidate
+        roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
+                     "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
+                     "candidates_per_launch": ncand}
+    else:
+        # k_pinf_recur: one launch per subproblem batch; reads the class table, writes R rows
+        bw = int(min(B, sum(max(v) - min(v) for v in lv.nu))) + 1
+        bytes_per_launch = K * nt * (bw * 8 + (B + 1) * 8)
+        ops = 2.0 * K * (nt - 1) * (B + 1) * bw
+        roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
+                     "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS}
+    ach = bytes_per_launch / avg_s / 1e9
+    roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "kernel": res["dom_name"],
+            "avg_launch_us": round(avg_s * 1e6, 3), "bytes_per_launch": bytes_per_launch}
+    roof_valu = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in roof_valu.items()}
+    return roof, roof_valu
+
+
+def cpu_baseline(args):
+    """The reference recurrence (C restatement, oracle/) on the host: a bounded truncated sample."""
+    from oracle.oracle import OracleC, Levels, P_INF, P_ONE
+    from mioc.synth import CONFIGS, make_inputs
+    cfg = CONFIGS[args.config]
+    p = cfg.p if args.p is None else (math.inf if args.p == "inf" else float(args.p))
+    lt, df, uo = make_inputs(cfg, nt=args.cpu_steps + 1)
+    lv = Levels(lt.nu, [tuple(t) for t in lt.tuples])
+    oc = OracleC()
+    t0 = time.perf_counter()
+    oc.bellman_steps(lv, df, uo, cfg.B, P_INF if p == math.inf else P_ONE, cfg.beta, cfg.dt, args.cpu_steps)
+    dt = time.perf_counter() - t0
+    per_step = dt / args.cpu_steps
+    per_sub = per_step * (cfg.nt - 1)
+    return {"value": 1.0 / per_sub, "unit": "subproblems/s", "cores": 1, "kind": "port",
+            "sample": f"{args.cpu_steps} of {cfg.nt - 1} recursion steps of the reference loop (C restatement, "
+                      f"1 thread) at L={lt.L}, B={cfg.B}; {per_step:.3f} s/step, extrapolated x{cfg.nt - 1}"}
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = local
+    res = run(args, rank, world, device, dist, torch)
+    variant = None
+    if args.variant == "pinf" and args.p is None and args.nt is None and math.isfinite(res["p"]):
+        a2 = argparse.Namespace(**vars(args))
+        a2.p = "inf"
+        a2.steps = max(args.steps, 3)
+        r2 = run(a2, rank, world, device, dist, torch)
+        roof2, valu2 = roofline_of(r2, a2)
+        variant = {"p": "inf", "value": round(world * r2["K"] * a2.steps / r2["elapsed"], 6),
+                   "unit": "subproblems/s", "ms_per_step": round(1e3 * r2["elapsed"] / a2.steps, 3),
+                   "algorithm": "p=Inf exact collapse (k_pinf_prep/recur/walk)", "roofline": roof2,
+                   "roofline_valu": valu2, "backtrack_ms": round(r2["walk_ms"] / max(1, a2.steps), 3)}
+    if rank == 0:
+        roof, valu = roofline_of(res, args)
+        value = world * res["K"] * args.steps / res["elapsed"]
+        out = {
+            "metric": "bellman_TRM! subproblems/sec (nt=65536, 4096 levels, budget=256) + HBM GB/s",
+            "value": round(value, 6),
+            "unit": "subproblems/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * res["elapsed"] / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded N(0,1) df, rand_func_int-shaped u_old; SURVEY §8 d)",
+            "config": {"workload": f"{args.config}: nt={res['nt']}, 4096 levels (8^4 product), B={res['B']}, "
+                                   f"beta=1e-3, p={'inf' if res['p'] == math.inf else int(res['p'])}, "
+                                   f"{res['K']} subproblem(s) per GPU per step",
+                       "parallelism": f"replicas x{world} (independent subproblems, RCCL gather of results)"},
+            "algorithm": {native_name(res["algo"]): res["dom_name"]},
+            "roofline": roof,
+            "roofline_valu": valu,
+            "backtrack_ms": round(res["walk_ms"] / max(1, args.steps), 3),
+        }
+        if variant:
+            out["variant_p_inf"] = variant
+        if not args.no_cpu_baseline and world == 1 and args.nt is None:
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def native_name(algo):
+    return {1: "generic min-plus sweep", 2: "p=Inf exact collapse"}.get(algo, str(algo))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,135 @@
+/*
+ * mioc.h -- C ABI of libmioc, the MI355X (gfx950) implementation of the reference's DP
+ * trust-region subproblem.
+ *
+ * The reference (Julia, Jonas477/mixed-integer-optimal-control---algorithm-tools) has no FFI; the
+ * entry points below are what a `ccall` glue for its hot path binds (INTEGRATION.md shows the Julia
+ * stubs).  Each entry cites the reference interface it replaces.
+ *
+ * Conventions
+ *   - every call returns an int32 status (MIOC_OK == 0, negative on error); no C++ exception
+ *     crosses the ABI; mioc_last_error(ctx) returns a NUL-terminated description;
+ *   - host arrays are borrowed for the duration of a synchronous call only, column-major
+ *     (Julia layout): df[m + nx*i], u[m + nx*i], 0 <= m < nx, 0 <= i < nt;
+ *   - a context owns all device memory (value fronts, the compact argmin table, level tables) and
+ *     keeps the DP resident between mioc_bellman and mioc_backtrack, so the trust-region halving
+ *     path (multi-trust.jl:108-110) costs only a backtrack;
+ *   - a context is not thread-safe; distinct contexts may be used concurrently; every call first
+ *     selects the context's device (HIP's current device is per host thread).
+ */
+#ifndef MIOC_H
+#define MIOC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes --------------------------------------------------------------------------- */
+#define MIOC_OK 0
+#define MIOC_EINVAL -1      /* bad argument / shape */
+#define MIOC_EINEXACT -2    /* |nu - u_old| not integral: the reference's InexactError,
+                               HelpFunctions.jl:37,57 (convert(Int64, ...)) */
+#define MIOC_ENOMEM -3      /* device allocation failed */
+#define MIOC_EHIP -4        /* HIP runtime error */
+#define MIOC_EINFEASIBLE -5 /* no finite value within the budget; the reference would read an
+                               unwritten U cell at HelpFunctions.jl:116 */
+#define MIOC_ESTATE -6      /* call order violated (e.g. backtrack before bellman, B_use > B) */
+#define MIOC_ENONFINITE -7  /* non-finite gradient entry */
+
+/* ---- switching-cost kinds: beta * (sum_m |nu_jm - nu_lm|^p)^(1/p), HelpFunctions.jl:63-67 ----- */
+#define MIOC_P_INF 0    /* p = Inf: the reference evaluates (sum |d|^Inf)^(1/Inf) == x^0.0 == 1.0, so
+                           every transition (including "no switch") costs beta.  Reproduced. */
+#define MIOC_P_ONE 1    /* p = 1: weight = sum_m |d_m| (exact integer) */
+#define MIOC_P_INTLUT 2 /* integer p >= 2: weight = table[sum_m |d_m|^p]; the host supplies Julia's
+                           Float64(S)^(1/p) for S = 0..table_len-1 */
+#define MIOC_P_TABLE 3  /* any p: weight = table[rank_l * L + rank_j] (L*L host-supplied weights) */
+
+/* ---- algorithm selection (mioc_set_option(MIOC_OPT_ALGO, ...)) ----------------------------- */
+#define MIOC_OPT_ALGO 1
+#define MIOC_ALGO_AUTO 0    /* p=Inf -> class collapse, otherwise the generic min-plus sweep */
+#define MIOC_ALGO_GENERIC 1 /* per-step min-plus sweep over every (c, l, j): any p */
+#define MIOC_ALGO_PINF 2    /* exact p=Inf collapse onto per-budget row minima */
+#define MIOC_OPT_TIMING 2   /* 1: record HIP events around the dominant kernel (mioc_kernel_stats) */
+
+typedef struct mioc_ctx mioc_ctx;
+
+const char *mioc_version(void);
+
+/* Create / destroy a context on HIP device `device`. */
+int32_t mioc_create(int32_t device, mioc_ctx **out);
+int32_t mioc_destroy(mioc_ctx *ctx);
+const char *mioc_last_error(const mioc_ctx *ctx);
+int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value);
+
+/*
+ * Flattened admissible-level iterator: replaces `obj.𝓥` + `obj.iterator`
+ * (product_iterator / bounded_sum_iterator, julia_opt/AdmissibleIterators.jl:9-49) as consumed by
+ * bellman_TRM! (HelpFunctions.jl:29,49,60) and eval_u_TRM! (HelpFunctions.jl:104-118).
+ *   counts[M]          |V_m|
+ *   values[sum counts] level values, V_1 then V_2 ...
+ *   tuples[L*M]        admissible tuples in iterator order, tuple-major, 1-based level indices
+ * The iterator order must be the grid's column-major order filtered (both reference iterators are).
+ */
+int32_t mioc_set_levels(mioc_ctx *ctx, int64_t M, const int64_t *counts, const int64_t *values, int64_t L,
+                        const int32_t *tuples);
+
+/*
+ * Switching cost: the `β` and `p` arguments of bellman_TRM! (HelpFunctions.jl:20, :63-67),
+ * TRM_parameters.β / .p (multi-trust.jl:27-28).  p_int is p for MIOC_P_INTLUT; `table` as above.
+ */
+int32_t mioc_set_cost(mioc_ctx *ctx, int32_t p_kind, int64_t p_int, double beta, int64_t table_len,
+                      const double *table);
+
+/*
+ * bellman_TRM!(∇f, u_old, B, β, p, Δt, nu, U, Φ, iterator)  -- HelpFunctions.jl:20-83,
+ * called at multi-trust.jl:112.  U and Φ live in the context (device memory), not on the host:
+ * the reference layout would be 2.21 TB for nt=65536, 4096 levels, B=256.
+ * Host buffers df (∇f) and u_old: nx x nt column-major.  B = floor(Δ⁰/Δt) (multi-trust.jl:69).
+ */
+int32_t mioc_bellman(mioc_ctx *ctx, const double *df, const double *u_old, int64_t nx, int64_t nt, int64_t B,
+                     double dt);
+
+/*
+ * eval_u_TRM!(u, u_old, U, Φ, B, nu)  -- HelpFunctions.jl:98-124, called at multi-trust.jl:110,113.
+ * B_use <= B of the last mioc_bellman (the halving path reuses the DP, multi-trust.jl:108-110).
+ * u_out: nx x nt column-major level values (obj.x); phi_star: the minimal Φ value (nullable);
+ * switch_mask: nt bytes, switch_mask[i] = (u[:,i] != u[:,i-1]), switch_mask[0] = 0 (nullable).
+ */
+int32_t mioc_backtrack(mioc_ctx *ctx, int64_t B_use, double *u_out, double *phi_star, uint8_t *switch_mask);
+
+/*
+ * Batched, device-resident variants (inputs already in HBM; the bench and the multi-GPU batch
+ * runner use these).  K independent subproblems sharing levels, cost, nt and B (random restarts):
+ *   d_df, d_u_old : K x nx x nt (subproblem-major, each nx x nt column-major), device pointers
+ *   d_u_out       : K x nx x nt device pointer;  d_phi_star: K doubles (device, nullable)
+ *   d_status      : K int32 (device, nullable): per-subproblem MIOC_OK / MIOC_EINFEASIBLE
+ * Work is enqueued on the context's stream; call mioc_synchronize before reading results.
+ */
+int32_t mioc_bellman_batch_device(mioc_ctx *ctx, int64_t K, const double *d_df, const double *d_u_old,
+                                  int64_t nx, int64_t nt, int64_t B, double dt);
+int32_t mioc_backtrack_batch_device(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_star,
+                                    int32_t *d_status);
+int32_t mioc_synchronize(mioc_ctx *ctx);
+
+/* The HIP stream the context enqueues on (hipStream_t), for callers that order their own work. */
+void *mioc_stream(mioc_ctx *ctx);
+
+/*
+ * Kernel timing (MIOC_OPT_TIMING=1): HIP events recorded on the context's stream around the
+ * launches of each kernel class.  which: 0 = dominant DP kernel of the last bellman call (generic
+ * step sweep or p=Inf recursion), 2 = p=Inf class-table prep,
+ * 1 = backtrack.  Returns cumulative milliseconds, launch count and the kernel's name.
+ */
+int32_t mioc_kernel_stats(mioc_ctx *ctx, int32_t which, double *total_ms, int64_t *launches,
+                          const char **name);
+int32_t mioc_reset_stats(mioc_ctx *ctx);
+
+/* Which algorithm served the last mioc_bellman* call (MIOC_ALGO_GENERIC / MIOC_ALGO_PINF). */
+int32_t mioc_last_algo(mioc_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIOC_H */

@@ -1,0 +1,552 @@
+// mioc_api.cpp -- the C ABI of libmioc (include/mioc.h): context, validation, buffer management
+// and the orchestration of the gfx950 kernels.  No C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mioc_internal.h"
+
+using namespace mioc;
+
+namespace {
+
+constexpr int kStats = 4;  // 0 dominant DP kernel, 1 backtrack walk, 2 p=Inf prep, 3 argmin
+
+int fail(mioc_ctx *ctx, int code, const std::string &msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+int hip_fail(mioc_ctx *ctx, hipError_t e, const char *where) {
+  return fail(ctx, MIOC_EHIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(ctx, expr)                                      \
+  do {                                                          \
+    hipError_t _e = (expr);                                     \
+    if (_e != hipSuccess) return hip_fail((ctx), _e, #expr);    \
+  } while (0)
+
+template <typename T>
+int grow(mioc_ctx *ctx, T **p, size_t *cap_bytes, size_t need_bytes, const char *what) {
+  if (*p && *cap_bytes >= need_bytes) return MIOC_OK;
+  if (*p) {
+    hipFree(*p);
+    *p = nullptr;
+    *cap_bytes = 0;
+  }
+  if (need_bytes == 0) need_bytes = 16;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), need_bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *p = nullptr;
+    char buf[160];
+    std::snprintf(buf, sizeof buf, "cannot allocate %.3f GB for %s", need_bytes / 1e9, what);
+    return fail(ctx, MIOC_ENOMEM, buf);
+  }
+  *cap_bytes = need_bytes;
+  return MIOC_OK;
+}
+
+LevelsDev levels_dev(const mioc_ctx *ctx) {
+  LevelsDev Lv;
+  Lv.M = (int)ctx->M;
+  Lv.L = (int)ctx->L;
+  Lv.nuval = ctx->d_nuval;
+  Lv.nuint = ctx->d_nuint;
+  Lv.gidx = ctx->d_gidx;
+  Lv.p_kind = ctx->p_kind;
+  Lv.p_int = (int)ctx->p_int;
+  Lv.beta = ctx->beta;
+  Lv.costlut = ctx->d_costlut;
+  Lv.costtab = ctx->d_costtab;
+  return Lv;
+}
+
+ProblemDev problem_dev(const mioc_ctx *ctx) {
+  ProblemDev P;
+  P.K = ctx->K;
+  P.M = (int)ctx->M;
+  P.nt = ctx->nt;
+  P.B = ctx->B;
+  P.RP = ctx->RP;
+  P.dt = ctx->dt;
+  P.df = ctx->d_df;
+  P.uold = ctx->d_uold;
+  return P;
+}
+
+void free_all(mioc_ctx *ctx) {
+  void *ptrs[] = {ctx->d_nuval, ctx->d_nuint,  ctx->d_gidx,      ctx->d_numin,       ctx->d_numax,
+                  ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
+                  ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
+                  ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
+                  ctx->d_status_own};
+  for (void *p : ptrs)
+    if (p) hipFree(p);
+  if (ctx->h_flags) hipHostFree(ctx->h_flags);
+  for (auto &pair : ctx->ev)
+    for (auto &e : pair)
+      if (e) hipEventDestroy(e);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+}
+
+// (re)build the device cost tables for the current levels + cost
+int build_cost_tables(mioc_ctx *ctx) {
+  if (!ctx->have_levels || !ctx->have_cost) return MIOC_OK;
+  const int64_t M = ctx->M, L = ctx->L;
+  std::vector<double> lut;
+  if (ctx->p_kind == MIOC_P_INF) {
+    lut.assign(1, ctx->beta * 1.0);
+  } else if (ctx->p_kind == MIOC_P_ONE || ctx->p_kind == MIOC_P_INTLUT) {
+    int64_t maxkey = 0;
+    for (int64_t m = 0; m < M; ++m) {
+      int64_t d = (int64_t)(ctx->numax_h[m] - ctx->numin_h[m]);
+      int64_t t = 1;
+      if (ctx->p_kind == MIOC_P_ONE)
+        t = d;
+      else
+        for (int64_t q = 0; q < ctx->p_int; ++q) t *= d;
+      maxkey += t;
+    }
+    if (maxkey > (1 << 24)) return fail(ctx, MIOC_EINVAL, "switching-cost key range too large");
+    lut.resize(maxkey + 1);
+    for (int64_t s = 0; s <= maxkey; ++s) {
+      double w;
+      if (ctx->p_kind == MIOC_P_ONE) {
+        w = (double)s;  // sum of |d| accumulated in Float64 is exact; s^(1/1) == s
+      } else {
+        if (s >= (int64_t)ctx->table.size())
+          return fail(ctx, MIOC_EINVAL, "MIOC_P_INTLUT table shorter than the largest key sum |d|^p");
+        w = ctx->table[s];
+      }
+      lut[s] = ctx->beta * w;
+    }
+  } else {  // MIOC_P_TABLE
+    if ((int64_t)ctx->table.size() != L * L)
+      return fail(ctx, MIOC_EINVAL, "MIOC_P_TABLE needs table_len == L*L for the current levels");
+    std::vector<double> tab(L * L);
+    for (int64_t q = 0; q < L * L; ++q) tab[q] = ctx->beta * ctx->table[q];
+    size_t cap = 0;
+    if (ctx->d_costtab) hipFree(ctx->d_costtab), ctx->d_costtab = nullptr;
+    int rc = grow(ctx, &ctx->d_costtab, &cap, tab.size() * sizeof(double), "pair cost table");
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(ctx->d_costtab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
+    lut.assign(1, 0.0);
+  }
+  size_t cap = 0;
+  if (ctx->d_costlut) hipFree(ctx->d_costlut), ctx->d_costlut = nullptr;
+  int rc = grow(ctx, &ctx->d_costlut, &cap, lut.size() * sizeof(double), "cost lut");
+  if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpy(ctx->d_costlut, lut.data(), lut.size() * sizeof(double), hipMemcpyHostToDevice));
+  ctx->costlut_len = (int64_t)lut.size();
+  return MIOC_OK;
+}
+
+void ev_begin(mioc_ctx *ctx, int which, const char *name) {
+  if (!ctx->timing) return;
+  if (!ctx->ev[which][0]) {
+    hipEventCreate(&ctx->ev[which][0]);
+    hipEventCreate(&ctx->ev[which][1]);
+  }
+  hipEventRecord(ctx->ev[which][0], ctx->stream);
+  ctx->stat_name[which] = name;
+}
+void ev_end(mioc_ctx *ctx, int which, int64_t launches) {
+  if (!ctx->timing) return;
+  hipEventRecord(ctx->ev[which][1], ctx->stream);
+  // fold the measurement in at the next synchronising call (no host sync here)
+  ctx->ev_pending[which] = true;
+  ctx->pending_launches[which] = launches;
+}
+void ev_collect(mioc_ctx *ctx) {
+  for (int w = 0; w < kStats; ++w) {
+    if (!ctx->ev_pending[w]) continue;
+    hipEventSynchronize(ctx->ev[w][1]);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->ev[w][0], ctx->ev[w][1]) == hipSuccess) {
+      ctx->stat_ms[w] += ms;
+      ctx->stat_launches[w] += ctx->pending_launches[w];
+    }
+    ctx->ev_pending[w] = false;
+  }
+}
+
+// --------------------------------------------------------------------------------------------------
+// the DP
+// --------------------------------------------------------------------------------------------------
+int run_bellman(mioc_ctx *ctx) {
+  ProblemDev P = problem_dev(ctx);
+  LevelsDev Lv = levels_dev(ctx);
+  // validation pass: finite df, integral u_old, max budget class
+  HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int32_t), ctx->stream));
+  HIP_TRY(ctx, launch_validate(ctx->stream, P, ctx->d_numin, ctx->d_numax, ctx->d_flags));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->h_flags, ctx->d_flags, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->h_flags[0] & 2)
+    return fail(ctx, MIOC_EINEXACT, "u_old has a non-integral entry: convert(Int64, abs(nu - u_old)) "
+                                    "would throw InexactError (HelpFunctions.jl:37,57)");
+  if (ctx->h_flags[0] & 1) return fail(ctx, MIOC_ENONFINITE, "df has a non-finite entry");
+  const int bmax = ctx->h_flags[1];
+
+  int algo = (int)ctx->opt_algo;
+  const bool pinf_ok = ctx->p_kind == MIOC_P_INF && bmax + 1 <= 64 && ctx->RP / 64 <= 16;
+  if (algo == MIOC_ALGO_AUTO) algo = pinf_ok ? MIOC_ALGO_PINF : MIOC_ALGO_GENERIC;
+  if (algo == MIOC_ALGO_PINF && !pinf_ok)
+    return fail(ctx, MIOC_EINVAL, "p=Inf collapse needs p_kind MIOC_P_INF, <= 64 budget classes and B < 1024");
+  ctx->algo = algo;
+  const size_t K = (size_t)ctx->K, nt = (size_t)ctx->nt, L = (size_t)ctx->L, RP = (size_t)ctx->RP;
+
+  if (algo == MIOC_ALGO_GENERIC) {
+    ctx->ubytes = L <= 256 ? 1 : 2;
+    const size_t front_stride = L * RP;
+    int rc = grow(ctx, &ctx->d_front, &ctx->front_cap, 2 * K * front_stride * sizeof(double), "value fronts");
+    if (rc) return rc;
+    const size_t u_stride_k = (nt > 1 ? nt - 1 : 1) * L * (size_t)(ctx->B + 1);
+    rc = grow(ctx, &ctx->d_U, &ctx->U_cap, K * u_stride_k * ctx->ubytes, "argmin table U");
+    if (rc) return rc;
+    double *fr[2] = {ctx->d_front, ctx->d_front + K * front_stride};
+    HIP_TRY(ctx, launch_generic_terminal(ctx->stream, P, Lv, fr[(nt - 1) & 1], front_stride));
+    ev_begin(ctx, 0, "k_generic_step");
+    for (int i = ctx->nt - 2; i >= 0; --i)
+      HIP_TRY(ctx, launch_generic_step(ctx->stream, P, Lv, i, fr[(i + 1) & 1], fr[i & 1], ctx->d_U, ctx->ubytes,
+                                       front_stride, u_stride_k));
+    ev_end(ctx, 0, ctx->nt - 1);
+  } else {
+    PinfDev &D = ctx->pinf;
+    D.BW = bmax + 1;
+    const size_t kcells = K * nt * (size_t)D.BW;
+    size_t cap_km = ctx->pinf_cap_k, cap_k2 = ctx->pinf_cap_k, cap_kf = ctx->pinf_cap_k;
+    int rc = grow(ctx, &D.kmin, &cap_km, kcells * sizeof(double), "class minima");
+    if (!rc) rc = grow(ctx, &D.k2, &cap_k2, kcells * sizeof(double), "class second minima");
+    if (!rc) rc = grow(ctx, &D.kfirst, &cap_kf, kcells * sizeof(double), "class first ranks");
+    if (rc) return rc;
+    ctx->pinf_cap_k = std::min(cap_km, std::min(cap_k2, cap_kf));
+    rc = grow(ctx, &D.R, &ctx->pinf_cap_R, K * nt * RP * sizeof(double), "row minima R");
+    if (rc) return rc;
+    ev_begin(ctx, 2, "k_pinf_prep");
+    HIP_TRY(ctx, launch_pinf_prep(ctx->stream, P, Lv, D));
+    ev_end(ctx, 2, 1);
+    ev_begin(ctx, 0, "k_pinf_recur");
+    HIP_TRY(ctx, launch_pinf_recur(ctx->stream, P, D));
+    ev_end(ctx, 0, 1);
+  }
+  ctx->have_dp = true;
+  return MIOC_OK;
+}
+
+int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_star, int32_t *d_status) {
+  if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "backtrack called before bellman");
+  if (B_use < 0 || B_use > ctx->B)
+    return fail(ctx, MIOC_ESTATE, "B_use must satisfy 0 <= B_use <= B of the last bellman call");
+  ProblemDev P = problem_dev(ctx);
+  LevelsDev Lv = levels_dev(ctx);
+  const size_t K = (size_t)ctx->K, nt = (size_t)ctx->nt;
+  size_t cap = 0;
+  if (!ctx->d_start) {
+    int rc = grow(ctx, &ctx->d_start, &cap, 4096 * sizeof(Start), "start cells");
+    if (rc) return rc;
+  }
+  if (K > 4096) return fail(ctx, MIOC_EINVAL, "batch larger than 4096 subproblems");
+  int rc = grow(ctx, &ctx->d_ranks, &ctx->ranks_cap, K * nt * sizeof(int32_t), "rank path");
+  if (rc) return rc;
+  if (ctx->algo == MIOC_ALGO_GENERIC) {
+    const size_t front_stride = (size_t)ctx->L * ctx->RP;
+    const size_t u_stride_k = (nt > 1 ? nt - 1 : 1) * (size_t)ctx->L * (size_t)(ctx->B + 1);
+    HIP_TRY(ctx, launch_generic_argmin0(ctx->stream, P, Lv, ctx->d_front, front_stride, (int)B_use, ctx->d_start));
+    ev_begin(ctx, 1, "k_generic_walk");
+    HIP_TRY(ctx, launch_generic_walk(ctx->stream, P, Lv, ctx->d_U, ctx->ubytes, u_stride_k, ctx->d_start,
+                                     ctx->d_ranks));
+    ev_end(ctx, 1, 1);
+  } else {
+    HIP_TRY(ctx, launch_pinf_start(ctx->stream, P, Lv, ctx->pinf, (int)B_use, ctx->d_start));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags + 2, 0, 2 * sizeof(int32_t), ctx->stream));
+    ev_begin(ctx, 1, "k_pinf_walk");
+    HIP_TRY(ctx, launch_pinf_walk(ctx->stream, P, Lv, ctx->pinf, ctx->d_start, ctx->d_ranks, ctx->d_flags + 2));
+    ev_end(ctx, 1, 1);
+  }
+  HIP_TRY(ctx, launch_expand(ctx->stream, P, Lv, ctx->d_start, ctx->d_ranks, d_u_out, d_phi_star, d_status));
+  return MIOC_OK;
+}
+
+int check_ready(mioc_ctx *ctx) {
+  if (!ctx) return MIOC_EINVAL;
+  if (!ctx->have_levels) return fail(ctx, MIOC_ESTATE, "mioc_set_levels has not been called");
+  if (!ctx->have_cost) return fail(ctx, MIOC_ESTATE, "mioc_set_cost has not been called");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  return MIOC_OK;
+}
+
+int set_problem(mioc_ctx *ctx, int64_t K, int64_t nx, int64_t nt, int64_t B, double dt) {
+  if (nx != ctx->M) return fail(ctx, MIOC_EINVAL, "nx does not match the number of controls in the level table");
+  if (K < 1 || K > 4096) return fail(ctx, MIOC_EINVAL, "batch size must be in [1, 4096]");
+  if (nt < 1 || nt > (1 << 30)) return fail(ctx, MIOC_EINVAL, "nt out of range");
+  if (B < 0 || B > (1 << 20)) return fail(ctx, MIOC_EINVAL, "B out of range");
+  if (!std::isfinite(dt)) return fail(ctx, MIOC_EINVAL, "dt must be finite");
+  ctx->K = (int)K;
+  ctx->nt = (int)nt;
+  ctx->B = (int)B;
+  ctx->RP = (int)(((B + 1 + kRowTile - 1) / kRowTile) * kRowTile);
+  ctx->dt = dt;
+  ctx->have_dp = false;
+  size_t need = (size_t)K * nx * nt * sizeof(double);
+  size_t cap = ctx->in_cap, cap2 = ctx->in_cap;
+  int rc = grow(ctx, &ctx->d_df, &cap, need, "df copy");
+  if (!rc) rc = grow(ctx, &ctx->d_uold, &cap2, need, "u_old copy");
+  if (rc) return rc;
+  ctx->in_cap = std::min(cap, cap2);
+  return MIOC_OK;
+}
+
+}  // namespace
+
+// ==================================================================================================
+// C ABI
+// ==================================================================================================
+extern "C" {
+
+const char *mioc_version(void) { return "mioc 0.1.0 (gfx950)"; }
+
+int32_t mioc_create(int32_t device, mioc_ctx **out) {
+  if (!out) return MIOC_EINVAL;
+  *out = nullptr;
+  mioc_ctx *ctx = new (std::nothrow) mioc_ctx();
+  if (!ctx) return MIOC_ENOMEM;
+  ctx->device = device;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    delete ctx;
+    return MIOC_EHIP;
+  }
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&ctx->d_flags, 16) != hipSuccess || hipHostMalloc(&ctx->h_flags, 16, 0) != hipSuccess) {
+    free_all(ctx);
+    delete ctx;
+    return MIOC_EHIP;
+  }
+  *out = ctx;
+  return MIOC_OK;
+}
+
+int32_t mioc_destroy(mioc_ctx *ctx) {
+  if (!ctx) return MIOC_EINVAL;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  free_all(ctx);
+  delete ctx;
+  return MIOC_OK;
+}
+
+const char *mioc_last_error(const mioc_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
+  if (!ctx) return MIOC_EINVAL;
+  if (option == MIOC_OPT_ALGO) {
+    if (value < MIOC_ALGO_AUTO || value > MIOC_ALGO_PINF) return fail(ctx, MIOC_EINVAL, "unknown algorithm");
+    ctx->opt_algo = value;
+    return MIOC_OK;
+  }
+  if (option == MIOC_OPT_TIMING) {
+    ctx->timing = value != 0;
+    return MIOC_OK;
+  }
+  return fail(ctx, MIOC_EINVAL, "unknown option");
+}
+
+int32_t mioc_set_levels(mioc_ctx *ctx, int64_t M, const int64_t *counts, const int64_t *values, int64_t L,
+                        const int32_t *tuples) {
+  if (!ctx) return MIOC_EINVAL;
+  if (M < 1 || M > kMaxM) return fail(ctx, MIOC_EINVAL, "number of controls must be in [1, 8]");
+  if (!counts || !values || !tuples) return fail(ctx, MIOC_EINVAL, "null level arrays");
+  if (L < 1 || L > 65535) return fail(ctx, MIOC_EINVAL, "number of admissible tuples must be in [1, 65535]");
+  std::vector<int64_t> off(M + 1, 0);
+  int64_t Lgrid = 1;
+  for (int64_t m = 0; m < M; ++m) {
+    if (counts[m] < 1 || counts[m] > 4096) return fail(ctx, MIOC_EINVAL, "level count out of range");
+    off[m + 1] = off[m] + counts[m];
+    Lgrid *= counts[m];
+    if (Lgrid > (int64_t)1 << 31) return fail(ctx, MIOC_EINVAL, "level grid too large");
+  }
+  for (int64_t q = 0; q < off[M]; ++q)
+    if (values[q] < -(1 << 24) || values[q] > (1 << 24)) return fail(ctx, MIOC_EINVAL, "level value out of range");
+  ctx->M = M;
+  ctx->L = L;
+  ctx->Lgrid = Lgrid;
+  ctx->counts.assign(counts, counts + M);
+  ctx->values.assign(values, values + off[M]);
+  ctx->tuples.assign(tuples, tuples + L * M);
+  ctx->nuval_h.assign(L * M, 0.0);
+  std::vector<int32_t> nuint(L * M), gidx(L);
+  for (int64_t r = 0; r < L; ++r) {
+    int64_t g = 0, stride = 1;
+    for (int64_t m = 0; m < M; ++m) {
+      int32_t t = tuples[r * M + m];
+      if (t < 1 || t > counts[m]) return fail(ctx, MIOC_EINVAL, "tuple level index out of range (1-based)");
+      int64_t v = values[off[m] + t - 1];
+      ctx->nuval_h[r * M + m] = (double)v;
+      nuint[r * M + m] = (int32_t)v;
+      g += (int64_t)(t - 1) * stride;
+      stride *= counts[m];
+    }
+    gidx[r] = (int32_t)g;
+  }
+  ctx->numin_h.assign(M, 0.0);
+  ctx->numax_h.assign(M, 0.0);
+  for (int64_t m = 0; m < M; ++m) {
+    int64_t lo = values[off[m]], hi = values[off[m]];
+    for (int64_t q = off[m]; q < off[m + 1]; ++q) lo = std::min(lo, values[q]), hi = std::max(hi, values[q]);
+    ctx->numin_h[m] = (double)lo;
+    ctx->numax_h[m] = (double)hi;
+  }
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  size_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+  void *olds[] = {ctx->d_nuval, ctx->d_nuint, ctx->d_gidx, ctx->d_numin, ctx->d_numax};
+  for (void *p : olds)
+    if (p) hipFree(p);
+  ctx->d_nuval = nullptr, ctx->d_nuint = nullptr, ctx->d_gidx = nullptr, ctx->d_numin = nullptr, ctx->d_numax = nullptr;
+  int rc = grow(ctx, &ctx->d_nuval, &c0, L * M * sizeof(double), "levels");
+  if (!rc) rc = grow(ctx, &ctx->d_nuint, &c1, L * M * sizeof(int32_t), "levels");
+  if (!rc) rc = grow(ctx, &ctx->d_gidx, &c2, L * sizeof(int32_t), "levels");
+  if (!rc) rc = grow(ctx, &ctx->d_numin, &c3, M * sizeof(double), "levels");
+  if (!rc) rc = grow(ctx, &ctx->d_numax, &c4, M * sizeof(double), "levels");
+  if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpy(ctx->d_nuval, ctx->nuval_h.data(), L * M * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(ctx, hipMemcpy(ctx->d_nuint, nuint.data(), L * M * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIP_TRY(ctx, hipMemcpy(ctx->d_gidx, gidx.data(), L * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIP_TRY(ctx, hipMemcpy(ctx->d_numin, ctx->numin_h.data(), M * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(ctx, hipMemcpy(ctx->d_numax, ctx->numax_h.data(), M * sizeof(double), hipMemcpyHostToDevice));
+  ctx->have_levels = true;
+  ctx->have_dp = false;
+  return build_cost_tables(ctx);
+}
+
+int32_t mioc_set_cost(mioc_ctx *ctx, int32_t p_kind, int64_t p_int, double beta, int64_t table_len,
+                      const double *table) {
+  if (!ctx) return MIOC_EINVAL;
+  if (p_kind < MIOC_P_INF || p_kind > MIOC_P_TABLE) return fail(ctx, MIOC_EINVAL, "unknown p_kind");
+  if (!std::isfinite(beta)) return fail(ctx, MIOC_EINVAL, "beta must be finite");
+  if (p_kind == MIOC_P_INTLUT && (p_int < 2 || p_int > 8))
+    return fail(ctx, MIOC_EINVAL, "MIOC_P_INTLUT needs 2 <= p_int <= 8");
+  if ((p_kind == MIOC_P_INTLUT || p_kind == MIOC_P_TABLE) && (!table || table_len < 1))
+    return fail(ctx, MIOC_EINVAL, "this p_kind needs a host-supplied weight table");
+  ctx->p_kind = p_kind;
+  ctx->p_int = p_kind == MIOC_P_INTLUT ? p_int : 1;
+  ctx->beta = beta;
+  if (table && table_len > 0)
+    ctx->table.assign(table, table + table_len);
+  else
+    ctx->table.clear();
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  ctx->have_cost = true;
+  ctx->have_dp = false;
+  return build_cost_tables(ctx);
+}
+
+int32_t mioc_bellman_batch_device(mioc_ctx *ctx, int64_t K, const double *d_df, const double *d_u_old, int64_t nx,
+                                  int64_t nt, int64_t B, double dt) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (!d_df || !d_u_old) return fail(ctx, MIOC_EINVAL, "null input pointer");
+  rc = set_problem(ctx, K, nx, nt, B, dt);
+  if (rc) return rc;
+  const size_t bytes = (size_t)K * nx * nt * sizeof(double);
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->d_df, d_df, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->d_uold, d_u_old, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  return run_bellman(ctx);
+}
+
+int32_t mioc_bellman(mioc_ctx *ctx, const double *df, const double *u_old, int64_t nx, int64_t nt, int64_t B,
+                     double dt) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (!df || !u_old) return fail(ctx, MIOC_EINVAL, "null input pointer");
+  rc = set_problem(ctx, 1, nx, nt, B, dt);
+  if (rc) return rc;
+  const size_t bytes = (size_t)nx * nt * sizeof(double);
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->d_df, df, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->d_uold, u_old, bytes, hipMemcpyHostToDevice, ctx->stream));
+  rc = run_bellman(ctx);
+  if (rc) return rc;
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  ev_collect(ctx);
+  return MIOC_OK;
+}
+
+int32_t mioc_backtrack_batch_device(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_star,
+                                    int32_t *d_status) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (!d_u_out) return fail(ctx, MIOC_EINVAL, "null output pointer");
+  return run_backtrack(ctx, B_use, d_u_out, d_phi_star, d_status);
+}
+
+int32_t mioc_backtrack(mioc_ctx *ctx, int64_t B_use, double *u_out, double *phi_star, uint8_t *switch_mask) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (!u_out) return fail(ctx, MIOC_EINVAL, "null output pointer");
+  if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "backtrack called before bellman");
+  if (ctx->K != 1) return fail(ctx, MIOC_ESTATE, "host backtrack after a batched bellman: use the batch API");
+  const size_t n = (size_t)ctx->M * ctx->nt;
+  size_t c1 = 0, c2 = 0;
+  rc = grow(ctx, &ctx->d_uout_own, &ctx->uout_cap, n * sizeof(double), "u staging");
+  if (!rc && !ctx->d_phistar_own) rc = grow(ctx, &ctx->d_phistar_own, &c1, 16, "phi staging");
+  if (!rc && !ctx->d_status_own) rc = grow(ctx, &ctx->d_status_own, &c2, 16, "status staging");
+  if (rc) return rc;
+  rc = run_backtrack(ctx, B_use, ctx->d_uout_own, ctx->d_phistar_own, ctx->d_status_own);
+  if (rc) return rc;
+  double ps = 0.0;
+  int32_t st = 0;
+  HIP_TRY(ctx, hipMemcpyAsync(u_out, ctx->d_uout_own, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(&ps, ctx->d_phistar_own, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->d_status_own, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  ev_collect(ctx);
+  if (phi_star) *phi_star = ps;
+  if (st != MIOC_OK) return fail(ctx, MIOC_EINFEASIBLE, "no finite Φ value within the budget B_use");
+  if (switch_mask) {
+    const int64_t M = ctx->M;
+    switch_mask[0] = 0;
+    for (int64_t i = 1; i < ctx->nt; ++i) {
+      uint8_t sw = 0;
+      for (int64_t m = 0; m < M; ++m) sw |= u_out[m + M * i] != u_out[m + M * (i - 1)];
+      switch_mask[i] = sw;
+    }
+  }
+  return MIOC_OK;
+}
+
+int32_t mioc_synchronize(mioc_ctx *ctx) {
+  if (!ctx) return MIOC_EINVAL;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  ev_collect(ctx);
+  return MIOC_OK;
+}
+
+void *mioc_stream(mioc_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int32_t mioc_kernel_stats(mioc_ctx *ctx, int32_t which, double *total_ms, int64_t *launches, const char **name) {
+  if (!ctx || which < 0 || which >= kStats) return MIOC_EINVAL;
+  ev_collect(ctx);
+  if (total_ms) *total_ms = ctx->stat_ms[which];
+  if (launches) *launches = ctx->stat_launches[which];
+  if (name) *name = ctx->stat_name[which];
+  return MIOC_OK;
+}
+
+int32_t mioc_reset_stats(mioc_ctx *ctx) {
+  if (!ctx) return MIOC_EINVAL;
+  ev_collect(ctx);
+  for (int w = 0; w < kStats; ++w) ctx->stat_ms[w] = 0.0, ctx->stat_launches[w] = 0;
+  return MIOC_OK;
+}
+
+int32_t mioc_last_algo(mioc_ctx *ctx) { return ctx ? ctx->algo : MIOC_EINVAL; }
+
+}  // extern "C"

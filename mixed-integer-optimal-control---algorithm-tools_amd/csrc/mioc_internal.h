@@ -1,0 +1,153 @@
+// mioc_internal.h -- context and kernel-launch declarations shared by the C ABI (mioc_api.cpp)
+// and the gfx950 kernels (mioc_generic.hip, mioc_pinf.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/mioc.h"
+
+namespace mioc {
+
+constexpr int kMaxM = 8;          // controls per tuple supported by the kernels
+constexpr int kRowTile = 64;      // budget rows per lane-tile; fronts are padded to a multiple
+
+// Device-side view of the flattened level table + switching cost, passed by value to kernels.
+struct LevelsDev {
+  int M = 0;
+  int L = 0;
+  const double *nuval = nullptr;   // [L][M] level values per iterator rank
+  const int32_t *nuint = nullptr;  // [L][M] same, as int32 (distance keys)
+  const int32_t *gidx = nullptr;   // [L] grid linear index per rank (argmin tie-break)
+  int p_kind = MIOC_P_INF;
+  int p_int = 1;
+  double beta = 0.0;
+  const double *costlut = nullptr; // beta*weight by integer key (P_INF: [beta], P_ONE/P_INTLUT)
+  const double *costtab = nullptr; // [L][L] beta*weight (P_TABLE only)
+};
+
+// One batch of K subproblems sharing levels, cost, nt, B.
+struct ProblemDev {
+  int K = 0;
+  int M = 0;
+  int nt = 0;
+  int B = 0;
+  int RP = 0;                      // padded rows per front column: roundup(B+1, 64)
+  double dt = 0.0;
+  const double *df = nullptr;      // [K][nt][M]  (each subproblem nx x nt column-major)
+  const double *uold = nullptr;    // [K][nt][M]
+};
+
+struct Start {                      // backtrack start cell per subproblem
+  double phi;
+  int32_t c;
+  int32_t r;
+  int32_t status;
+  int32_t pad;
+};
+
+// ---- kernel launchers (mioc_generic.hip) ------------------------------------------------------
+hipError_t launch_validate(hipStream_t s, const ProblemDev &P, const double *numin, const double *numax,
+                           int32_t *flags);
+hipError_t launch_generic_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, double *front,
+                                   size_t front_stride);
+hipError_t launch_generic_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, int i,
+                               const double *psi, double *phi, void *U, int ubytes, size_t front_stride,
+                               size_t u_stride_k);
+hipError_t launch_generic_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const double *front0,
+                                  size_t front_stride, int Bu, Start *start);
+hipError_t launch_generic_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const void *U, int ubytes,
+                               size_t u_stride_k, const Start *start, int32_t *ranks);
+hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const Start *start,
+                         const int32_t *ranks, double *u_out, double *phi_star, int32_t *status);
+
+// ---- p = Inf collapse (mioc_pinf.hip) -----------------------------------------------------------
+struct PinfDev {
+  int BW = 0;                      // budget classes tracked: bmax+1 <= B+1
+  double *kmin = nullptr;          // [K][nt][BW] min over ranks of class b of K_r (T1 at terminal)
+  double *k2 = nullptr;            // [K][nt][BW] second-smallest distinct value in the class
+  int32_t *kfirst = nullptr;       // [K][nt][BW] first rank attaining kmin
+  double *R = nullptr;             // [K][nt][RP] row minima R_i[c] = min_r Φ_i[c, r]
+};
+hipError_t launch_pinf_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D);
+hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D);
+hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D, int Bu,
+                             Start *start);
+hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
+                            const Start *start, int32_t *ranks, int32_t *nfallback);
+
+}  // namespace mioc
+
+// ---- the context ----------------------------------------------------------------------------------
+struct mioc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int64_t opt_algo = MIOC_ALGO_AUTO;
+  bool timing = false;
+
+  // levels (host copies + device tables)
+  bool have_levels = false;
+  int64_t M = 0, L = 0, Lgrid = 0;
+  std::vector<int64_t> counts, values;
+  std::vector<int32_t> tuples;     // [L][M] 1-based
+  std::vector<double> nuval_h;     // [L][M]
+  std::vector<double> numin_h, numax_h;
+  double *d_nuval = nullptr;
+  int32_t *d_nuint = nullptr;
+  int32_t *d_gidx = nullptr;
+  double *d_numin = nullptr, *d_numax = nullptr;
+
+  // cost
+  bool have_cost = false;
+  int32_t p_kind = MIOC_P_INF;
+  int64_t p_int = 1;
+  double beta = 0.0;
+  std::vector<double> table;
+  double *d_costlut = nullptr;
+  double *d_costtab = nullptr;
+  int64_t costlut_len = 0;
+
+  // owned problem inputs (device)
+  double *d_df = nullptr, *d_uold = nullptr;
+  size_t in_cap = 0;               // doubles per array
+
+  // last DP
+  bool have_dp = false;
+  int algo = 0;
+  int K = 0, nt = 0, B = 0, RP = 0;
+  double dt = 0.0;
+
+  // generic buffers
+  double *d_front = nullptr;       // [2][K][L][RP]
+  size_t front_cap = 0;            // bytes
+  void *d_U = nullptr;             // [K][nt-1][L][B+1] uint8 / uint16
+  size_t U_cap = 0;                // bytes
+  int ubytes = 1;
+
+  // p = Inf buffers
+  mioc::PinfDev pinf;
+  size_t pinf_cap_k = 0, pinf_cap_R = 0;
+
+  // backtrack scratch
+  mioc::Start *d_start = nullptr;
+  int32_t *d_ranks = nullptr;
+  size_t ranks_cap = 0;
+  int32_t *d_flags = nullptr;      // [4] validation flags / counters
+  int32_t *h_flags = nullptr;      // pinned mirror
+  double *d_uout_own = nullptr;    // host-API backtrack output staging
+  double *d_phistar_own = nullptr;
+  int32_t *d_status_own = nullptr;
+  size_t uout_cap = 0;
+
+  // timing
+  hipEvent_t ev[4][2] = {};
+  double stat_ms[4] = {};
+  int64_t stat_launches[4] = {};
+  bool ev_pending[4] = {};
+  int64_t pending_launches[4] = {};
+  const char *stat_name[4] = {"", "", "", ""};
+};

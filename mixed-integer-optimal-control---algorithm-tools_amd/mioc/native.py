@@ -1,0 +1,227 @@
+"""ctypes binding of ``libmioc.so`` (the C ABI declared in ``include/mioc.h``).
+
+This is the product path.  There is no CPU fallback: if the HIP library is missing or no GPU is
+visible, every entry point raises ``MiocNativeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+
+import numpy as np
+
+from .iterators import LevelTable
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libmioc.so")
+
+MIOC_OK = 0
+MIOC_EINVAL = -1
+MIOC_EINEXACT = -2
+MIOC_ENOMEM = -3
+MIOC_EHIP = -4
+MIOC_EINFEASIBLE = -5
+MIOC_ESTATE = -6
+MIOC_ENONFINITE = -7
+
+MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
+MIOC_OPT_ALGO, MIOC_OPT_TIMING = 1, 2
+MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF = 0, 1, 2
+
+EXPORTED = [
+    "mioc_version", "mioc_create", "mioc_destroy", "mioc_last_error", "mioc_set_option", "mioc_set_levels",
+    "mioc_set_cost", "mioc_bellman", "mioc_backtrack", "mioc_bellman_batch_device",
+    "mioc_backtrack_batch_device", "mioc_synchronize", "mioc_stream", "mioc_kernel_stats",
+    "mioc_reset_stats", "mioc_last_algo",
+]
+
+
+class MiocNativeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"mioc error {code}: {msg}")
+        self.code = code
+
+
+class InexactError(MiocNativeError):
+    """Non-integral |ν - u_old| -- the reference's InexactError (HelpFunctions.jl:37,57)."""
+
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load libmioc.so; raise loudly if it is missing (no silent fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise MiocNativeError(MIOC_EHIP, f"HIP library not built: {p} (run __graft_entry__.build())")
+    # One HIP runtime per process: torch ships its own libamdhip64.so (soname libamdhip64.so.7).
+    # Loading torch first makes the dynamic linker bind libmioc's DT_NEEDED libamdhip64.so.7 to that
+    # same runtime, so torch tensors / torch.distributed and libmioc share devices and streams.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(p)
+    vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+    sig = {
+        "mioc_version": (ctypes.c_char_p, []),
+        "mioc_create": (i32, [i32, ctypes.POINTER(vp)]),
+        "mioc_destroy": (i32, [vp]),
+        "mioc_last_error": (ctypes.c_char_p, [vp]),
+        "mioc_set_option": (i32, [vp, i32, i64]),
+        "mioc_set_levels": (i32, [vp, i64, vp, vp, i64, vp]),
+        "mioc_set_cost": (i32, [vp, i32, i64, dbl, i64, vp]),
+        "mioc_bellman": (i32, [vp, vp, vp, i64, i64, i64, dbl]),
+        "mioc_backtrack": (i32, [vp, i64, vp, ctypes.POINTER(dbl), vp]),
+        "mioc_bellman_batch_device": (i32, [vp, i64, vp, vp, i64, i64, i64, dbl]),
+        "mioc_backtrack_batch_device": (i32, [vp, i64, vp, vp, vp]),
+        "mioc_synchronize": (i32, [vp]),
+        "mioc_stream": (vp, [vp]),
+        "mioc_kernel_stats": (i32, [vp, i32, ctypes.POINTER(dbl), ctypes.POINTER(i64),
+                                    ctypes.POINTER(ctypes.c_char_p)]),
+        "mioc_reset_stats": (i32, [vp]),
+        "mioc_last_algo": (i32, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def cost_spec(p, L=None, levels=None):
+    """Map the reference's ``p`` (Int, Float64 or Inf; multi-trust.jl:28) to (p_kind, p_int, table).
+
+    p = Inf and p = 1 are exact on the device.  For other p the weight (sum |d|^p)^(1/p) uses
+    Julia's own ``^`` in the reference; here the host supplies it (computed with Python's pow unless a
+    caller passes Julia's values) -- parity for p not in {1, Inf} is unpinned.
+    """
+    if p == math.inf:
+        return MIOC_P_INF, 1, None
+    if float(p) == 1.0:
+        return MIOC_P_ONE, 1, None
+    if float(p) == int(p) and 2 <= int(p) <= 8:
+        pi = int(p)
+        maxkey = sum(int(max(v) - min(v)) ** pi for v in levels.nu)
+        return MIOC_P_INTLUT, pi, np.array([float(s) ** (1.0 / pi) for s in range(maxkey + 1)])
+    if not p > 0:
+        raise ValueError("Only positive integer valued `p` are accepted!")
+    nv = levels.nuval
+    d = np.abs(nv[:, None, :] - nv[None, :, :]) ** float(p)
+    return MIOC_P_TABLE, 1, np.ascontiguousarray((d.sum(axis=2) ** (1.0 / float(p))).reshape(-1))
+
+
+class Context:
+    """One device context: levels + cost + the resident DP (fronts / argmin table / class tables)."""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.mioc_create(int(device), ctypes.byref(h))
+        if rc != MIOC_OK:
+            raise MiocNativeError(rc, f"mioc_create(device={device}) failed (no visible HIP device?)")
+        self.h = h
+        self.levels = None
+        self.M = None
+        self.nt = None
+        self.B = None
+
+    def close(self):
+        if self.h:
+            self.lib.mioc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != MIOC_OK:
+            msg = self.lib.mioc_last_error(self.h).decode()
+            if rc == MIOC_EINEXACT:
+                raise InexactError(rc, msg)
+            raise MiocNativeError(rc, msg)
+
+    def set_option(self, option, value):
+        self._check(self.lib.mioc_set_option(self.h, option, int(value)))
+
+    def set_levels(self, levels: LevelTable):
+        self.levels = levels
+        self.M = levels.M
+        self._check(self.lib.mioc_set_levels(self.h, levels.M, _p(levels.counts), _p(levels.values),
+                                             levels.L, _p(levels.tuples)))
+
+    def set_cost(self, p, beta, table=None, p_int=None, p_kind=None):
+        if p_kind is None:
+            p_kind, p_int, tab = cost_spec(p, levels=self.levels)
+            if table is not None:
+                tab = np.ascontiguousarray(table, dtype=np.float64)
+        else:
+            tab = None if table is None else np.ascontiguousarray(table, dtype=np.float64)
+            p_int = p_int or 1
+        self._tab = tab
+        self._check(self.lib.mioc_set_cost(self.h, p_kind, int(p_int), float(beta),
+                                           0 if tab is None else tab.size,
+                                           None if tab is None else _p(tab)))
+
+    # -- host-buffer API (Julia-style: ∇f and u_old are nx x nt, column-major) --------------
+    def bellman(self, df, u_old, B, dt):
+        df = np.asfortranarray(df, dtype=np.float64)
+        u_old = np.asfortranarray(u_old, dtype=np.float64)
+        if df.shape != u_old.shape:
+            raise ValueError("df and u_old must have the same shape (nx, nt)")
+        nx, nt = df.shape
+        self.nt, self.B = nt, int(B)
+        self._check(self.lib.mioc_bellman(self.h, _p(df), _p(u_old), nx, nt, int(B), float(dt)))
+
+    def backtrack(self, B_use=None):
+        B_use = self.B if B_use is None else int(B_use)
+        u = np.zeros((self.M, self.nt), dtype=np.float64, order="F")
+        ps = ctypes.c_double(0.0)
+        sw = np.zeros(self.nt, dtype=np.uint8)
+        self._check(self.lib.mioc_backtrack(self.h, B_use, _p(u), ctypes.byref(ps), _p(sw)))
+        return u, ps.value, sw.astype(bool)
+
+    # -- device-resident batch API (pointers are device addresses, e.g. torch .data_ptr()) ----
+    def bellman_batch_device(self, K, df_ptr, uold_ptr, nx, nt, B, dt):
+        self.nt, self.B = nt, int(B)
+        self._check(self.lib.mioc_bellman_batch_device(self.h, int(K), ctypes.c_void_p(df_ptr),
+                                                       ctypes.c_void_p(uold_ptr), int(nx), int(nt), int(B),
+                                                       float(dt)))
+
+    def backtrack_batch_device(self, B_use, u_ptr, phi_ptr=0, status_ptr=0):
+        self._check(self.lib.mioc_backtrack_batch_device(self.h, int(B_use), ctypes.c_void_p(u_ptr),
+                                                         ctypes.c_void_p(phi_ptr or None),
+                                                         ctypes.c_void_p(status_ptr or None)))
+
+    def synchronize(self):
+        self._check(self.lib.mioc_synchronize(self.h))
+
+    def stream(self):
+        return self.lib.mioc_stream(self.h)
+
+    def kernel_stats(self, which=0):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int64(0)
+        name = ctypes.c_char_p()
+        self._check(self.lib.mioc_kernel_stats(self.h, int(which), ctypes.byref(ms), ctypes.byref(n),
+                                               ctypes.byref(name)))
+        return ms.value, n.value, (name.value or b"").decode()
+
+    def reset_stats(self):
+        self._check(self.lib.mioc_reset_stats(self.h))
+
+    def last_algo(self):
+        return self.lib.mioc_last_algo(self.h)

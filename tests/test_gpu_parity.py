@@ -1,0 +1,277 @@
+"""GPU parity: libmioc (through the C ABI) against the CPU oracle and the golden fixtures.
+
+Bar: the control u (hence the switching pattern) and Φ* bit-identical to the oracle; pred within
+1e-12 relative.  Full-size configs that the oracle finishes in seconds (C1, C2, C3, one C5 restart)
+are compared directly; the 4096-level C4 config is compared on truncated fixtures and, at full
+size, through size-independent properties (exact objective recomputation along the returned path,
+exact budget, admissibility, DP(B)/backtrack(B') == DP(B')/backtrack(B'), algorithm agreement).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import golden_files, load_golden
+from mioc import native
+from mioc.iterators import LevelTable
+from mioc.synth import CONFIGS, make_inputs
+from oracle.oracle import P_INF, P_INTLUT, P_ONE, Levels
+
+pytestmark = pytest.mark.gpu
+
+ALGOS_PINF = (native.MIOC_ALGO_PINF, native.MIOC_ALGO_GENERIC)
+
+
+def _ctx(levels, p_kind, beta, algo, p_int=1, table=None):
+    ctx = native.Context(0)
+    ctx.set_levels(levels)
+    ctx.set_cost(None, beta, table=table, p_int=p_int, p_kind=p_kind)
+    ctx.set_option(native.MIOC_OPT_ALGO, algo)
+    return ctx
+
+
+def _oracle_levels(lt):
+    return Levels(lt.nu, [tuple(int(x) for x in t) for t in lt.tuples])
+
+
+def _algos(p_kind):
+    return ALGOS_PINF if p_kind == P_INF else (native.MIOC_ALGO_GENERIC,)
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
+def test_golden_fixtures(path):
+    g = load_golden(path)
+    lt = LevelTable(g["nu"], g["tuple_list"])
+    table = g["wtab"] if g["wtab"].size else None
+    for algo in _algos(g["p_kind"]):
+        ctx = _ctx(lt, g["p_kind"], g["beta"], algo, p_int=g["p_int"], table=table)
+        ctx.bellman(g["df"], g["u_old"], g["B"], g["dt"])
+        assert ctx.last_algo() == algo
+        u, phi, sw = ctx.backtrack(g["Bp"])
+        assert np.array_equal(u, g["u"]), f"{g['name']} algo={algo}"
+        assert phi == g["phi_star"][0], f"{g['name']} algo={algo}: {phi!r} vs {g['phi_star'][0]!r}"
+        assert np.array_equal(sw[1:], np.any(g["u"][:, 1:] != g["u"][:, :-1], axis=0))
+        ctx.close()
+
+
+def _random_case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    shapes = [([[0, 1]] * 3, "sos1"), ([[0, 1, 2], [0, 1]], "prod"), ([[-2, 0, 3]], "prod"),
+              ([list(range(4))] * 2, "prod"), ([[0, 1]] * 4, "prod"), ([list(range(6))] * 2, "prod")]
+    nu, kind = shapes[seed % len(shapes)]
+    lv = Levels.product(nu) if kind == "prod" else Levels.bounded_sum(nu, 1, 1)
+    n = int(rng.integers(1, 40))
+    B = int(rng.integers(0, 30))
+    mode = seed % 4
+    if mode == 0:
+        df = np.zeros((lv.M, n))                              # all ties
+    elif mode == 1:
+        df = rng.integers(-4, 5, size=(lv.M, n)).astype(float)  # integer gradients: many exact ties
+    else:
+        df = rng.standard_normal((lv.M, n))
+    uo = np.array([lv.nuval[rng.integers(lv.L)] for _ in range(n)], dtype=np.float64).T
+    return lv, df, uo, B, rng
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_random_vs_oracle(oracle_c, seed):
+    lv, df, uo, B, rng = _random_case(seed)
+    pk = [P_ONE, P_INF][seed % 2]
+    beta = [1e-3, 0.25, 0.1][seed % 3]
+    dt = [0.5, 1 / 3, 2.0 ** -6][seed % 3]
+    phi, U = oracle_c.bellman(lv, df, uo, B, pk, beta, dt)
+    lt = LevelTable(lv.nu, [tuple(t) for t in lv.tuples])
+    budgets = sorted({B, B // 2, 0, int(rng.integers(0, B + 1))})
+    for algo in _algos(pk):
+        ctx = _ctx(lt, pk, beta, algo)
+        ctx.bellman(df, uo, B, dt)
+        for Bp in budgets:  # one DP, several budgets: the halving reuse of multi-trust.jl:108-110
+            try:
+                ou, ops = oracle_c.backtrack(lv, uo, phi, U, B, Bp)
+            except Exception:
+                with pytest.raises(native.MiocNativeError):
+                    ctx.backtrack(Bp)
+                continue
+            u, ps, _ = ctx.backtrack(Bp)
+            assert np.array_equal(u, ou), f"seed={seed} algo={algo} Bp={Bp}"
+            assert ps == ops, f"seed={seed} algo={algo} Bp={Bp}: {ps!r} vs {ops!r}"
+        ctx.close()
+
+
+def test_p2_lut_and_table_kinds_vs_oracle(oracle_c):
+    cfg = CONFIGS["C5"]
+    lt, df, uo = make_inputs(cfg, nt=40)
+    lv = _oracle_levels(lt)
+    B = 20
+    k, pint, tab = native.cost_spec(2, levels=lt)
+    phi, U = oracle_c.bellman(lv, df, uo, B, P_INTLUT, 1e-3, cfg.dt, p_int=2, wtab=tab)
+    ou, ops = oracle_c.backtrack(lv, uo, phi, U, B, B)
+    ctx = _ctx(lt, k, 1e-3, native.MIOC_ALGO_GENERIC, p_int=pint, table=tab)
+    ctx.bellman(df, uo, B, cfg.dt)
+    u, ps, _ = ctx.backtrack(B)
+    assert np.array_equal(u, ou) and ps == ops
+    # the same weights as a full pair table (MIOC_P_TABLE) must give the same answer
+    nv = lt.nuval
+    S = (np.abs(nv[:, None, :] - nv[None, :, :]) ** 2).sum(axis=2).astype(int)
+    ctx2 = _ctx(lt, native.MIOC_P_TABLE, 1e-3, native.MIOC_ALGO_GENERIC, table=tab[S].reshape(-1))
+    ctx2.bellman(df, uo, B, cfg.dt)
+    u2, ps2, _ = ctx2.backtrack(B)
+    assert np.array_equal(u2, ou) and ps2 == ops
+
+
+@pytest.mark.parametrize("key", ["C1", "C2", "C3"])
+def test_full_size_sos1_configs_vs_oracle(oracle_c, key):
+    """C1/C2/C3 at their full BASELINE sizes (3-of-8 SOS1 levels, p=Inf): both algorithms."""
+    cfg = CONFIGS[key]
+    lt, df, uo = make_inputs(cfg)
+    lv = _oracle_levels(lt)
+    phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_INF, cfg.beta, cfg.dt)
+    for Bp in (cfg.B, cfg.B // 2, cfg.B // 8):
+        ou, ops = oracle_c.backtrack(lv, uo, phi, U, cfg.B, Bp)
+        for algo in ALGOS_PINF:
+            ctx = _ctx(lt, P_INF, cfg.beta, algo)
+            ctx.bellman(df, uo, cfg.B, cfg.dt)
+            u, ps, _ = ctx.backtrack(Bp)
+            assert np.array_equal(u, ou), f"{key} algo={algo} Bp={Bp}"
+            assert ps == ops
+            ctx.close()
+
+
+def test_full_size_c5_restart_vs_oracle(oracle_c):
+    cfg = CONFIGS["C5"]
+    lt, df, uo = make_inputs(cfg, k=3)
+    lv = _oracle_levels(lt)
+    phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_ONE, cfg.beta, cfg.dt)
+    ou, ops = oracle_c.backtrack(lv, uo, phi, U, cfg.B, cfg.B)
+    ctx = _ctx(lt, P_ONE, cfg.beta, native.MIOC_ALGO_GENERIC)
+    ctx.bellman(df, uo, cfg.B, cfg.dt)
+    u, ps, _ = ctx.backtrack(cfg.B)
+    assert np.array_equal(u, ou) and ps == ops
+
+
+def _path_objective(lt, df, u, dt, beta, p_kind):
+    """Φ* recomputed along a control in the reference's rounding order (HelpFunctions.jl:52-71)."""
+    M, n = u.shape
+    T1 = np.zeros(n)
+    for m in range(M):
+        T1 = T1 + (dt * df[m]) * u[m]
+    if p_kind == P_INF:
+        cost = np.full(n - 1, beta * 1.0)
+    else:
+        w = np.zeros(n - 1)
+        for m in range(M):
+            w = w + np.abs(u[m, 1:] - u[m, :-1])
+        cost = beta * w
+    K = T1[:-1] + cost
+    V = T1[-1]
+    for i in range(n - 2, -1, -1):
+        V = K[i] + V
+    return V
+
+
+@pytest.mark.parametrize("p", [math.inf, 1], ids=["pinf", "p1"])
+def test_full_size_c4_properties(p):
+    """The 4096-level / nt=65536 / B=256 roofline config: properties that hold at any size."""
+    cfg = CONFIGS["C4"]
+    lt, df, uo = make_inputs(cfg)
+    pk = P_INF if p == math.inf else P_ONE
+    B = cfg.B
+    ctx = _ctx(lt, pk, cfg.beta, native.MIOC_ALGO_AUTO)
+    ctx.bellman(df, uo, B, cfg.dt)
+    results = {}
+    for Bp in (B, B // 2):
+        u, ps, _ = ctx.backtrack(Bp)
+        rows = {tuple(r) for r in lt.nuval}
+        assert all(tuple(c) in rows for c in u.T)                          # admissible
+        used = int(np.abs(u - uo).sum())
+        assert used <= Bp                                                  # trust-region budget
+        assert _path_objective(lt, df, u, cfg.dt, cfg.beta, pk) == ps      # Φ* exact along the path
+        results[Bp] = (u, ps)
+    # DP(B) then backtrack(B/2) == DP(B/2) then backtrack(B/2): exact-budget semantics
+    ctx.bellman(df, uo, B // 2, cfg.dt)
+    u2, ps2, _ = ctx.backtrack(B // 2)
+    assert np.array_equal(u2, results[B // 2][0]) and ps2 == results[B // 2][1]
+    if pk == P_INF:  # the collapse and the generic sweep are independent algorithms: must agree
+        ctx.set_option(native.MIOC_OPT_ALGO, native.MIOC_ALGO_GENERIC)
+        ctx.bellman(df[:, :4096], uo[:, :4096], B, cfg.dt)
+        ug, pg, _ = ctx.backtrack(B)
+        ctx.set_option(native.MIOC_OPT_ALGO, native.MIOC_ALGO_PINF)
+        ctx.bellman(df[:, :4096], uo[:, :4096], B, cfg.dt)
+        up, pp, _ = ctx.backtrack(B)
+        assert np.array_equal(ug, up) and pg == pp
+    ctx.close()
+
+
+def test_batch_device_api_equals_single():
+    import torch
+    cfg = CONFIGS["C5"]
+    K, nt, B = 6, 300, 40
+    lt = cfg.levels()
+    dfs, uos = [], []
+    for k in range(K):
+        _, df, uo = make_inputs(cfg, k=k, nt=nt, levels=lt)
+        dfs.append(df)
+        uos.append(uo)
+    for pk, algos in ((P_ONE, (native.MIOC_ALGO_GENERIC,)), (P_INF, ALGOS_PINF)):
+        for algo in algos:
+            ctx = _ctx(lt, pk, cfg.beta, algo)
+            ddf = torch.tensor(np.stack([d.T for d in dfs]), dtype=torch.float64, device="cuda")
+            duo = torch.tensor(np.stack([d.T for d in uos]), dtype=torch.float64, device="cuda")
+            du = torch.empty_like(ddf)
+            dphi = torch.empty(K, dtype=torch.float64, device="cuda")
+            dst = torch.empty(K, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            ctx.bellman_batch_device(K, ddf.data_ptr(), duo.data_ptr(), lt.M, nt, B, cfg.dt)
+            ctx.backtrack_batch_device(B // 2, du.data_ptr(), dphi.data_ptr(), dst.data_ptr())
+            ctx.synchronize()
+            ub = du.cpu().numpy()
+            for k in range(K):
+                single = _ctx(lt, pk, cfg.beta, algo)
+                single.bellman(dfs[k], uos[k], B, cfg.dt)
+                u, ps, _ = single.backtrack(B // 2)
+                assert np.array_equal(ub[k].T, u), f"k={k} pk={pk} algo={algo}"
+                assert dphi[k].item() == ps and dst[k].item() == 0
+                single.close()
+            ctx.close()
+
+
+def test_error_codes():
+    lt = LevelTable([[0, 1, 2]])
+    ctx = _ctx(lt, P_ONE, 0.1, native.MIOC_ALGO_AUTO)
+    with pytest.raises(native.MiocNativeError) as e:
+        ctx.backtrack(1)
+    assert e.value.code == native.MIOC_ESTATE
+    with pytest.raises(native.InexactError):
+        ctx.bellman(np.zeros((1, 4)), np.array([[0.0, 0.5, 1.0, 2.0]]), 3, 0.1)
+    with pytest.raises(native.MiocNativeError) as e:
+        ctx.bellman(np.array([[0.0, np.nan, 1.0, 2.0]]), np.zeros((1, 4)), 3, 0.1)
+    assert e.value.code == native.MIOC_ENONFINITE
+    with pytest.raises(native.MiocNativeError) as e:
+        ctx.bellman(np.zeros((2, 4)), np.zeros((2, 4)), 3, 0.1)
+    assert e.value.code == native.MIOC_EINVAL
+    ctx.bellman(np.ones((1, 4)), np.zeros((1, 4)), 3, 0.1)
+    with pytest.raises(native.MiocNativeError) as e:
+        ctx.backtrack(4)
+    assert e.value.code == native.MIOC_ESTATE
+    # u_old outside every level with budget 0: no finite Φ -> infeasible (the reference reads stale U)
+    ctx.bellman(np.ones((1, 4)), np.full((1, 4), 7.0), 0, 0.1)
+    with pytest.raises(native.MiocNativeError) as e:
+        ctx.backtrack(0)
+    assert e.value.code == native.MIOC_EINFEASIBLE
+    ctx.close()
+
+
+def test_trm_on_gpu_matches_trm_on_oracle():
+    """TRM driver end to end (fishing, p=Inf and doubletank-shaped p=1): GPU solver == oracle solver."""
+    import mioc
+    from mioc.ode import DTMObj, LVMObj
+    from test_host import OracleSolver
+    for cls, p, beta, D0 in ((LVMObj, math.inf, 1e-4, 2.0), (DTMObj, 1, 1e-3, 0.5)):
+        objs = [cls(nt=256), cls(nt=256)]
+        par = mioc.TRM_parameters(beta=beta, Delta0=D0, p=p, maxiter=20)
+        x0 = mioc.rand_func(objs[0], rng=11)
+        lt = LevelTable(objs[0].V, objs[0].iterator)
+        J_gpu = mioc.TRM(objs[0], par, x0=x0)
+        J_cpu = mioc.TRM(objs[1], par, x0=x0, solver=OracleSolver(lt, p, beta))
+        assert J_gpu == J_cpu
+        assert np.array_equal(objs[0].x, objs[1].x)
