@@ -221,7 +221,9 @@ int run_bellman(mioc_ctx *ctx) {
   } else {
     PinfDev &D = ctx->pinf;
     D.BW = bmax + 1;
-    const size_t kcells = K * nt * (size_t)D.BW;
+    D.BWP = 8;
+    while (D.BWP < D.BW) D.BWP *= 2;
+    const size_t kcells = K * nt * (size_t)D.BWP;
     size_t cap_km = ctx->pinf_cap_k, cap_k2 = ctx->pinf_cap_k, cap_kf = ctx->pinf_cap_k;
     int rc = grow(ctx, &D.kmin, &cap_km, kcells * sizeof(double), "class minima");
     if (!rc) rc = grow(ctx, &D.k2, &cap_k2, kcells * sizeof(double), "class second minima");

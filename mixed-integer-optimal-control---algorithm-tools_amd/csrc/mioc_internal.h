@@ -67,9 +67,10 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
 // ---- p = Inf collapse (mioc_pinf.hip) -----------------------------------------------------------
 struct PinfDev {
   int BW = 0;                      // budget classes tracked: bmax+1 <= B+1
-  double *kmin = nullptr;          // [K][nt][BW] min over ranks of class b of K_r (T1 at terminal)
-  double *k2 = nullptr;            // [K][nt][BW] second-smallest distinct value in the class
-  int32_t *kfirst = nullptr;       // [K][nt][BW] first rank attaining kmin
+  int BWP = 0;                     // padded class-row width: pow2 >= max(8, BW) (pad = +Inf / -1)
+  double *kmin = nullptr;          // [K][nt][BWP] min over ranks of class b of K_r (T1 at terminal)
+  double *k2 = nullptr;            // [K][nt][BWP] second-smallest distinct value in the class
+  int32_t *kfirst = nullptr;       // [K][nt][BWP] first rank attaining kmin
   double *R = nullptr;             // [K][nt][RP] row minima R_i[c] = min_r Φ_i[c, r]
 };
 hipError_t launch_pinf_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D);

@@ -11,7 +11,7 @@
 // fl(K_l + Φ_{i+1}[c', j]) == Φ_i[c, l]) from the class tables; a class where a second distinct K
 // could round to the same value is resolved by an exact scan of the row (counted in nfallback).
 //
-// Tables per subproblem k:  kmin/k2/kfirst [nt][BW]  (terminal row i = nt-1 holds T1 minima, no β)
+// Tables per subproblem k:  kmin/k2/kfirst [nt][BWP] (terminal row i = nt-1 holds T1 minima, no β)
 //                           R              [nt][RP]
 #include <hip/hip_runtime.h>
 
@@ -88,11 +88,12 @@ __global__ __launch_bounds__(256) void k_pinf_prep(ProblemDev P, LevelsDev Lv, P
       atomicMin(reinterpret_cast<unsigned long long *>(&sk2[b]), (unsigned long long)key);
   }
   __syncthreads();
-  const size_t row = ((size_t)k * P.nt + i) * BW;
-  for (int b = threadIdx.x; b < BW; b += blockDim.x) {
-    D.kmin[row + b] = from_okey(skmin[b]);
-    D.k2[row + b] = from_okey(sk2[b]);
-    D.kfirst[row + b] = sfirst[b] == INT_MAX ? -1 : sfirst[b];
+  const size_t row = ((size_t)k * P.nt + i) * D.BWP;
+  for (int b = threadIdx.x; b < D.BWP; b += blockDim.x) {
+    const bool in = b < BW;
+    D.kmin[row + b] = in ? from_okey(skmin[b]) : INFINITY;
+    D.k2[row + b] = in ? from_okey(sk2[b]) : INFINITY;
+    D.kfirst[row + b] = (!in || sfirst[b] == INT_MAX) ? -1 : sfirst[b];
   }
 }
 
@@ -104,66 +105,101 @@ hipError_t launch_pinf_prep(hipStream_t s, const ProblemDev &P, const LevelsDev 
 }
 
 // ---------------------------------------------------------------------------------------------
-// sequential recursion over steps, one workgroup per subproblem; R_{i+1} and the class row live in
-// LDS (double-buffered), R_i is streamed to HBM for the backtrack.
+// LDS-DMA staging helpers (global_load_lds_dwordx4: 1 KiB per wave-instruction, no VGPRs).  The
+// LDS destination is wave-uniform base + lane*16, so a linear copy maps lane i to bytes [16i, 16i+16).
 // ---------------------------------------------------------------------------------------------
-constexpr int PR_MAXPF = 4;  // prefetch registers per thread: BW <= 4 * blockDim
+__device__ __forceinline__ void glds_copy(const void *gsrc, void *ldst, int bytes, int tid, int nthreads) {
+  const int wave = tid >> 6, lane = tid & 63, nw = (nthreads + 63) >> 6;
+  for (int off = wave * 1024; off < bytes; off += nw * 1024) {
+    if (off + lane * 16 < bytes)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void *)((const char *)gsrc + off + lane * 16),
+          (__attribute__((address_space(3))) void *)((char *)ldst + off), 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-__global__ __launch_bounds__(1024) void k_pinf_recur(ProblemDev P, PinfDev D) {
+__device__ __forceinline__ double dpp_swap_pair(double x) {  // value of lane ^ 1 (quad_perm [1,0,3,2])
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// ---------------------------------------------------------------------------------------------
+// sequential recursion over steps, one workgroup per subproblem.
+//   R_i[c] = min_{b < BWP} fl(Kmin_i[b] + R_{i+1}[c - b])      (padding: Kmin = +Inf, R[<0] = +Inf)
+// Two threads per budget row c split the classes (b even-half / odd-half) and combine through DPP.
+// Class rows for CH steps at a time are staged into LDS by LDS-DMA one chunk ahead; the barrier per
+// step waits only on LDS (lgkmcnt), so the streamed R_i stores and the next chunk's DMA stay in flight.
+// ---------------------------------------------------------------------------------------------
+template <int BWP>
+__global__ __launch_bounds__(1024) void k_pinf_recur(ProblemDev P, PinfDev D, int CH) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int RP = P.RP, BW = D.BW, B = P.B, nt = P.nt, k = blockIdx.x;
-  double *Ra = sm, *Rb = sm + RP, *Ka = Rb + RP, *Kb = Ka + BW;
-  const double *kmin = D.kmin + (size_t)k * nt * BW;
+  constexpr int HB = BWP / 2;
+  const int RP = P.RP, B = P.B, nt = P.nt, k = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  double *Ra = sm, *Rb = sm + (BWP + RP), *Kbuf = Rb + (BWP + RP);  // Kbuf: [2][CH][BWP]
+  const double *kmin = D.kmin + (size_t)k * nt * BWP;
   double *R = D.R + (size_t)k * nt * RP;
-  for (int c = threadIdx.x; c < RP; c += blockDim.x) {
-    const double v = (c < BW) ? kmin[(size_t)(nt - 1) * BW + c] : INFINITY;
+  for (int c = tid; c < BWP + RP; c += nthr) {
+    const int cc = c - BWP;
+    const double v = (cc >= 0 && cc < BWP) ? kmin[(size_t)(nt - 1) * BWP + cc] : INFINITY;
     Ra[c] = v;
     Rb[c] = INFINITY;
-    R[(size_t)(nt - 1) * RP + c] = v;
+    if (cc >= 0) R[(size_t)(nt - 1) * RP + cc] = (cc <= B) ? v : INFINITY;
   }
-  if (nt >= 2)
-    for (int b = threadIdx.x; b < BW; b += blockDim.x) Ka[b] = kmin[(size_t)(nt - 2) * BW + b];
-  __syncthreads();
-  double *Rp = Ra, *Rn = Rb, *Kc = Ka, *Kn = Kb;
-  for (int i = nt - 2; i >= 0; --i) {
-    double pf[PR_MAXPF];
-    if (i >= 1) {
+  if (nt < 2) return;
+  int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
+  glds_copy(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, tid, nthr);
+  vm_drain();
+  lds_barrier();
+  double *Rp = Ra, *Rn = Rb;
+  const int h = tid & 1;
+  for (int q = 0; hi >= 0; ++q) {
+    double *Kc = Kbuf + (size_t)(q & 1) * CH * BWP;
+    const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
+    if (nhi >= 0)
+      glds_copy(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8, tid,
+                nthr);
+    for (int i = hi; i >= lo; --i) {
+      const double *Krow = Kc + (i - lo) * BWP + h * HB;
+      for (int c = tid >> 1; c < RP; c += nthr >> 1) {
+        const double *Rrow = Rp + BWP + c - h * HB;
+        double m = INFINITY;
 #pragma unroll
-      for (int q = 0; q < PR_MAXPF; ++q) {
-        const int b = threadIdx.x + q * blockDim.x;
-        pf[q] = (b < BW) ? kmin[(size_t)(i - 1) * BW + b] : INFINITY;
+        for (int j = 0; j < HB; ++j) m = fmin(m, Krow[j] + Rrow[-j]);
+        m = fmin(m, dpp_swap_pair(m));
+        if (h == 0 && c <= B) {
+          Rn[BWP + c] = m;
+          R[(size_t)i * RP + c] = m;
+        }
       }
+      lds_barrier();
+      double *t = Rp;
+      Rp = Rn;
+      Rn = t;
     }
-    for (int c = threadIdx.x; c <= B; c += blockDim.x) {
-      double m = INFINITY;
-      const int bl = c < BW - 1 ? c : BW - 1;
-      for (int b = 0; b <= bl; ++b) m = fmin(m, Kc[b] + Rp[c - b]);
-      Rn[c] = m;
-      R[(size_t)i * RP + c] = m;
-    }
-    if (i >= 1) {
-#pragma unroll
-      for (int q = 0; q < PR_MAXPF; ++q) {
-        const int b = threadIdx.x + q * blockDim.x;
-        if (b < BW) Kn[b] = pf[q];
-      }
-    }
-    __syncthreads();
-    double *t = Rp;
-    Rp = Rn;
-    Rn = t;
-    t = Kc;
-    Kc = Kn;
-    Kn = t;
+    vm_drain();
+    lds_barrier();
+    hi = nhi;
+    lo = nlo;
   }
 }
 
+int pinf_chunk_recur(int BWP) { return BWP <= 16 ? 64 : 32; }
+
 hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D) {
-  int threads = ((P.B + 1 + 63) / 64) * 64;
+  int threads = 2 * P.RP;
   if (threads > 1024) threads = 1024;
-  if (D.BW > PR_MAXPF * threads) return hipErrorInvalidValue;
-  size_t lds = (size_t)(2 * P.RP + 2 * D.BW) * sizeof(double);
-  hipLaunchKernelGGL(k_pinf_recur, dim3(P.K), dim3(threads), lds, s, P, D);
+  const int CH = pinf_chunk_recur(D.BWP);
+  size_t lds = (size_t)(2 * (D.BWP + P.RP) + 2 * CH * D.BWP) * sizeof(double);
+  switch (D.BWP) {
+    case 8: hipLaunchKernelGGL(k_pinf_recur<8>, dim3(P.K), dim3(threads), lds, s, P, D, CH); break;
+    case 16: hipLaunchKernelGGL(k_pinf_recur<16>, dim3(P.K), dim3(threads), lds, s, P, D, CH); break;
+    case 32: hipLaunchKernelGGL(k_pinf_recur<32>, dim3(P.K), dim3(threads), lds, s, P, D, CH); break;
+    case 64: hipLaunchKernelGGL(k_pinf_recur<64>, dim3(P.K), dim3(threads), lds, s, P, D, CH); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -258,174 +294,173 @@ hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev
 
 // ---------------------------------------------------------------------------------------------
 // forward walk, one wave per subproblem.  State at step i: (c, l, K_l(i), b̃_l(i), Φ_i[c, l]).
-// Lane b examines budget class b of step j = i+1: all levels of the class with K == Kmin give
-// Φ_{i+1}[c', ·] = V_b = fl(Kmin + R_{i+2}[c' - b]), the first of them is kfirst; a level with a
-// larger K gives at least fl(K2 + R_{i+2}[c' - b]).  If that second value could still satisfy
+// Lane b examines budget class b of step j = i+1: the levels of the class with K == Kmin give
+// Φ_j[c', ·] = V_b = fl(Kmin + R_{j+1}[c' - b]) and the first of them is kfirst; a level with a
+// larger K gives at least fl(K2 + R_{j+1}[c' - b]).  If that second value could still satisfy
 // fl(K_l + ·) == Φ_i[c, l], the step is resolved by an exact scan over all levels instead.
-// R rows i+2.. are prefetched into an LDS ring (state-independent), so a step costs LDS reads,
-// a few f64 ops and one wave reduction.
+// Class rows and R rows for CH steps are staged into LDS by LDS-DMA one chunk ahead, and the winner
+// is selected with a ballot + readlane (scalar), so a step costs two LDS reads and a few VALU ops.
 // ---------------------------------------------------------------------------------------------
-constexpr int PW_RING = 8;
-constexpr int PW_MAXRPL = 16;  // RP / 64 <= 16  (B < 1024)
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
 
 __global__ __launch_bounds__(64) void k_pinf_walk(ProblemDev P, LevelsDev Lv, PinfDev D, const Start *start,
-                                                  int32_t *ranks, int32_t *nfallback) {
-  extern __shared__ __attribute__((aligned(16))) double ring[];
-  const int k = blockIdx.x, lane = threadIdx.x, M = P.M, nt = P.nt, RP = P.RP, BW = D.BW;
+                                                  int32_t *ranks, int32_t *nfallback, int CH) {
+  extern __shared__ __attribute__((aligned(16))) double wsm[];
+  const int k = blockIdx.x, lane = threadIdx.x, M = P.M, nt = P.nt, RP = P.RP, BWP = D.BWP;
   const Start st = start[k];
   if (st.status != MIOC_OK) return;
   int32_t *rk = ranks + (size_t)k * nt;
   if (lane == 0) rk[0] = st.r;
   if (nt == 1) return;
+  // LDS: Rb[2][CH][RP], Km[2][CH][BWP], K2[2][CH][BWP] (doubles), Kf[2][CH][BWP] (int32)
+  double *Rb = wsm;
+  double *Km = Rb + 2 * (size_t)CH * RP;
+  double *K2 = Km + 2 * (size_t)CH * BWP;
+  int32_t *Kf = reinterpret_cast<int32_t *>(K2 + 2 * (size_t)CH * BWP);
   const double *R = D.R + (size_t)k * nt * RP;
+  const size_t crow0 = (size_t)k * nt * BWP;
   const double *dfk = P.df + (size_t)k * nt * M;
   const double *uok = P.uold + (size_t)k * nt * M;
   const double beta = Lv.beta;
-  const int rpl = RP / 64;  // R doubles per lane per row
+  const int nsteps = nt - 1;  // walk steps i = 0 .. nt-2
 
-  for (int q = 0; q < PW_RING; ++q) {
-    const int row = 2 + q;
-    if (row < nt)
-      for (int c = lane; c < RP; c += 64) ring[(row % PW_RING) * RP + c] = R[(size_t)row * RP + c];
-  }
-  // state
-  int r = st.r, c = st.c;
-  double target = st.phi;
-  double Kr, lvK;
-  int br;
+  auto stage = [&](int q, int buf) {
+    const int i0 = q * CH;
+    const int ni = (i0 + CH <= nsteps ? CH : nsteps - i0);
+    // class rows j = i0+1 .. i0+ni
+    glds_copy(D.kmin + crow0 + (size_t)(i0 + 1) * BWP, Km + (size_t)buf * CH * BWP, ni * BWP * 8, lane, 64);
+    glds_copy(D.k2 + crow0 + (size_t)(i0 + 1) * BWP, K2 + (size_t)buf * CH * BWP, ni * BWP * 8, lane, 64);
+    glds_copy(D.kfirst + crow0 + (size_t)(i0 + 1) * BWP, Kf + (size_t)buf * CH * BWP, ni * BWP * 4, lane, 64);
+    // R rows j+1 = i0+2 .. i0+ni+1 (row nt does not exist: the terminal step needs none)
+    int nr = ni;
+    if (i0 + 1 + nr > nt - 1) nr = nt - 1 - (i0 + 1);
+    if (nr > 0) glds_copy(R + (size_t)(i0 + 2) * RP, Rb + (size_t)buf * CH * RP, nr * RP * 8, lane, 64);
+  };
+
+  int r = st.r, c = st.c, br;
+  double target = st.phi, Kr;
   {
     const double *nuv = Lv.nuval + (size_t)r * M;
     Kr = p_t1(nuv, dfk, M, P.dt) + beta;
     br = p_bt(nuv, uok, M);
   }
-  (void)lvK;
-  // class row prefetch (lane b; BW <= 64)
-  const bool have_b = lane < BW;
-  size_t crow = ((size_t)k * nt + 1) * BW + lane;
-  double nkm = have_b ? D.kmin[crow] : INFINITY;
-  double nk2 = have_b ? D.k2[crow] : INFINITY;
-  int nkf = have_b ? D.kfirst[crow] : -1;
-  __syncthreads();
-
   int fallbacks = 0;
-  for (int i = 0; i + 1 < nt; ++i) {
-    const int j = i + 1;
-    const bool term = (j == nt - 1);
-    // issue the ring refill for row i+2+RING (lands in the slot row i+2 occupies now)
-    const int frow = i + 2 + PW_RING;
-    double pf[PW_MAXRPL];
-    if (frow < nt) {
-#pragma unroll
-      for (int q = 0; q < PW_MAXRPL; ++q)
-        if (q < rpl) pf[q] = R[(size_t)frow * RP + lane + 64 * q];
-    }
-    const double km = nkm, k2 = nk2;
-    const int kf = nkf;
-    if (j + 1 < nt && have_b) {  // prefetch class row j+1
-      crow += BW;
-      nkm = D.kmin[crow];
-      nk2 = D.k2[crow];
-      nkf = D.kfirst[crow];
-    }
-    const int cp = c - br;
-    int win = INT_MAX;
-    double winV = INFINITY, winK = INFINITY;
-    int winb = -1;
-    bool amb = false;
-    if (have_b && km < INFINITY) {
-      const int b = lane;
+  stage(0, 0);
+  vm_drain();
+  lds_barrier();
+  const int nq = (nsteps + CH - 1) / CH;
+  for (int q = 0; q < nq; ++q) {
+    const int buf = q & 1;
+    if (q + 1 < nq) stage(q + 1, buf ^ 1);
+    const int i0 = q * CH, i1 = (i0 + CH <= nsteps ? i0 + CH : nsteps);
+    const double *KmB = Km + (size_t)buf * CH * BWP;
+    const double *K2B = K2 + (size_t)buf * CH * BWP;
+    const int32_t *KfB = Kf + (size_t)buf * CH * BWP;
+    const double *RbB = Rb + (size_t)buf * CH * RP;
+    for (int i = i0; i < i1; ++i) {
+      const int row = i - i0, j = i + 1, cp = c - br;
+      const bool term = (j == nt - 1);
+      const bool inb = lane < BWP;
+      const double km = inb ? KmB[row * BWP + lane] : INFINITY;
       double x = INFINITY;
       if (term)
-        x = (b == cp) ? 0.0 : INFINITY;
-      else if (cp >= b)
-        x = ring[((j + 1) % PW_RING) * RP + cp - b];
-      if (x < INFINITY) {
-        const double V = term ? km : km + x;
-        if (Kr + V == target) {
-          if (k2 < INFINITY) {
-            const double V2 = term ? k2 : k2 + x;
-            if (Kr + V2 == target) amb = true;
+        x = (lane == cp) ? 0.0 : INFINITY;
+      else if (inb && lane <= cp)
+        x = RbB[(size_t)row * RP + cp - lane];
+      const bool ok = km < INFINITY && x < INFINITY;
+      const double V = term ? km : km + x;
+      const bool match = ok && (Kr + V == target);
+      const unsigned long long mm = __ballot(match);
+      bool amb = false;
+      if (match) {
+        const double k2 = K2B[row * BWP + lane];
+        amb = k2 < INFINITY && (Kr + (term ? k2 : k2 + x) == target);
+      }
+      const unsigned long long am = __ballot(amb);
+      int win, winb;
+      double winV, winK;
+      if (mm != 0 && am == 0) {
+        const int kf = inb ? KfB[row * BWP + lane] : INT_MAX;
+        winb = __builtin_ffsll((long long)mm) - 1;
+        win = __builtin_amdgcn_readlane(kf, winb);
+        for (unsigned long long rest = mm & (mm - 1); rest; rest &= rest - 1) {
+          const int l2 = __builtin_ffsll((long long)rest) - 1;
+          const int f2 = __builtin_amdgcn_readlane(kf, l2);
+          if (f2 < win) {
+            win = f2;
+            winb = l2;
           }
-          win = kf;
-          winV = V;
-          winK = km;
-          winb = b;
         }
+        winV = readlane_f64(V, winb);
+        winK = readlane_f64(km, winb);
+      } else {
+        // exact scan of row c' of Φ_j: first rank s with fl(K_l + Φ_j[c', s]) == Φ_i[c, l]
+        ++fallbacks;
+        const double *dfj = dfk + (size_t)j * M;
+        const double *uoj = uok + (size_t)j * M;
+        int sbest = INT_MAX, sb = -1;
+        double sV = INFINITY, sK = INFINITY;
+        for (int s = lane; s < Lv.L; s += 64) {
+          const double *nuv = Lv.nuval + (size_t)s * M;
+          const int bs = p_bt(nuv, uoj, M);
+          const double t1 = p_t1(nuv, dfj, M, P.dt);
+          double val = INFINITY, Ks = t1;
+          if (term) {
+            if (bs == cp) val = t1;
+          } else {
+            Ks = t1 + beta;
+            if (cp >= bs && bs < BWP) val = Ks + RbB[(size_t)row * RP + cp - bs];
+          }
+          if (val < INFINITY && Kr + val == target && s < sbest) {
+            sbest = s;
+            sV = val;
+            sK = Ks;
+            sb = bs;
+          }
+        }
+        int m2 = sbest;
+        for (int off = 32; off > 0; off >>= 1) m2 = min(m2, __shfl_xor(m2, off));
+        const unsigned long long bal = __ballot(sbest == m2 && m2 != INT_MAX);
+        if (bal == 0) {  // inconsistent tables: cannot happen for a consistent DP
+          if (lane == 0) atomicAdd(nfallback + 1, 1);
+          return;
+        }
+        const int src = __builtin_ffsll((long long)bal) - 1;
+        win = m2;
+        winV = readlane_f64(sV, src);
+        winK = readlane_f64(sK, src);
+        winb = __builtin_amdgcn_readlane(sb, src);
       }
+      if (lane == 0) rk[j] = win;
+      r = win;
+      c = cp;
+      target = winV;
+      Kr = winK;
+      br = winb;
     }
-    // wave argmin over the first rank
-    int wmin = win;
-    for (int off = 32; off > 0; off >>= 1) wmin = min(wmin, __shfl_xor(wmin, off));
-    const bool any_amb = __any(amb);
-    if (!any_amb) {
-      const unsigned long long bal = __ballot(win == wmin && wmin != INT_MAX);
-      const int src = bal ? (__ffsll((long long)bal) - 1) : 0;
-      winV = __shfl(winV, src);
-      winK = __shfl(winK, src);
-      winb = __shfl(winb, src);
-      win = wmin;
-    } else {
-      // exact scan of row c' of Φ_{j}: first rank s with fl(K_l + Φ_j[c', s]) == Φ_i[c, l]
-      ++fallbacks;
-      const double *dfj = dfk + (size_t)j * M;
-      const double *uoj = uok + (size_t)j * M;
-      int sbest = INT_MAX;
-      double sV = INFINITY, sK = INFINITY;
-      int sb = -1;
-      for (int s = lane; s < Lv.L; s += 64) {
-        const double *nuv = Lv.nuval + (size_t)s * M;
-        const int bs = p_bt(nuv, uoj, M);
-        const double t1 = p_t1(nuv, dfj, M, P.dt);
-        double val = INFINITY, Ks = t1;
-        if (term) {
-          if (bs == cp) val = t1;
-        } else {
-          Ks = t1 + beta;
-          if (cp >= bs && bs < BW) val = Ks + ring[((j + 1) % PW_RING) * RP + cp - bs];
-        }
-        if (val < INFINITY && Kr + val == target && s < sbest) {
-          sbest = s;
-          sV = val;
-          sK = Ks;
-          sb = bs;
-        }
-      }
-      int m2 = sbest;
-      for (int off = 32; off > 0; off >>= 1) m2 = min(m2, __shfl_xor(m2, off));
-      const unsigned long long bal = __ballot(sbest == m2 && m2 != INT_MAX);
-      const int src = bal ? (__ffsll((long long)bal) - 1) : 0;
-      win = m2;
-      winV = __shfl(sV, src);
-      winK = __shfl(sK, src);
-      winb = __shfl(sb, src);
-    }
-    if (win == INT_MAX) {  // cannot happen for a consistent DP; mark and stop
-      if (lane == 0) atomicAdd(nfallback + 1, 1);
-      break;
-    }
-    if (lane == 0) rk[j] = win;
-    r = win;
-    c = cp;
-    target = winV;
-    Kr = winK;
-    br = winb;
-    // complete the ring refill
-    if (frow < nt) {
-#pragma unroll
-      for (int q = 0; q < PW_MAXRPL; ++q)
-        if (q < rpl) ring[(frow % PW_RING) * RP + lane + 64 * q] = pf[q];
-    }
-    __syncthreads();
+    vm_drain();
+    lds_barrier();
   }
   (void)r;
   if (lane == 0 && fallbacks) atomicAdd(nfallback, fallbacks);
 }
 
+int pinf_chunk_walk(int RP, int BWP) {
+  const int per = RP * 8 + BWP * 20;  // bytes per staged step
+  int ch = (96 * 1024) / (2 * per);
+  return ch < 1 ? 1 : (ch > 32 ? 32 : ch);
+}
+
 hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
                             const Start *start, int32_t *ranks, int32_t *nfallback) {
-  if (D.BW > 64 || P.RP / 64 > PW_MAXRPL) return hipErrorInvalidValue;
-  size_t lds = (size_t)PW_RING * P.RP * sizeof(double);
-  hipLaunchKernelGGL(k_pinf_walk, dim3(P.K), dim3(64), lds, s, P, Lv, D, start, ranks, nfallback);
+  if (D.BWP > 64) return hipErrorInvalidValue;
+  const int CH = pinf_chunk_walk(P.RP, D.BWP);
+  size_t lds = (size_t)2 * CH * ((size_t)P.RP * 8 + (size_t)D.BWP * 20);
+  hipLaunchKernelGGL(k_pinf_walk, dim3(P.K), dim3(64), lds, s, P, Lv, D, start, ranks, nfallback, CH);
   return hipGetLastError();
 }
 

@@ -187,6 +187,10 @@ class Context:
         self._check(self.lib.mioc_bellman(self.h, _p(df), _p(u_old), nx, nt, int(B), float(dt)))
 
     def backtrack(self, B_use=None):
+        if self.nt is None:  # no DP yet: let the library report the state error (MIOC_ESTATE)
+            dummy = np.zeros(1, dtype=np.float64)
+            self._check(self.lib.mioc_backtrack(self.h, 0 if B_use is None else int(B_use), _p(dummy),
+                                                None, None))
         B_use = self.B if B_use is None else int(B_use)
         u = np.zeros((self.M, self.nt), dtype=np.float64, order="F")
         ps = ctypes.c_double(0.0)
