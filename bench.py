@@ -49,8 +49,8 @@ def candidates_per_step(levels, uo, B):
     nv = levels.nuval
     tot = 0
     nt = uo.shape[1]
-    for s in range(0, nt - 1, 2048):
-        e = min(nt - 1, s + 2048)
+    for s in range(0, nt - 1, 512):
+        e = min(nt - 1, s + 512)
         bt = np.abs(nv[:, :, None] - uo[None, :, s:e]).sum(axis=1)  # L x steps
         tot += np.maximum(0, B + 1 - bt).sum()
     return levels.L * tot / max(1, nt - 1)
@@ -158,6 +158,17 @@ def roofline_of(res, args):
         roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
                      "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
                      "candidates_per_launch": ncand}
+    elif res["dom_name"] == "k_pyr_step":
+        # the same algorithmic traffic as the reference DP step: front in + front out + compact U
+        bytes_per_launch = K * (B + 1) * L * (8 + 8 + 2)
+        M = lv.M
+        smax = int(sum(max(v) - min(v) for v in lv.nu))
+        ops = 1.0 * K * (B + 1) * L * (smax + 1) * (2 * M + 2)  # upper bound: every level, 2M min + 2 add
+        ncand = K * candidates_per_step(lv, res["uo"], B)
+        roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
+                     "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
+                     "note": "pyramid ops upper bound (all levels); brute-force-equivalent candidates/s "
+                             f"= {ncand / avg_s:.4g}"}
     else:
         # k_pinf_recur: one launch per subproblem batch; reads the class table, writes R rows
         bw = int(min(B, sum(max(v) - min(v) for v in lv.nu))) + 1
@@ -251,7 +262,8 @@ def main():
 
 
 def native_name(algo):
-    return {1: "generic min-plus sweep", 2: "p=Inf exact collapse"}.get(algo, str(algo))
+    return {1: "generic min-plus sweep", 2: "p=Inf exact collapse", 3: "p=1 exact L1-ball pyramid"}.get(algo,
+                                                                                                  str(algo))
 
 
 if __name__ == "__main__":

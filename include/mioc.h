@@ -48,9 +48,11 @@ extern "C" {
 
 /* ---- algorithm selection (mioc_set_option(MIOC_OPT_ALGO, ...)) ----------------------------- */
 #define MIOC_OPT_ALGO 1
-#define MIOC_ALGO_AUTO 0    /* p=Inf -> class collapse, otherwise the generic min-plus sweep */
+#define MIOC_ALGO_AUTO 0    /* p=Inf -> class collapse; p=1 on a large product grid -> pyramid;
+                               otherwise the generic min-plus sweep */
 #define MIOC_ALGO_GENERIC 1 /* per-step min-plus sweep over every (c, l, j): any p */
 #define MIOC_ALGO_PINF 2    /* exact p=Inf collapse onto per-budget row minima */
+#define MIOC_ALGO_PYRAMID 3 /* p=1 on product grids of consecutive levels: exact L1-ball pyramid */
 #define MIOC_OPT_TIMING 2   /* 1: record HIP events around the dominant kernel (mioc_kernel_stats) */
 
 typedef struct mioc_ctx mioc_ctx;
@@ -126,8 +128,15 @@ int32_t mioc_kernel_stats(mioc_ctx *ctx, int32_t which, double *total_ms, int64_
                           const char **name);
 int32_t mioc_reset_stats(mioc_ctx *ctx);
 
-/* Which algorithm served the last mioc_bellman* call (MIOC_ALGO_GENERIC / MIOC_ALGO_PINF). */
+/* Which algorithm served the last mioc_bellman* call (MIOC_ALGO_GENERIC / _PINF / _PYRAMID). */
 int32_t mioc_last_algo(mioc_ctx *ctx);
+
+/*
+ * Diagnostics of the last bellman/backtrack: counters[0] rows resolved by the exact scan (pyramid: rows
+ * whose values are not pairwise separated), [1] targets resolved by the exact scan (minimum reached at two
+ * levels), [2] p=Inf walk steps resolved by the exact scan, [3] internal consistency failures (must be 0).
+ */
+int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n);
 
 #ifdef __cplusplus
 }

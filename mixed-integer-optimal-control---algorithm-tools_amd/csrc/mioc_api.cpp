@@ -87,7 +87,7 @@ void free_all(mioc_ctx *ctx) {
                   ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
-                  ctx->d_status_own};
+                  ctx->d_status_own, ctx->d_stage,    ctx->d_counters};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (ctx->h_flags) hipHostFree(ctx->h_flags);
@@ -196,14 +196,39 @@ int run_bellman(mioc_ctx *ctx) {
   const int bmax = ctx->h_flags[1];
 
   int algo = (int)ctx->opt_algo;
-  const bool pinf_ok = ctx->p_kind == MIOC_P_INF && bmax + 1 <= 64 && ctx->RP / 64 <= 16;
-  if (algo == MIOC_ALGO_AUTO) algo = pinf_ok ? MIOC_ALGO_PINF : MIOC_ALGO_GENERIC;
+  const bool pinf_ok = ctx->p_kind == MIOC_P_INF && bmax + 1 <= 64;
+  const bool pyr_ok = ctx->p_kind == MIOC_P_ONE && ctx->pyr_ok;
+  if (algo == MIOC_ALGO_AUTO)
+    algo = pinf_ok ? MIOC_ALGO_PINF : (pyr_ok && ctx->L >= 256 ? MIOC_ALGO_PYRAMID : MIOC_ALGO_GENERIC);
   if (algo == MIOC_ALGO_PINF && !pinf_ok)
-    return fail(ctx, MIOC_EINVAL, "p=Inf collapse needs p_kind MIOC_P_INF, <= 64 budget classes and B < 1024");
+    return fail(ctx, MIOC_EINVAL, "p=Inf collapse needs p_kind MIOC_P_INF and <= 64 budget classes");
+  if (algo == MIOC_ALGO_PYRAMID && !pyr_ok)
+    return fail(ctx, MIOC_EINVAL, "the L1-ball pyramid needs p = 1 and a product grid of consecutive integer "
+                                  "levels (first dimension <= 8 levels, <= 4096 tuples)");
+  if (!ctx->d_counters) {
+    size_t cc = 0;
+    int rc0 = grow(ctx, &ctx->d_counters, &cc, 8 * sizeof(int32_t), "counters");
+    if (rc0) return rc0;
+  }
+  HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(int32_t), ctx->stream));
   ctx->algo = algo;
   const size_t K = (size_t)ctx->K, nt = (size_t)ctx->nt, L = (size_t)ctx->L, RP = (size_t)ctx->RP;
 
-  if (algo == MIOC_ALGO_GENERIC) {
+  if (algo == MIOC_ALGO_PYRAMID) {
+    const size_t s_stride = (size_t)(ctx->B + 1) * L;
+    int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, 2 * K * s_stride * sizeof(double), "staging fronts");
+    if (rc) return rc;
+    const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
+    rc = grow(ctx, &ctx->d_U, &ctx->U_cap, K * uu_stride_k * sizeof(uint16_t), "argmin table U");
+    if (rc) return rc;
+    double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
+    HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, st[(nt - 1) & 1], s_stride));
+    ev_begin(ctx, 0, "k_pyr_step");
+    for (int i = ctx->nt - 2; i >= 0; --i)
+      HIP_TRY(ctx, launch_pyr_step(ctx->stream, P, Lv, ctx->pyr, i, st[(i + 1) & 1], st[i & 1],
+                                   (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters));
+    ev_end(ctx, 0, ctx->nt - 1);
+  } else if (algo == MIOC_ALGO_GENERIC) {
     ctx->ubytes = L <= 256 ? 1 : 2;
     const size_t front_stride = L * RP;
     int rc = grow(ctx, &ctx->d_front, &ctx->front_cap, 2 * K * front_stride * sizeof(double), "value fronts");
@@ -258,7 +283,15 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
   if (K > 4096) return fail(ctx, MIOC_EINVAL, "batch larger than 4096 subproblems");
   int rc = grow(ctx, &ctx->d_ranks, &ctx->ranks_cap, K * nt * sizeof(int32_t), "rank path");
   if (rc) return rc;
-  if (ctx->algo == MIOC_ALGO_GENERIC) {
+  if (ctx->algo == MIOC_ALGO_PYRAMID) {
+    const size_t s_stride = (size_t)(ctx->B + 1) * ctx->L;
+    const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
+    HIP_TRY(ctx, launch_stage_argmin0(ctx->stream, P, Lv, ctx->d_stage, s_stride, (int)B_use, ctx->d_start));
+    ev_begin(ctx, 1, "k_stage_walk");
+    HIP_TRY(ctx, launch_stage_walk(ctx->stream, P, Lv, (const uint16_t *)ctx->d_U, uu_stride_k, ctx->d_start,
+                                   ctx->d_ranks));
+    ev_end(ctx, 1, 1);
+  } else if (ctx->algo == MIOC_ALGO_GENERIC) {
     const size_t front_stride = (size_t)ctx->L * ctx->RP;
     const size_t u_stride_k = (nt > 1 ? nt - 1 : 1) * (size_t)ctx->L * (size_t)(ctx->B + 1);
     HIP_TRY(ctx, launch_generic_argmin0(ctx->stream, P, Lv, ctx->d_front, front_stride, (int)B_use, ctx->d_start));
@@ -350,7 +383,7 @@ const char *mioc_last_error(const mioc_ctx *ctx) { return ctx ? ctx->err.c_str()
 int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   if (!ctx) return MIOC_EINVAL;
   if (option == MIOC_OPT_ALGO) {
-    if (value < MIOC_ALGO_AUTO || value > MIOC_ALGO_PINF) return fail(ctx, MIOC_EINVAL, "unknown algorithm");
+    if (value < MIOC_ALGO_AUTO || value > MIOC_ALGO_PYRAMID) return fail(ctx, MIOC_EINVAL, "unknown algorithm");
     ctx->opt_algo = value;
     return MIOC_OK;
   }
@@ -423,6 +456,29 @@ int32_t mioc_set_levels(mioc_ctx *ctx, int64_t M, const int64_t *counts, const i
   HIP_TRY(ctx, hipMemcpy(ctx->d_gidx, gidx.data(), L * sizeof(int32_t), hipMemcpyHostToDevice));
   HIP_TRY(ctx, hipMemcpy(ctx->d_numin, ctx->numin_h.data(), M * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(ctx, hipMemcpy(ctx->d_numax, ctx->numax_h.data(), M * sizeof(double), hipMemcpyHostToDevice));
+  // pyramid domain: product iterator in grid order, consecutive integer levels, dim 0 <= 8 levels
+  {
+    bool ok = L == Lgrid && L <= 4096 && M >= 2 && M <= 6 && (counts[0] == 8 || counts[0] == 4) &&
+              Lgrid / counts[0] <= 512;
+    for (int64_t r = 0; ok && r < L; ++r) ok = gidx[r] == r;
+    for (int64_t m = 0; ok && m < M; ++m)
+      for (int64_t q = 0; ok && q < counts[m]; ++q) ok = values[off[m] + q] == values[off[m]] + q;
+    ctx->pyr_ok = ok;
+    mioc::PyrGeom G;
+    G.M = (int)M;
+    G.ncol = (int)(Lgrid / counts[0]);
+    int cs = 1;
+    for (int64_t m = 0; m < M; ++m) {
+      G.n[m] = (int)counts[m];
+      G.base[m] = (int)values[off[m]];
+      G.Smax += (int)counts[m] - 1;
+      if (m >= 1) {
+        G.cstride[m] = cs;
+        cs *= (int)counts[m];
+      }
+    }
+    ctx->pyr = G;
+  }
   ctx->have_levels = true;
   ctx->have_dp = false;
   return build_cost_tables(ctx);
@@ -550,5 +606,17 @@ int32_t mioc_reset_stats(mioc_ctx *ctx) {
 }
 
 int32_t mioc_last_algo(mioc_ctx *ctx) { return ctx ? ctx->algo : MIOC_EINVAL; }
+
+int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
+  if (!ctx || !counters || n < 0) return MIOC_EINVAL;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  int32_t c[4] = {0, 0, 0, 0}, f[4] = {0, 0, 0, 0};
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->d_counters) HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
+  HIP_TRY(ctx, hipMemcpy(f, ctx->d_flags, sizeof f, hipMemcpyDeviceToHost));
+  const int64_t all[4] = {c[0], c[1], f[2], f[3]};
+  for (int32_t q = 0; q < n && q < 4; ++q) counters[q] = all[q];
+  return MIOC_OK;
+}
 
 }  // extern "C"

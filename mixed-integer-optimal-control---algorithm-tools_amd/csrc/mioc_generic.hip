@@ -415,4 +415,76 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// staging layout (pyramid path): Φ_0[l, c] = S_0[c - b̃_l(0)][l],  U_i[l, c] = UU_i[c - b̃_l(i)][l]
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_stage_argmin0(ProblemDev P, LevelsDev Lv, const double *S0_all,
+                                                        size_t s_stride, int Bu, Start *start) {
+  const int k = blockIdx.x, L = Lv.L, M = P.M;
+  const double *S0 = S0_all + (size_t)k * s_stride;
+  const double *uo0 = P.uold + (size_t)k * P.nt * M;
+  ArgKey best;
+  best.v = ~0ull;
+  best.pos = ~0ull;
+  best.val = INFINITY;
+  best.r = -1;
+  best.c = 0;
+  for (int r = threadIdx.x; r < L; r += blockDim.x) {
+    const int b = bt_of(Lv.nuval + (size_t)r * M, uo0, M);
+    for (int c = b; c <= Bu; ++c) {  // first minimum over c for this l, then (value, grid index, c)
+      const double v = S0[(size_t)(c - b) * L + r];
+      ArgKey a;
+      a.v = jl_key(v);
+      a.pos = ((uint64_t)(uint32_t)Lv.gidx[r] << 32) | (uint32_t)c;
+      a.val = v;
+      a.r = r;
+      a.c = c;
+      if (key_less(a, best)) best = a;
+    }
+  }
+  best = block_argmin(best);
+  if (threadIdx.x == 0) {
+    Start st;
+    st.phi = best.val;
+    st.c = best.c;
+    st.r = best.r;
+    st.status = (best.r >= 0 && best.val < INFINITY) ? MIOC_OK : MIOC_EINFEASIBLE;
+    st.pad = 0;
+    start[k] = st;
+  }
+}
+
+hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const double *S0,
+                                size_t s_stride, int Bu, Start *start) {
+  hipLaunchKernelGGL(k_stage_argmin0, dim3(P.K), dim3(1024), 0, s, P, Lv, S0, s_stride, Bu, start);
+  return hipGetLastError();
+}
+
+__global__ void k_stage_walk(ProblemDev P, LevelsDev Lv, const uint16_t *__restrict__ UU, size_t uu_stride_k,
+                             const Start *start, int32_t *ranks) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= P.K) return;
+  const Start st = start[k];
+  int32_t *rk = ranks + (size_t)k * P.nt;
+  if (st.status != MIOC_OK) return;
+  int r = st.r, c = st.c;
+  rk[0] = r;
+  const uint16_t *Uk = UU + (size_t)k * uu_stride_k;
+  const size_t step = (size_t)(P.B + 1) * Lv.L;
+  for (int i = 0; i + 1 < P.nt; ++i) {
+    const double *uoi = P.uold + ((size_t)k * P.nt + i) * P.M;
+    const int b = bt_of(Lv.nuval + (size_t)r * P.M, uoi, P.M);
+    const int s = (int)Uk[(size_t)i * step + (size_t)(c - b) * Lv.L + r];
+    c -= b;
+    r = s;
+    rk[i + 1] = r;
+  }
+}
+
+hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,
+                             size_t uu_stride_k, const Start *start, int32_t *ranks) {
+  hipLaunchKernelGGL(k_stage_walk, dim3((P.K + 63) / 64), dim3(64), 0, s, P, Lv, UU, uu_stride_k, start, ranks);
+  return hipGetLastError();
+}
+
 }  // namespace mioc

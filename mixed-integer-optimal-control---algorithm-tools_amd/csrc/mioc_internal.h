@@ -41,6 +41,16 @@ struct ProblemDev {
   const double *uold = nullptr;    // [K][nt][M]
 };
 
+// Product grid with consecutive integer levels per dimension (the L1-ball pyramid's domain).
+struct PyrGeom {
+  int M = 0;
+  int ncol = 0;                    // grid columns: L / n[0]
+  int Smax = 0;                    // largest L1 distance: sum_m (n_m - 1)
+  int n[kMaxM] = {};               // levels per dimension
+  int base[kMaxM] = {};            // first level value per dimension
+  int cstride[kMaxM] = {};         // column-index stride of dimension m >= 1
+};
+
 struct Start {                      // backtrack start cell per subproblem
   double phi;
   int32_t c;
@@ -63,6 +73,17 @@ hipError_t launch_generic_walk(hipStream_t s, const ProblemDev &P, const LevelsD
                                size_t u_stride_k, const Start *start, int32_t *ranks);
 hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const Start *start,
                          const int32_t *ranks, double *u_out, double *phi_star, int32_t *status);
+
+// ---- L1-ball pyramid (mioc_pyramid.hip) + staging-layout backtrack (mioc_generic.hip) -------------
+hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, double *S, size_t s_stride);
+hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
+                           const double *Sin, double *Sout, uint16_t *UU, size_t s_stride, size_t uu_stride_k,
+                           int32_t *counters);
+size_t pyr_lds_bytes(const PyrGeom &G);
+hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const double *S0,
+                                size_t s_stride, int Bu, Start *start);
+hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,
+                             size_t uu_stride_k, const Start *start, int32_t *ranks);
 
 // ---- p = Inf collapse (mioc_pinf.hip) -----------------------------------------------------------
 struct PinfDev {
@@ -121,6 +142,13 @@ struct mioc_ctx {
   int algo = 0;
   int K = 0, nt = 0, B = 0, RP = 0;
   double dt = 0.0;
+
+  // pyramid (p = 1, product grid, unit gaps)
+  bool pyr_ok = false;
+  mioc::PyrGeom pyr;
+  double *d_stage = nullptr;       // [2][K][B+1][L] source-row-major fronts
+  size_t stage_cap = 0;
+  int32_t *d_counters = nullptr;   // [8] diagnostics: dirty rows, multi-level targets, ...
 
   // generic buffers
   double *d_front = nullptr;       // [2][K][L][RP]

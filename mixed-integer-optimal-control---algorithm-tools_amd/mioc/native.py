@@ -27,13 +27,13 @@ MIOC_ENONFINITE = -7
 
 MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
 MIOC_OPT_ALGO, MIOC_OPT_TIMING = 1, 2
-MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF = 0, 1, 2
+MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID = 0, 1, 2, 3
 
 EXPORTED = [
     "mioc_version", "mioc_create", "mioc_destroy", "mioc_last_error", "mioc_set_option", "mioc_set_levels",
     "mioc_set_cost", "mioc_bellman", "mioc_backtrack", "mioc_bellman_batch_device",
     "mioc_backtrack_batch_device", "mioc_synchronize", "mioc_stream", "mioc_kernel_stats",
-    "mioc_reset_stats", "mioc_last_algo",
+    "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics",
 ]
 
 
@@ -55,7 +55,7 @@ def load_library(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("MIOC_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise MiocNativeError(MIOC_EHIP, f"HIP library not built: {p} (run __graft_entry__.build())")
     # One HIP runtime per process: torch ships its own libamdhip64.so (soname libamdhip64.so.7).
@@ -85,6 +85,7 @@ def load_library(path=None):
                                     ctypes.POINTER(ctypes.c_char_p)]),
         "mioc_reset_stats": (i32, [vp]),
         "mioc_last_algo": (i32, [vp]),
+        "mioc_diagnostics": (i32, [vp, vp, i32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -229,3 +230,21 @@ class Context:
 
     def last_algo(self):
         return self.lib.mioc_last_algo(self.h)
+
+    def diagnostics(self):
+        """[rows resolved by exact scan, targets resolved by exact scan, p=Inf walk fallbacks, errors]."""
+        out = np.zeros(4, dtype=np.int64)
+        self._check(self.lib.mioc_diagnostics(self.h, _p(out), 4))
+        return out.tolist()
+
+
+def pyramid_eligible(levels: LevelTable):
+    """Mirror of the library's L1-ball pyramid domain test (mioc_set_levels)."""
+    if levels.L != int(np.prod(levels.counts)) or not (2 <= levels.M <= 6) or levels.L > 4096:
+        return False
+    if int(levels.counts[0]) not in (4, 8) or levels.L // int(levels.counts[0]) > 512:
+        return False
+    strides = np.cumprod(np.concatenate([[1], levels.counts[:-1]]))
+    if not np.array_equal(((levels.tuples - 1) * strides).sum(axis=1), np.arange(levels.L)):
+        return False
+    return all(list(v) == list(range(v[0], v[0] + len(v))) for v in levels.nu)

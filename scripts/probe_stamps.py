@@ -1,0 +1,31 @@
+"""Phase timing of the pyramid kernel (diagnostic build libmioc_stamps.so, s_memtime per workgroup)."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")
+os.environ["MIOC_LIB"] = os.path.join(PKG, "lib", "libmioc_stamps.so")
+sys.path.insert(0, PKG); sys.path.insert(0, ROOT)
+import numpy as np
+from mioc import native
+from mioc.synth import CONFIGS, make_inputs
+nt = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+cfg = CONFIGS["C4"]
+lt, df, uo = make_inputs(cfg, nt=nt)
+ctx = native.Context(0); ctx.set_levels(lt); ctx.set_cost(1, cfg.beta); ctx.set_option(native.MIOC_OPT_ALGO, 3)
+ctx.bellman(df, uo, cfg.B, cfg.dt)
+nb = cfg.B + 1
+buf = (ctypes.c_ulonglong * (nb * 8))()
+lib = native.load_library()
+f = lib.mioc_debug_pyr_stamps; f.argtypes = [ctypes.c_void_p, ctypes.c_int64]; f.restype = ctypes.c_int32
+assert f(buf, nb) == 0
+st = np.array(buf, dtype=np.int64).reshape(nb, 8)
+names = ["load+T1 (0->1)", "reductions (1->2)", "hash+dirty (2->3)", "pyramid (3->4)", "lookup+store (4->5)"]
+full = st[:, 5] > 0
+print("blocks with all stamps:", full.sum(), "of", nb)
+s = st[full]
+for k, nm in enumerate(names):
+    d = s[:, k + 1] - s[:, k]
+    print(f"{nm:22s} cycles median {np.median(d):9.0f}  p90 {np.percentile(d, 90):9.0f}  max {d.max():9.0f}")
+tot = s[:, 5] - s[:, 0]
+print(f"{'total':22s} cycles median {np.median(tot):9.0f}  max {tot.max():9.0f}")
+print("levels executed: median", np.median(s[:, 6]), "max", s[:, 6].max(), "min", s[:, 6].min())
+print("start skew (cycles): ", (st[:, 0] - st[:, 0].min()).max(), " end spread:", (s[:, 5].max() - st[:, 0].min()))

@@ -34,8 +34,12 @@ def _oracle_levels(lt):
     return Levels(lt.nu, [tuple(int(x) for x in t) for t in lt.tuples])
 
 
-def _algos(p_kind):
-    return ALGOS_PINF if p_kind == P_INF else (native.MIOC_ALGO_GENERIC,)
+def _algos(p_kind, lt=None):
+    if p_kind == P_INF:
+        return ALGOS_PINF
+    if p_kind == P_ONE and lt is not None and native.pyramid_eligible(lt):
+        return (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID)
+    return (native.MIOC_ALGO_GENERIC,)
 
 
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
@@ -43,7 +47,7 @@ def test_golden_fixtures(path):
     g = load_golden(path)
     lt = LevelTable(g["nu"], g["tuple_list"])
     table = g["wtab"] if g["wtab"].size else None
-    for algo in _algos(g["p_kind"]):
+    for algo in _algos(g["p_kind"], lt):
         ctx = _ctx(lt, g["p_kind"], g["beta"], algo, p_int=g["p_int"], table=table)
         ctx.bellman(g["df"], g["u_old"], g["B"], g["dt"])
         assert ctx.last_algo() == algo
@@ -57,7 +61,9 @@ def test_golden_fixtures(path):
 def _random_case(seed):
     rng = np.random.default_rng(1000 + seed)
     shapes = [([[0, 1]] * 3, "sos1"), ([[0, 1, 2], [0, 1]], "prod"), ([[-2, 0, 3]], "prod"),
-              ([list(range(4))] * 2, "prod"), ([[0, 1]] * 4, "prod"), ([list(range(6))] * 2, "prod")]
+              ([list(range(4))] * 2, "prod"), ([[0, 1]] * 4, "prod"), ([list(range(6))] * 2, "prod"),
+              ([list(range(8)), list(range(-1, 3))], "prod"), ([list(range(4))] * 3, "prod"),
+              ([list(range(8))] * 2, "prod")]
     nu, kind = shapes[seed % len(shapes)]
     lv = Levels.product(nu) if kind == "prod" else Levels.bounded_sum(nu, 1, 1)
     n = int(rng.integers(1, 40))
@@ -73,7 +79,7 @@ def _random_case(seed):
     return lv, df, uo, B, rng
 
 
-@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("seed", range(72))
 def test_random_vs_oracle(oracle_c, seed):
     lv, df, uo, B, rng = _random_case(seed)
     pk = [P_ONE, P_INF][seed % 2]
@@ -82,7 +88,7 @@ def test_random_vs_oracle(oracle_c, seed):
     phi, U = oracle_c.bellman(lv, df, uo, B, pk, beta, dt)
     lt = LevelTable(lv.nu, [tuple(t) for t in lv.tuples])
     budgets = sorted({B, B // 2, 0, int(rng.integers(0, B + 1))})
-    for algo in _algos(pk):
+    for algo in _algos(pk, lt):
         ctx = _ctx(lt, pk, beta, algo)
         ctx.bellman(df, uo, B, dt)
         for Bp in budgets:  # one DP, several budgets: the halving reuse of multi-trust.jl:108-110
@@ -275,3 +281,48 @@ def test_trm_on_gpu_matches_trm_on_oracle():
         J_cpu = mioc.TRM(objs[1], par, x0=x0, solver=OracleSolver(lt, p, beta))
         assert J_gpu == J_cpu
         assert np.array_equal(objs[0].x, objs[1].x)
+
+
+@pytest.mark.parametrize("mode", ["gauss", "integer", "zero", "dyadic"])
+def test_pyramid_vs_oracle_512_levels(oracle_c, mode):
+    """8x8x8 product grid, p=1: clean rows (pyramid + value lookup) and dirty rows (exact scan)."""
+    rng = np.random.default_rng({"gauss": 1, "integer": 2, "zero": 3, "dyadic": 4}[mode])
+    lv = Levels.product([list(range(8))] * 3)
+    lt = LevelTable(lv.nu, [tuple(t) for t in lv.tuples])
+    n, B = 12, 20
+    if mode == "gauss":
+        df = rng.standard_normal((3, n))
+    elif mode == "integer":
+        df = rng.integers(-3, 4, size=(3, n)).astype(float)
+    elif mode == "zero":
+        df = np.zeros((3, n))
+    else:
+        df = rng.integers(-64, 65, size=(3, n)) / 64.0
+    uo = np.array([lv.nuval[rng.integers(lv.L)] for _ in range(n)], dtype=np.float64).T
+    beta, dt = (0.125, 0.25) if mode != "gauss" else (1e-3, 2.0 ** -10)
+    phi, U = oracle_c.bellman(lv, df, uo, B, P_ONE, beta, dt)
+    ctx = _ctx(lt, P_ONE, beta, native.MIOC_ALGO_PYRAMID)
+    ctx.bellman(df, uo, B, dt)
+    diag = ctx.diagnostics()
+    for Bp in (B, B // 2, 3):
+        ou, ops = oracle_c.backtrack(lv, uo, phi, U, B, Bp)
+        u, ps, _ = ctx.backtrack(Bp)
+        assert np.array_equal(u, ou), f"{mode} Bp={Bp} diag={diag}"
+        assert ps == ops
+    if mode in ("integer", "zero"):
+        assert diag[0] > 0  # the exact-scan path for rows with tied values was exercised
+    ctx.close()
+
+
+def test_pyramid_equals_generic_at_c4_scale():
+    """4096 levels, B=256, p=1: the pyramid and the generic sweep are independent algorithms."""
+    cfg = CONFIGS["C4"]
+    lt, df, uo = make_inputs(cfg, nt=48)
+    out = {}
+    for algo in (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID):
+        ctx = _ctx(lt, P_ONE, cfg.beta, algo)
+        ctx.bellman(df, uo, cfg.B, cfg.dt)
+        out[algo] = [ctx.backtrack(Bp)[:2] for Bp in (cfg.B, 100, 7)]
+        ctx.close()
+    for (ug, pg), (up, pp) in zip(out[native.MIOC_ALGO_GENERIC], out[native.MIOC_ALGO_PYRAMID]):
+        assert np.array_equal(ug, up) and pg == pp
