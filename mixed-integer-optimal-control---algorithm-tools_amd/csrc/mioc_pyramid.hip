@@ -27,10 +27,10 @@
 namespace mioc {
 
 constexpr int PY_T = 512;          // threads per workgroup: one grid column (dim-0 run) per thread
-constexpr int PY_CPT = 1;          // grid columns per thread
-constexpr int PY_HBITS = 13;
-constexpr int PY_HSIZE = 1 << PY_HBITS;
-constexpr long long PY_EMPTY = 0x7FFFFFFFFFFFFFFFLL;
+constexpr int PY_NW = PY_T / 64;   // waves per workgroup
+constexpr int PY_HS = 12288;       // hash slots (uint32): <= 4096 sources, load <= 1/3
+constexpr int PY_G = 8;            // bucket width = 2^PY_G · δ
+constexpr unsigned PY_RB = 13;     // hash entry = tag << PY_RB | (rank + 1); 0 = empty
 
 // v_min_f64 without the sNaN-quieting v_max_f64 x,x that llvm.minnum puts in front of every operand
 // not known to be canonical (inputs here are finite or +Inf, never NaN)
@@ -53,58 +53,31 @@ __device__ unsigned long long g_pyr_stamps[4096][8];
   } while (0)
 #endif
 
-struct PyrView {
-  double *lvl;        // [2][ncol][8]
-  long long *hkey;    // [PY_HSIZE]
-  uint16_t *hval;     // [PY_HSIZE]
-};
-
-__device__ __forceinline__ unsigned py_hash(long long q) {
-  return (unsigned)(((unsigned long long)q * 0x9E3779B97F4A7C15ull) >> (64 - PY_HBITS));
+// Bucket hash.  A bucket is an integer-valued double fq = floor(Ψ·2^k) (+0.0, so -0 and +0 agree); the
+// slot comes from the high bits of a 32-bit mix of its bit pattern, a 19-bit tag from the low bits.
+// A tag match is confirmed against the exact bucket kept per rank in LDS (keyarr), so false matches
+// only cost a probe.
+__device__ __forceinline__ void py_hslot(double fq, unsigned &slot, unsigned &tag) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(fq);
+  unsigned h = (unsigned)u * 0x9E3779B1u + (unsigned)(u >> 32) * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  slot = __umulhi(h, (unsigned)PY_HS);
+  tag = h & ((1u << (32 - PY_RB)) - 1);
 }
+__device__ __forceinline__ unsigned py_next(unsigned s) { return s + 1 == (unsigned)PY_HS ? 0u : s + 1; }
 
-// returns true if q was already present (a duplicate bucket)
-__device__ __forceinline__ bool py_insert(PyrView V, long long q, int rank) {
-  unsigned s = py_hash(q);
+// rank holding bucket fq, or -1
+__device__ __forceinline__ int py_find(const unsigned *htab, const double *keyarr, double fq) {
+  unsigned s, tag;
+  py_hslot(fq, s, tag);
   for (;;) {
-    unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long *>(&V.hkey[s]),
-                                       (unsigned long long)PY_EMPTY, (unsigned long long)q);
-    if (old == (unsigned long long)PY_EMPTY) {
-      V.hval[s] = (uint16_t)rank;
-      return false;
-    }
-    if ((long long)old == q) return true;
-    s = (s + 1) & (PY_HSIZE - 1);
+    const unsigned e = htab[s];
+    if (e == 0u) return -1;
+    if ((e >> PY_RB) == tag && keyarr[(e & ((1u << PY_RB) - 1)) - 1] == fq) return (int)(e & ((1u << PY_RB) - 1)) - 1;
+    s = py_next(s);
   }
-}
-
-__device__ __forceinline__ int py_find(PyrView V, long long q) {
-  unsigned s = py_hash(q);
-  for (;;) {
-    const long long k = V.hkey[s];
-    if (k == q) return V.hval[s];
-    if (k == PY_EMPTY) return -1;
-    s = (s + 1) & (PY_HSIZE - 1);
-  }
-}
-
-__device__ __forceinline__ double py_block_max(double v, double *red) {
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double r = red[0];
-  for (int w = 1; w < PY_T / 64; ++w) r = fmax(r, red[w]);
-  __syncthreads();
-  return r;
-}
-__device__ __forceinline__ double py_block_min(double v, double *red) {
-  for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double r = red[0];
-  for (int w = 1; w < PY_T / 64; ++w) r = fmin(r, red[w]);
-  __syncthreads();
-  return r;
 }
 
 struct PyrDims {  // geometry copied by value into registers (never escapes to memory)
@@ -174,29 +147,36 @@ __device__ __forceinline__ void col_store(double *buf, int col, const double *v)
   for (int c = 0; c < N0 / 2; ++c) base[c ^ sw] = make_double2(v[2 * c], v[2 * c + 1]);
 }
 template <int N0>
-__device__ __forceinline__ void col_min(const double *buf, int col, double *acc) {
+__device__ __forceinline__ void col_load(const double *buf, int col, double2 *t) {
   const double2 *base = reinterpret_cast<const double2 *>(buf + (size_t)col * N0);
   const int sw = col_swz<N0>(col);
 #pragma unroll
-  for (int c = 0; c < N0 / 2; ++c) {
-    const double2 t = base[c ^ sw];
-    acc[2 * c] = vmin(acc[2 * c], t.x);
-    acc[2 * c + 1] = vmin(acc[2 * c + 1], t.y);
-  }
+  for (int c = 0; c < N0 / 2; ++c) t[c] = base[c ^ sw];
+}
+
+// workgroup-wide OR of one flag per thread: wave ballot, one LDS word per wave, one barrier
+__device__ __forceinline__ bool py_any(bool f, int *slots) {
+  const unsigned long long bal = __ballot(f);
+  if ((threadIdx.x & 63) == 0) slots[threadIdx.x >> 6] = bal != 0ull;
+  __syncthreads();
+  int r = 0;
+#pragma unroll
+  for (int w = 0; w < PY_NW; ++w) r |= slots[w];
+  return r != 0;
 }
 
 template <int M, int N0>
-__global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i,
+__global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i, int early_exit,
                                                    const double *__restrict__ Sin_all, double *__restrict__ Sout_all,
                                                    uint16_t *__restrict__ UU_all, size_t s_stride, size_t uu_stride_k,
                                                    int32_t *__restrict__ counters) {
   static_assert(N0 == 4 || N0 == 8, "column length");
-  constexpr int CW = N0;                 // doubles per column in LDS
-  constexpr int NP = PY_CPT * N0;        // points per thread
+  static_assert(M >= 2, "product grid");
   extern __shared__ __attribute__((aligned(16))) unsigned char pys[];
-  __shared__ double red[PY_T / 64];
-  __shared__ double sc[64];              // costlut (β·S), S <= Smax < 64
-  __shared__ int vote[2][PY_T / 64];     // per-wave early-exit votes, double-buffered by level parity
+  __shared__ double red[2][PY_NW];
+  __shared__ double sc[64];             // costlut (β·S), S <= Smax < 64, for the exact scans
+  __shared__ int anyv[PY_NW], anyd[PY_NW];
+  __shared__ int vote[2][PY_NW];        // per-wave early-exit votes, double-buffered by level parity
   __shared__ int nlist;
   PyrDims D;
 #pragma unroll
@@ -213,126 +193,171 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
   const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
   const double *uo1 = P.uold + ((size_t)k * P.nt + i + 1) * M;
-  PyrView V;
-  V.lvl = reinterpret_cast<double *>(pys);
-  V.hkey = reinterpret_cast<long long *>(pys + (size_t)2 * ncol * CW * sizeof(double));
-  V.hval = reinterpret_cast<uint16_t *>(V.hkey + PY_HSIZE);
-  const double *costlut = Lv.costlut;
+  double *lvl = reinterpret_cast<double *>(pys);                 // [2][L] level buffers
+  double *keyarr = lvl + (size_t)2 * L;                          // [L] bucket of Ψ_j by rank j
+  unsigned *htab = reinterpret_cast<unsigned *>(keyarr + L);     // [PY_HS]
   PY_STAMP(0);
-  if (tid <= Smax) sc[tid] = costlut[tid];
-  double a[M], uo0[M], uo1v[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    a[m] = P.dt * dfi[m];
-    uo0[m] = uoi[m];
-    uo1v[m] = uo1[m];
-  }
+  if (tid <= Smax) sc[tid] = Lv.costlut[tid];
 
-  // ---- own points: targets (T1, validity) and sources (Ψ) -------------------------------------
-  // invalid targets carry T1 = +Inf and best = -Inf, so the level loop needs no branches
-  double cur[NP], T1[NP], best[NP], bmb[NP];
-  unsigned valid = 0, multi = 0;
-  int nbm[PY_CPT];                       // per column: has lower / upper neighbour in dim m (bits 2m, 2m+1)
-  double psimax = 0.0, psimin = INFINITY;
+  // ---- this thread's grid column: coordinates 1..M-1 are shared by its N0 points ---------------
+  const bool colok = tid < ncol;
+  const int col = colok ? tid : 0;
+  double a[M], pc[M];
 #pragma unroll
-  for (int c2 = 0; c2 < PY_CPT; ++c2) {
-    const int col = tid + PY_T * c2;
-    int msk = 0, cc = col;
+  for (int m = 0; m < M; ++m) a[m] = P.dt * dfi[m];
+  int bcl = 0, bcs = 0, nbm = 0;
+  {
+    int cc = col;
 #pragma unroll
     for (int m = 1; m < M; ++m) {
       const int xm = cc % D.n[m];
       cc /= D.n[m];
-      msk |= (xm > 0 ? 1 : 0) << (2 * m);
-      msk |= (xm + 1 < D.n[m] ? 1 : 0) << (2 * m + 1);
-    }
-    nbm[c2] = col < ncol ? msk : 0;
-  }
-#pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    const int col = tid + PY_T * (q / N0), x0 = q % N0;
-    cur[q] = INFINITY;
-    T1[q] = INFINITY;
-    best[q] = -INFINITY;
-    bmb[q] = INFINITY;
-    if (col < ncol) {
-      int g = x0 + N0 * col;
-      double t = 0.0;
-      int bl = 0, bs = 0;
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const int x = g % D.n[m];
-        g /= D.n[m];
-        const double nu = (double)(D.base[m] + x);
-        t = t + a[m] * nu;  // ((0 + (Δt*df_1)*ν_1) + ...), HelpFunctions.jl:52-57
-        bl += (int)fabs(nu - uo0[m]);
-        bs += (int)fabs(nu - uo1v[m]);
-      }
-      if (bl <= B - cp) {
-        valid |= 1u << q;
-        T1[q] = t;
-        best[q] = INFINITY;
-      }
-      const double v = cp >= bs ? Sin[(size_t)(cp - bs) * L + x0 + N0 * col] : INFINITY;
-      cur[q] = v;
-      if (v < INFINITY) {
-        psimax = fmax(psimax, fabs(v));
-        psimin = fmin(psimin, v);
-      }
+      const double nu = (double)(D.base[m] + xm);
+      pc[m] = a[m] * nu;
+      bcl += (int)fabs(nu - uoi[m]);
+      bcs += (int)fabs(nu - uo1[m]);
+      nbm |= (xm > 0 ? 1 : 0) << (2 * m);
+      nbm |= (xm + 1 < D.n[m] ? 1 : 0) << (2 * m + 1);
     }
   }
-  const int any_valid = __syncthreads_or(valid != 0);
-  if (!any_valid) {  // no target of this row lies inside the trust region
-    for (int g = tid; g < L; g += PY_T) Sout[g] = INFINITY;
-    return;
+  const double u00 = uoi[0], u10 = uo1[0];
+
+  // ---- own points: targets (T1, validity) and sources (Ψ); all N0 gathers issued together --------
+  // invalid targets carry T1 = +Inf and best = -Inf, so the level loop needs no branches
+  double cur[N0], T1[N0];
+  unsigned valid = 0, fin = 0;
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) {
+    const double nu0 = (double)(D.base[0] + x0);
+    const int bs = (int)fabs(nu0 - u10) + bcs;
+    const int row = cp - bs;
+    const bool ok = colok && row >= 0;
+    cur[x0] = Sin[(size_t)(ok ? row : 0) * L + x0 + N0 * col];
+    if (!ok) cur[x0] = INFINITY;
+  }
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) {
+    const double nu0 = (double)(D.base[0] + x0);
+    double t = 0.0;
+    t = t + a[0] * nu0;  // ((0 + (Δt*df_1)*ν_1) + ...), HelpFunctions.jl:52-57
+#pragma unroll
+    for (int m = 1; m < M; ++m) t = t + pc[m];
+    const int bl = (int)fabs(nu0 - u00) + bcl;
+    const bool v = colok && bl <= B - cp;
+    valid |= (unsigned)v << x0;
+    T1[x0] = v ? t : INFINITY;
+    fin |= (unsigned)(cur[x0] < INFINITY) << x0;
+  }
+  double psimax = 0.0, psimin = INFINITY;
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) {
+    const bool f = fin >> x0 & 1;
+    psimax = fmax(psimax, f ? fabs(cur[x0]) : 0.0);
+    psimin = fmin(psimin, cur[x0]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    psimax = fmax(psimax, __shfl_xor(psimax, off));
+    psimin = fmin(psimin, __shfl_xor(psimin, off));
+  }
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = psimax;
+    red[1][tid >> 6] = psimin;
+  }
+  const bool any_valid = py_any(valid != 0, anyv);  // its barrier also publishes red[][]
+  double Pmax = red[0][0], Rmin = red[1][0];
+#pragma unroll
+  for (int w = 1; w < PY_NW; ++w) {
+    Pmax = fmax(Pmax, red[0][w]);
+    Rmin = fmin(Rmin, red[1][w]);
   }
   PY_STAMP(1);
-  const double Pmax = py_block_max(psimax, red);
-  const double Rmin = py_block_min(psimin, red);
-  if (!(Rmin < INFINITY)) {  // nothing is reachable from this source row
-    for (int g = tid; g < L; g += PY_T) Sout[g] = INFINITY;
+  if (!any_valid || !(Rmin < INFINITY)) {  // no target in the trust region, or nothing reachable
+    if (colok) {
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) Sout[x0 + N0 * col] = INFINITY;
+    }
     return;
   }
   // δ >= 2 ulp of any candidate fl(K + Ψ):  |K| <= sum_m |Δt·df_m|·max|ν_m| + β·Smax
-  double kb = sc[Smax];
+  double kb = fabs(sc[Smax]);
 #pragma unroll
   for (int m = 0; m < M; ++m)
     kb += fabs(a[m]) * fmax(fabs((double)D.base[m]), fabs((double)(D.base[m] + D.n[m] - 1)));
   const double Y = (Pmax + kb) * (1.0 + 0x1p-40) + 0x1p-1000;
-  const int E = ilogb(Y) + 1;                   // |y| < 2^E for every candidate y
-  const double inv_delta = ldexp(1.0, 52 - E);  // δ = 2^(E-52)
+  const int E = ilogb(Y) + 1;                                  // |y| < 2^E for every candidate y
+  const double inv_w = ldexp(1.0, min(52 - PY_G - E, 1000));  // bucket width 2^(E-52+G) >= δ = 2^(E-52)
+  constexpr double FR = 0x1p-8;                                // δ / bucket width (2^-PY_G)
 
-  // ---- clean-row test: no two finite Ψ within δ (bucket hash: same or adjacent bucket) ---------
-  PY_STAMP(2);
-  for (int s2 = tid; s2 < PY_HSIZE; s2 += PY_T) V.hkey[s2] = PY_EMPTY;
+  // ---- clean-row test: no two finite Ψ within δ, i.e. no shared bucket and no close pair across a
+  // bucket border.  Inserts of all N0 points advance in lock-step so their LDS atomics overlap. ----
+  double fq[N0], fr[N0];
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) {
+    const double x = (fin >> x0 & 1) ? cur[x0] * inv_w : 0.0;
+    fq[x0] = floor(x) + 0.0;
+    fr[x0] = x - fq[x0];
+  }
+  {
+    uint4 *h4 = reinterpret_cast<uint4 *>(htab);
+    for (int s2 = tid; s2 < PY_HS / 4; s2 += PY_T) h4[s2] = make_uint4(0u, 0u, 0u, 0u);
+    if (colok) {
+      double2 *k2 = reinterpret_cast<double2 *>(keyarr + N0 * col);
+#pragma unroll
+      for (int c = 0; c < N0 / 2; ++c) k2[c] = make_double2(fq[2 * c], fq[2 * c + 1]);
+    }
+  }
   if (tid == 0) nlist = 0;
+  PY_STAMP(2);
   __syncthreads();
   bool dirty = false;
+  {
+    unsigned slot[N0], ent[N0];
 #pragma unroll
-  for (int q = 0; q < NP; ++q)
-    if (cur[q] < INFINITY)
-      dirty |= py_insert(V, (long long)floor(cur[q] * inv_delta), q % N0 + N0 * (tid + PY_T * (q / N0)));
+    for (int x0 = 0; x0 < N0; ++x0) {
+      unsigned tg;
+      py_hslot(fq[x0], slot[x0], tg);
+      ent[x0] = tg << PY_RB | (unsigned)(x0 + N0 * col + 1);
+    }
+    unsigned pend = fin;
+    while (pend) {
+      unsigned old[N0];
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) old[x0] = (pend >> x0 & 1) ? atomicCAS(&htab[slot[x0]], 0u, ent[x0]) : 0u;
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        if (!(pend >> x0 & 1)) continue;
+        const unsigned o = old[x0];
+        if (o == 0u) {
+          pend &= ~(1u << x0);
+        } else if ((o >> PY_RB) == (ent[x0] >> PY_RB) && keyarr[(o & ((1u << PY_RB) - 1)) - 1] == fq[x0]) {
+          dirty = true;  // two Ψ in one bucket
+          pend &= ~(1u << x0);
+        } else {
+          slot[x0] = py_next(slot[x0]);
+        }
+      }
+    }
+  }
   __syncthreads();
 #pragma unroll
-  for (int q = 0; q < NP; ++q)
-    if (cur[q] < INFINITY) {
-      const long long b = (long long)floor(cur[q] * inv_delta);
-      dirty |= py_find(V, b - 1) >= 0 || py_find(V, b + 1) >= 0;
-    }
-  const int row_dirty = __syncthreads_or(dirty);
+  for (int x0 = 0; x0 < N0; ++x0) {  // close to a bucket border: look at the neighbouring bucket
+    if (!(fin >> x0 & 1)) continue;
+    if (fr[x0] <= FR) dirty |= py_find(htab, keyarr, fq[x0] - 1.0) >= 0;
+    if (fr[x0] >= 1.0 - FR) dirty |= py_find(htab, keyarr, fq[x0] + 1.0) >= 0;
+  }
+  const bool row_dirty = py_any(dirty, anyd);
   PY_STAMP(3);
 
-  double *lvl = V.lvl;
   if (row_dirty) {
     // exact scan of every (target, j) pair, Ψ and the target data staged in LDS
-    double *psi = lvl;                                 // [L]
-    double *t1s = reinterpret_cast<double *>(V.hkey);  // [L]  (the hash is no longer needed)
+    double *psi = lvl;      // [L]
+    double *t1s = lvl + L;  // [L]  (+Inf marks a target outside the trust region)
+    if (colok) {
 #pragma unroll
-    for (int q = 0; q < NP; ++q) {
-      const int col = tid + PY_T * (q / N0);
-      if (col < ncol) {
-        const int g = q % N0 + N0 * col;
-        psi[g] = cur[q];
-        t1s[g] = T1[q];  // +Inf marks a target outside the trust region
+      for (int x0 = 0; x0 < N0; ++x0) {
+        psi[x0 + N0 * col] = cur[x0];
+        t1s[x0 + N0 * col] = T1[x0];
       }
     }
     __syncthreads();
@@ -349,94 +374,143 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   }
 
   // ---- the pyramid (branch-free level loop) ------------------------------------------------------
+  const double beta = Lv.beta;
+  double K[N0], best[N0], bmb[N0];
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) {
+    K[x0] = T1[x0] + beta * 0.0;  // K_l(0) = fl(T1 + fl(β·0))
+    best[x0] = (valid >> x0 & 1) ? INFINITY : -INFINITY;
+    bmb[x0] = INFINITY;
+  }
+  unsigned multi = 0;
   int S = 0;
   for (;; ++S) {
-    const double cS = sc[S];
     unsigned mlt = 0, meq = 0;
 #pragma unroll
-    for (int q = 0; q < NP; ++q) {
-      const double cand = (T1[q] + cS) + cur[q];
-      const bool lt = cand < best[q];
-      const bool eq = (cand == best[q]) & (cand < INFINITY);
-      best[q] = lt ? cand : best[q];
-      bmb[q] = lt ? cur[q] : bmb[q];
-      mlt |= (unsigned)lt << q;
-      meq |= (unsigned)eq << q;
+    for (int x0 = 0; x0 < N0; ++x0) {
+      const double cand = K[x0] + cur[x0];
+      const bool lt = cand < best[x0];
+      const bool eq = (cand == best[x0]) & (cand < INFINITY);
+      best[x0] = lt ? cand : best[x0];
+      bmb[x0] = lt ? cur[x0] : bmb[x0];
+      mlt |= (unsigned)lt << x0;
+      meq |= (unsigned)eq << x0;
     }
     multi = (multi & ~mlt) | meq;
     if (S == Smax) break;
     // can a deeper level still reach (or tie) the minimum of some target of this workgroup?
-    const double cN = sc[S + 1];
+    // (K_l(S) is non-decreasing in S for β >= 0; otherwise every level is visited)
+    const double cN = beta * (double)(S + 1);
     bool more = false;
 #pragma unroll
-    for (int q = 0; q < NP; ++q) more |= ((T1[q] + cN) + Rmin) <= best[q];
-    if ((tid & 63) == 0) vote[S & 1][tid >> 6] = 0;
-    double *buf = lvl + (size_t)(S & 1) * ncol * CW;
-#pragma unroll
-    for (int c2 = 0; c2 < PY_CPT; ++c2) {
-      const int col = tid + PY_T * c2;
-      if (col < ncol) col_store<N0>(buf, col, &cur[N0 * c2]);
+    for (int x0 = 0; x0 < N0; ++x0) {
+      K[x0] = T1[x0] + cN;
+      more |= (K[x0] + Rmin) <= best[x0];
     }
-    if (__ballot(more) && (tid & 63) == 0) vote[S & 1][tid >> 6] = 1;
+    double *buf = lvl + (size_t)(S & 1) * L;
+    if (colok) col_store<N0>(buf, col, cur);
+    {
+      const unsigned long long bal = __ballot(more);
+      if ((tid & 63) == 0) vote[S & 1][tid >> 6] = bal != 0ull;
+    }
     __syncthreads();
+    // every LDS read of this level is issued before the first use
     int go = 0;
 #pragma unroll
-    for (int w = 0; w < PY_T / 64; ++w) go |= vote[S & 1][w];
-    if (!go) break;
+    for (int w = 0; w < PY_NW; ++w) go |= vote[S & 1][w];
+    double2 nb[M - 1][2][N0 / 2];
+#pragma unroll
+    for (int m = 1; m < M; ++m) {
+      const int st = G.cstride[m];
+      col_load<N0>(buf, col - (((nbm >> (2 * m)) & 1) ? st : 0), nb[m - 1][0]);
+      col_load<N0>(buf, col + (((nbm >> (2 * m + 1)) & 1) ? st : 0), nb[m - 1][1]);
+    }
+    if (!go && early_exit) break;
     // dilate by the unit cross: BM_{S+1}(x) = min(BM_S(x), BM_S(x ± e_m)); a missing neighbour
     // reads the own column (min with itself is a no-op), so there is no divergence
+    double nw[N0];
 #pragma unroll
-    for (int c2 = 0; c2 < PY_CPT; ++c2) {
-      const int col = tid + PY_T * c2;
-      const int colc = col < ncol ? col : 0;
-      double nw[N0];
-#pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
-        double v = cur[N0 * c2 + x0];
-        if (x0 > 0) v = vmin(v, cur[N0 * c2 + x0 - 1]);
-        if (x0 + 1 < N0) v = vmin(v, cur[N0 * c2 + x0 + 1]);
-        nw[x0] = v;
-      }
-#pragma unroll
-      for (int m = 1; m < M; ++m) {
-        const int st = G.cstride[m];
-        col_min<N0>(buf, colc - (((nbm[c2] >> (2 * m)) & 1) ? st : 0), nw);
-        col_min<N0>(buf, colc + (((nbm[c2] >> (2 * m + 1)) & 1) ? st : 0), nw);
-      }
-#pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) cur[N0 * c2 + x0] = nw[x0];
+    for (int x0 = 0; x0 < N0; ++x0) {
+      double v = cur[x0];
+      if (x0 > 0) v = vmin(v, cur[x0 - 1]);
+      if (x0 + 1 < N0) v = vmin(v, cur[x0 + 1]);
+      nw[x0] = v;
     }
+#pragma unroll
+    for (int m = 0; m < M - 1; ++m)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int c = 0; c < N0 / 2; ++c) {
+          nw[2 * c] = vmin(nw[2 * c], nb[m][s2][c].x);
+          nw[2 * c + 1] = vmin(nw[2 * c + 1], nb[m][s2][c].y);
+        }
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) cur[x0] = nw[x0];
   }
-
-  // ---- argmin by value lookup; targets whose minimum is reached at two levels go to a list --------
-  __syncthreads();
   PY_STAMP(4);
 #ifdef MIOC_STAMPS
   if (tid == 0) g_pyr_stamps[blockIdx.x][6] = S;
 #endif
-  int *list = reinterpret_cast<int *>(lvl);  // the level buffers are free now
+
+  // ---- argmin by bucket lookup (lock-step probes); a target whose minimum is reached at two levels,
+  // or whose bucket is somehow missing, goes to the exact-scan list ----------------------------------
+  unsigned lpend = 0, lslot[N0], ltag[N0];
+  int rk[N0];
+  double lfq[N0];
+  const unsigned done = valid & ~multi;
 #pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    const int col = tid + PY_T * (q / N0);
-    if (col >= ncol) continue;
-    const int g = q % N0 + N0 * col;
-    if ((valid >> q & 1) && (multi >> q & 1)) {
-      list[atomicAdd(&nlist, 1)] = g;
-      continue;
+  for (int x0 = 0; x0 < N0; ++x0) {
+    rk[x0] = -1;
+    lfq[x0] = floor(bmb[x0] * inv_w) + 0.0;
+    py_hslot(lfq[x0], lslot[x0], ltag[x0]);
+    lpend |= (unsigned)((done >> x0 & 1) && best[x0] < INFINITY) << x0;
+  }
+  unsigned lost = 0;
+  while (lpend) {
+    unsigned e[N0];
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) e[x0] = (lpend >> x0 & 1) ? htab[lslot[x0]] : 0u;
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) {
+      if (!(lpend >> x0 & 1)) continue;
+      if (e[x0] == 0u) {
+        lpend &= ~(1u << x0);
+        lost |= 1u << x0;
+      } else if ((e[x0] >> PY_RB) == ltag[x0]) {
+        rk[x0] = (int)(e[x0] & ((1u << PY_RB) - 1)) - 1;  // confirmed below
+        lpend &= ~(1u << x0);
+      } else {
+        lslot[x0] = py_next(lslot[x0]);
+      }
     }
-    double bv = INFINITY;
-    int ba = -1;
-    if ((valid >> q & 1) && best[q] < INFINITY) {
-      bv = best[q];
-      ba = py_find(V, (long long)floor(bmb[q] * inv_delta));
+  }
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) {  // confirm tag matches against the exact bucket (one batch of reads)
+    if (rk[x0] >= 0 && keyarr[rk[x0]] != lfq[x0]) {
+      rk[x0] = py_find(htab, keyarr, lfq[x0]);
+      if (rk[x0] < 0) lost |= 1u << x0;
     }
-    Sout[g] = bv;
-    if (ba >= 0) UU[g] = (uint16_t)ba;
+  }
+  __syncthreads();  // level buffers are free: the list lives there
+  int *list = reinterpret_cast<int *>(lvl);
+  const unsigned tolist = (valid & multi) | lost;
+  if (colok) {
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) {
+      const int g = x0 + N0 * col;
+      if (tolist >> x0 & 1) {
+        list[atomicAdd(&nlist, 1)] = g;
+        continue;
+      }
+      Sout[g] = (valid >> x0 & 1) ? best[x0] : INFINITY;
+      if (rk[x0] >= 0) UU[g] = (uint16_t)rk[x0];
+    }
   }
   __syncthreads();
   const int nl = nlist;
-  for (int e = tid; e < nl; e += PY_T) {
-    const int g = list[e];
+  for (int e2 = tid; e2 < nl; e2 += PY_T) {
+    const int g = list[e2];
     int gg = g;
     double t = 0.0;
 #pragma unroll
@@ -447,6 +521,9 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     }
     double bv = INFINITY;
     int ba = -1;
+    double uo1v[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) uo1v[m] = uo1[m];
     py_brute_target<M>(D, sc, t, g, nullptr, Sin, uo1v, L, cp, &bv, &ba);
     Sout[g] = bv;
     if (ba >= 0) UU[g] = (uint16_t)ba;
@@ -486,7 +563,7 @@ hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsD
 }
 
 size_t pyr_lds_bytes(const PyrGeom &G) {
-  return (size_t)2 * G.ncol * G.n[0] * sizeof(double) + (size_t)PY_HSIZE * (sizeof(long long) + sizeof(uint16_t));
+  return (size_t)3 * G.ncol * G.n[0] * sizeof(double) + (size_t)PY_HS * sizeof(unsigned);
 }
 
 hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
@@ -494,9 +571,10 @@ hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
                            int32_t *counters) {
   const dim3 grid(P.B + 1, P.K), blk(PY_T);
   const size_t lds = pyr_lds_bytes(G);
+  const int early_exit = Lv.beta >= 0.0;
 #define PYR_CASE(MM, NN)                                                                                   \
   if (G.M == MM && G.n[0] == NN) {                                                                         \
-    hipLaunchKernelGGL((k_pyr_step<MM, NN>), grid, blk, lds, s, P, Lv, G, i, Sin, Sout, UU, s_stride,      \
+    hipLaunchKernelGGL((k_pyr_step<MM, NN>), grid, blk, lds, s, P, Lv, G, i, early_exit, Sin, Sout, UU, s_stride,      \
                        uu_stride_k, counters);                                                             \
     return hipGetLastError();                                                                              \
   }
@@ -504,7 +582,6 @@ hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
   PYR_CASE(2, 4) PYR_CASE(3, 4) PYR_CASE(4, 4) PYR_CASE(5, 4) PYR_CASE(6, 4)
 #undef PYR_CASE
   return hipErrorInvalidValue;
-  return hipGetLastError();
 }
 
 #ifdef MIOC_STAMPS
