@@ -144,6 +144,25 @@ def run(args, rank, world, device, dist, torch):
     return res
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/roundN_pmc_traffic.json,
+    made by scripts/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None."""
+    import glob
+    import re
+    files = glob.glob(os.path.join(ROOT, "profiles", "round*_pmc_traffic.json"))
+    if not files:
+        return None, None
+    f = max(files, key=lambda x: int(re.search(r"round(\d+)_", os.path.basename(x)).group(1)))
+    try:
+        with open(f) as fh:
+            e = json.load(fh)["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None, None
+    if not e or "hbm_bytes_per_launch" not in e:
+        return None, None
+    return e["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+
+
 def roofline_of(res, args):
     """Algorithmic bytes / flops of the dominant kernel per launch (SURVEY §8 d), over its HIP-event time."""
     lv, B, K, nt = res["levels"], res["B"], res["K"], res["nt"]
@@ -177,8 +196,10 @@ def roofline_of(res, args):
         roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
                      "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS}
     ach = bytes_per_launch / avg_s / 1e9
+    traffic, tsrc = pmc_traffic(res["dom_name"])
     roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "kernel": res["dom_name"],
+            "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None if traffic is None else round(traffic),
+            "traffic_source": tsrc, "kernel": res["dom_name"],
             "avg_launch_us": round(avg_s * 1e6, 3), "bytes_per_launch": bytes_per_launch}
     roof_valu = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in roof_valu.items()}
     return roof, roof_valu

@@ -1,0 +1,45 @@
+"""Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into HBM bytes per kernel launch.
+
+Usage: python scripts/pmc_traffic.py OUT.json LABEL=DIR/NAME_counter_collection.csv ...
+FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE
+reports half the bytes of wide reads, so it is doubled; WRITE_SIZE is taken as is.  Both counters
+count Infinity-Cache hits as memory-side traffic.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    n = name.split("(")[0].replace("void ", "").strip()
+    return n.split("::")[-1].split("<")[0]
+
+
+def main():
+    out = sys.argv[1]
+    res = {}
+    for spec in sys.argv[2:]:
+        label, path = spec.split("=", 1)
+        acc = defaultdict(lambda: defaultdict(list))
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                acc[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+        for k, d in acc.items():
+            e = res.setdefault(k, {})
+            for cname, vals in d.items():
+                scale = 1024.0 * (2.0 if cname == "FETCH_SIZE" else 1.0)
+                e[cname.lower() + "_bytes_per_launch"] = scale * sum(vals) / len(vals)
+                e["launches_" + cname.lower()] = len(vals)
+                e.setdefault("passes", []).append(label)
+    for k, e in res.items():
+        if "fetch_size_bytes_per_launch" in e and "write_size_bytes_per_launch" in e:
+            e["hbm_bytes_per_launch"] = e["fetch_size_bytes_per_launch"] + e["write_size_bytes_per_launch"]
+    json.dump({"note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes, mean per dispatch",
+               "kernels": res}, open(out, "w"), indent=1, sort_keys=True)
+    for k, e in sorted(res.items()):
+        print(k, {kk: (round(v) if isinstance(v, float) else v) for kk, v in e.items()})
+
+
+if __name__ == "__main__":
+    main()
