@@ -58,6 +58,7 @@ def candidates_per_step(levels, uo, B):
 
 def run(args, rank, world, device, dist, torch):
     from mioc import native
+    from mioc.batch import gather_results, level_ranks, shard
     from mioc.synth import CONFIGS, make_inputs
 
     cfg = CONFIGS[args.config]
@@ -83,9 +84,10 @@ def run(args, rank, world, device, dist, torch):
     K = args.batch
     nsets = args.warmup + args.steps
     dfs, uos = [], []
+    lo, hi = shard(world * K, world, rank)  # this rank's contiguous block of each step's global batch
     for s in range(nsets):
-        for b in range(K):
-            k = (s * world + rank) * K + b
+        for b in range(lo, hi):
+            k = s * world * K + b
             _, df, uo = make_inputs(cfg, k=k, nt=nt, levels=levels)
             dfs.append(df)
             uos.append(uo)
@@ -95,7 +97,6 @@ def run(args, rank, world, device, dist, torch):
     d_phi = torch.empty(K, dtype=torch.float64, device=device)
     d_st = torch.empty(K, dtype=torch.int32, device=device)
     nuval = torch.tensor(levels.nuval, dtype=torch.float64, device=device)
-    gather_buf = [torch.empty((K, nt), dtype=torch.int16, device=device) for _ in range(world)] if rank == 0 else None
 
     def step(s):
         ctx.bellman_batch_device(K, d_df[s].data_ptr(), d_uo[s].data_ptr(), levels.M, nt, B, dt)
@@ -103,11 +104,7 @@ def run(args, rank, world, device, dist, torch):
         if world > 1:
             ctx.synchronize()
             # controls as level ranks (uint16 payload) + Φ*, gathered to rank 0 over RCCL
-            ranks = (d_u.reshape(K * nt, 1, -1) == nuval.reshape(1, *nuval.shape)).all(dim=2).int().argmax(dim=1)
-            payload = ranks.to(torch.int16).reshape(K, nt)
-            dist.gather(payload, gather_buf, dst=0)
-            phis = [torch.empty_like(d_phi) for _ in range(world)] if rank == 0 else None
-            dist.gather(d_phi, phis, dst=0)
+            gather_results(dist, level_ranks(d_u, nuval), d_phi, world * K, world, rank)
 
     for s in range(args.warmup):
         step(s)

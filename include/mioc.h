@@ -132,11 +132,23 @@ int32_t mioc_reset_stats(mioc_ctx *ctx);
 int32_t mioc_last_algo(mioc_ctx *ctx);
 
 /*
- * Diagnostics of the last bellman/backtrack: counters[0] rows resolved by the exact scan (pyramid: rows
- * whose values are not pairwise separated), [1] targets resolved by the exact scan (minimum reached at two
- * levels), [2] p=Inf walk steps resolved by the exact scan, [3] internal consistency failures (must be 0).
+ * Diagnostics of the last bellman/backtrack: counters[0] pyramid targets resolved by the exact scan because
+ * their winning value has another source value within rounding distance, [1] pyramid targets resolved by
+ * the exact scan because their minimum is reached at two levels, [2] p=Inf walk steps resolved by the
+ * exact scan, [3] internal consistency failures (must be 0).
  */
 int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n);
+
+/*
+ * The argmin table `U` of the last bellman call, one step at a time, in the reference's layout
+ * (HelpFunctions.jl:74, U[:, c+1, l..., i+1] of multi-trust.jl:76): for subproblem k and step i
+ * (0 <= i < nt-1), U_out[c + (B+1)*g] = 0-based iterator rank of the source j minimising Φ_i at budget
+ * c and the target level with grid-linear index g (levels in column-major grid order), as an int32.
+ * Cells the reference never writes because Φ_i = +Inf there hold -1 when c < b̃(l, i) and are
+ * unspecified otherwise (the reference leaves them at whatever `U` held before).  U_out has
+ * (B+1) * prod(counts) entries.  The p=Inf collapse stores class tables instead (MIOC_EINVAL).
+ */
+int32_t mioc_get_argmin_table(mioc_ctx *ctx, int64_t k, int64_t step, int32_t *U_out);
 
 #ifdef __cplusplus
 }

@@ -197,14 +197,15 @@ int run_bellman(mioc_ctx *ctx) {
 
   int algo = (int)ctx->opt_algo;
   const bool pinf_ok = ctx->p_kind == MIOC_P_INF && bmax + 1 <= 64;
-  const bool pyr_ok = ctx->p_kind == MIOC_P_ONE && ctx->pyr_ok;
+  // the L1-ball identity min_j fl(K(d(l,j)) + Ψ_j) = min_S fl(K(S) + BM_S(l)) needs K non-decreasing in S
+  const bool pyr_ok = ctx->p_kind == MIOC_P_ONE && ctx->pyr_ok && ctx->beta >= 0.0;
   if (algo == MIOC_ALGO_AUTO)
     algo = pinf_ok ? MIOC_ALGO_PINF : (pyr_ok && ctx->L >= 256 ? MIOC_ALGO_PYRAMID : MIOC_ALGO_GENERIC);
   if (algo == MIOC_ALGO_PINF && !pinf_ok)
     return fail(ctx, MIOC_EINVAL, "p=Inf collapse needs p_kind MIOC_P_INF and <= 64 budget classes");
   if (algo == MIOC_ALGO_PYRAMID && !pyr_ok)
-    return fail(ctx, MIOC_EINVAL, "the L1-ball pyramid needs p = 1 and a product grid of consecutive integer "
-                                  "levels (first dimension <= 8 levels, <= 4096 tuples)");
+    return fail(ctx, MIOC_EINVAL, "the L1-ball pyramid needs p = 1, beta >= 0 and a product grid of consecutive "
+                                  "integer levels (first dimension 4 or 8 levels, <= 4096 tuples)");
   if (!ctx->d_counters) {
     size_t cc = 0;
     int rc0 = grow(ctx, &ctx->d_counters, &cc, 8 * sizeof(int32_t), "counters");
@@ -431,6 +432,7 @@ int32_t mioc_set_levels(mioc_ctx *ctx, int64_t M, const int64_t *counts, const i
     }
     gidx[r] = (int32_t)g;
   }
+  ctx->gidx_h = gidx;
   ctx->numin_h.assign(M, 0.0);
   ctx->numax_h.assign(M, 0.0);
   for (int64_t m = 0; m < M; ++m) {
@@ -616,6 +618,51 @@ int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
   HIP_TRY(ctx, hipMemcpy(f, ctx->d_flags, sizeof f, hipMemcpyDeviceToHost));
   const int64_t all[4] = {c[0], c[1], f[2], f[3]};
   for (int32_t q = 0; q < n && q < 4; ++q) counters[q] = all[q];
+  return MIOC_OK;
+}
+
+int32_t mioc_get_argmin_table(mioc_ctx *ctx, int64_t k, int64_t step, int32_t *U_out) {
+  if (!ctx || !U_out) return MIOC_EINVAL;
+  if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "no bellman result to read");
+  if (k < 0 || k >= ctx->K || step < 0 || step + 1 >= ctx->nt)
+    return fail(ctx, MIOC_EINVAL, "subproblem or step out of range (0 <= step < nt-1)");
+  if (ctx->algo != MIOC_ALGO_GENERIC && ctx->algo != MIOC_ALGO_PYRAMID)
+    return fail(ctx, MIOC_EINVAL, "the p=Inf collapse keeps per-budget class tables, not U");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  const int64_t R = ctx->B + 1, L = ctx->L, M = ctx->M, nt = ctx->nt;
+  std::vector<double> uo(M);
+  HIP_TRY(ctx, hipMemcpy(uo.data(), ctx->d_uold + ((size_t)k * nt + step) * M, M * sizeof(double),
+                         hipMemcpyDeviceToHost));
+  std::vector<int32_t> out((size_t)R * ctx->Lgrid, -1);
+  auto bt = [&](int64_t r) {
+    int64_t b = 0;
+    for (int64_t m = 0; m < M; ++m) b += (int64_t)std::fabs(ctx->nuval_h[r * M + m] - uo[m]);
+    return b;
+  };
+  const size_t step_cells = (size_t)R * L;
+  if (ctx->algo == MIOC_ALGO_PYRAMID) {  // staged: UU_i[c'][l] = U_i[l, c' + b̃_l(i)]
+    std::vector<uint16_t> uu(step_cells);
+    const uint16_t *src = (const uint16_t *)ctx->d_U + ((size_t)k * (nt - 1) + step) * step_cells;
+    HIP_TRY(ctx, hipMemcpy(uu.data(), src, step_cells * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < L; ++r) {
+      const int64_t b = bt(r);
+      for (int64_t c = b; c < R; ++c) out[c + R * ctx->gidx_h[r]] = uu[(c - b) * L + r];
+    }
+  } else {  // generic: U_i[l][c]
+    std::vector<unsigned char> raw(step_cells * ctx->ubytes);
+    const unsigned char *src = (const unsigned char *)ctx->d_U + ((size_t)k * (nt - 1) + step) * step_cells * ctx->ubytes;
+    HIP_TRY(ctx, hipMemcpy(raw.data(), src, raw.size(), hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < L; ++r) {
+      const int64_t b = bt(r);
+      for (int64_t c = b; c < R; ++c) {
+        const size_t q = (size_t)r * R + c;
+        out[c + R * ctx->gidx_h[r]] =
+            ctx->ubytes == 1 ? (int32_t)raw[q] : (int32_t)reinterpret_cast<const uint16_t *>(raw.data())[q];
+      }
+    }
+  }
+  std::memcpy(U_out, out.data(), out.size() * sizeof(int32_t));
   return MIOC_OK;
 }
 

@@ -117,6 +117,7 @@ struct mioc_ctx {
   std::vector<int64_t> counts, values;
   std::vector<int32_t> tuples;     // [L][M] 1-based
   std::vector<double> nuval_h;     // [L][M]
+  std::vector<int32_t> gidx_h;     // [L] grid-linear index of each admissible tuple
   std::vector<double> numin_h, numax_h;
   double *d_nuval = nullptr;
   int32_t *d_nuint = nullptr;
@@ -148,7 +149,7 @@ struct mioc_ctx {
   mioc::PyrGeom pyr;
   double *d_stage = nullptr;       // [2][K][B+1][L] source-row-major fronts
   size_t stage_cap = 0;
-  int32_t *d_counters = nullptr;   // [8] diagnostics: dirty rows, multi-level targets, ...
+  int32_t *d_counters = nullptr;   // [8] diagnostics: value-collision targets, multi-level targets, ...
 
   // generic buffers
   double *d_front = nullptr;       // [2][K][L][RP]

@@ -68,68 +68,45 @@ __device__ __forceinline__ void py_hslot(double fq, unsigned &slot, unsigned &ta
 }
 __device__ __forceinline__ unsigned py_next(unsigned s) { return s + 1 == (unsigned)PY_HS ? 0u : s + 1; }
 
-// rank holding bucket fq, or -1
-__device__ __forceinline__ int py_find(const unsigned *htab, const double *keyarr, double fq) {
-  unsigned s, tag;
-  py_hslot(fq, s, tag);
-  for (;;) {
-    const unsigned e = htab[s];
-    if (e == 0u) return -1;
-    if ((e >> PY_RB) == tag && keyarr[(e & ((1u << PY_RB) - 1)) - 1] == fq) return (int)(e & ((1u << PY_RB) - 1)) - 1;
-    s = py_next(s);
-  }
-}
-
 struct PyrDims {  // geometry copied by value into registers (never escapes to memory)
   int n[kMaxM];
   int base[kMaxM];
 };
 
-template <int M>
-__device__ __forceinline__ int py_dist(const PyrDims &D, int a, int b) {
-  int d = 0;
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const int xa = a % D.n[m], xb = b % D.n[m];
-    d += xa > xb ? xa - xb : xb - xa;
-    a /= D.n[m];
-    b /= D.n[m];
-  }
-  return d;
-}
+__device__ __forceinline__ double py_bucket(double v, double inv_w) { return floor(v * inv_w) + 0.0; }
 
-// Ψ_j = Φ_{i+1}[j, c'] read back from the staging buffer of step i+1
-template <int M>
-__device__ __forceinline__ double py_psi(const PyrDims &D, const double *Sin, const double *uo1, int L, int cp,
-                                         int j) {
-  int b = 0, g = j;
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const int x = g % D.n[m];
-    g /= D.n[m];
-    b += (int)fabs((double)(D.base[m] + x) - uo1[m]);
-  }
-  return cp >= b ? Sin[(size_t)(cp - b) * L + j] : INFINITY;
-}
-
-// exact first-index argmin for one target: the reference loop (HelpFunctions.jl:60-77) for one cell
-template <int M>
-__device__ __forceinline__ void py_brute_target(const PyrDims &D, const double *costlut, double T1l, int l,
-                                                const double *psi_lds, const double *Sin, const double *uo1, int L,
-                                                int cp, double *best, int *arg) {
-  double bv = INFINITY;
-  int ba = -1;
-  for (int j = 0; j < L; ++j) {
-    const double v = psi_lds ? psi_lds[j] : py_psi<M>(D, Sin, uo1, L, cp, j);
-    if (!(v < INFINITY)) continue;
-    const double val = (T1l + costlut[py_dist<M>(D, l, j)]) + v;
-    if (val < bv) {
-      bv = val;
-      ba = j;
+// Mark every source holding bucket fq as colliding (and report whether there was one).
+__device__ __forceinline__ bool py_mark_bucket(const unsigned *htab, const double *psiarr, unsigned char *coll,
+                                               double fq, double inv_w) {
+  unsigned s, tag;
+  py_hslot(fq, s, tag);
+  bool found = false;
+  for (;;) {
+    const unsigned e = htab[s];
+    if (e == 0u) return found;
+    if ((e >> PY_RB) == tag) {
+      const int r = (int)(e & ((1u << PY_RB) - 1)) - 1;
+      if (py_bucket(psiarr[r], inv_w) == fq) {
+        coll[r] = 1;
+        found = true;
+      }
     }
+    s = py_next(s);
   }
-  *best = bv;
-  *arg = ba;
+}
+
+// First source (probe order) whose Ψ equals v exactly, starting the walk at slot s; -1 if none.
+__device__ __forceinline__ int py_find_value(const unsigned *htab, const double *psiarr, unsigned s, unsigned tag,
+                                             double v) {
+  for (;;) {
+    const unsigned e = htab[s];
+    if (e == 0u) return -1;
+    if ((e >> PY_RB) == tag) {
+      const int r = (int)(e & ((1u << PY_RB) - 1)) - 1;
+      if (psiarr[r] == v) return r;
+    }
+    s = py_next(s);
+  }
 }
 
 // A column (N0 doubles = N0/2 16-byte chunks) is stored with its chunks XOR-swizzled by the column's
@@ -166,7 +143,7 @@ __device__ __forceinline__ bool py_any(bool f, int *slots) {
 }
 
 template <int M, int N0>
-__global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i, int early_exit,
+__global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i,
                                                    const double *__restrict__ Sin_all, double *__restrict__ Sout_all,
                                                    uint16_t *__restrict__ UU_all, size_t s_stride, size_t uu_stride_k,
                                                    int32_t *__restrict__ counters) {
@@ -174,10 +151,11 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   static_assert(M >= 2, "product grid");
   extern __shared__ __attribute__((aligned(16))) unsigned char pys[];
   __shared__ double red[2][PY_NW];
-  __shared__ double sc[64];             // costlut (β·S), S <= Smax < 64, for the exact scans
-  __shared__ int anyv[PY_NW], anyd[PY_NW];
+  __shared__ int anyv[PY_NW];
   __shared__ int vote[2][PY_NW];        // per-wave early-exit votes, double-buffered by level parity
-  __shared__ int nlist;
+  __shared__ double scan_v[2][PY_NW];   // exact-scan reductions, double-buffered by list position parity
+  __shared__ int scan_r[2][PY_NW];
+  __shared__ int nlist, nmulti;
   PyrDims D;
 #pragma unroll
   for (int m = 0; m < kMaxM; ++m) {
@@ -186,6 +164,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   }
   const int k = blockIdx.y;
   const int L = Lv.L, B = P.B, tid = threadIdx.x, ncol = G.ncol, Smax = G.Smax;
+  const double beta = Lv.beta;
   const int cp = B - (int)blockIdx.x;  // source row: high rows first
   const double *Sin = Sin_all + (size_t)k * s_stride;
   double *Sout = Sout_all + (size_t)k * s_stride + (size_t)cp * L;
@@ -193,11 +172,11 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
   const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
   const double *uo1 = P.uold + ((size_t)k * P.nt + i + 1) * M;
-  double *lvl = reinterpret_cast<double *>(pys);                 // [2][L] level buffers
-  double *keyarr = lvl + (size_t)2 * L;                          // [L] bucket of Ψ_j by rank j
-  unsigned *htab = reinterpret_cast<unsigned *>(keyarr + L);     // [PY_HS]
+  double *lvl = reinterpret_cast<double *>(pys);                             // [2][L] level buffers
+  double *psiarr = lvl + (size_t)2 * L;                                      // [L] Ψ_j by rank j
+  unsigned *htab = reinterpret_cast<unsigned *>(psiarr + L);                 // [PY_HS] bucket hash
+  unsigned char *coll = reinterpret_cast<unsigned char *>(htab + PY_HS);     // [L] Ψ_j has a close value
   PY_STAMP(0);
-  if (tid <= Smax) sc[tid] = Lv.costlut[tid];
 
   // ---- this thread's grid column: coordinates 1..M-1 are shared by its N0 points ---------------
   const bool colok = tid < ncol;
@@ -205,13 +184,16 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   double a[M], pc[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) a[m] = P.dt * dfi[m];
+  int xc[M];
   int bcl = 0, bcs = 0, nbm = 0;
+  xc[0] = 0;
   {
     int cc = col;
 #pragma unroll
     for (int m = 1; m < M; ++m) {
       const int xm = cc % D.n[m];
       cc /= D.n[m];
+      xc[m] = xm;
       const double nu = (double)(D.base[m] + xm);
       pc[m] = a[m] * nu;
       bcl += (int)fabs(nu - uoi[m]);
@@ -280,17 +262,18 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     return;
   }
   // δ >= 2 ulp of any candidate fl(K + Ψ):  |K| <= sum_m |Δt·df_m|·max|ν_m| + β·Smax
-  double kb = fabs(sc[Smax]);
+  double kb = beta * (double)Smax;
 #pragma unroll
   for (int m = 0; m < M; ++m)
     kb += fabs(a[m]) * fmax(fabs((double)D.base[m]), fabs((double)(D.base[m] + D.n[m] - 1)));
   const double Y = (Pmax + kb) * (1.0 + 0x1p-40) + 0x1p-1000;
   const int E = ilogb(Y) + 1;                                  // |y| < 2^E for every candidate y
   const double inv_w = ldexp(1.0, min(52 - PY_G - E, 1000));  // bucket width 2^(E-52+G) >= δ = 2^(E-52)
-  constexpr double FR = 0x1p-8;                                // δ / bucket width (2^-PY_G)
+  constexpr double FR = 1.0 / (double)(1 << PY_G);             // δ / bucket width
 
-  // ---- clean-row test: no two finite Ψ within δ, i.e. no shared bucket and no close pair across a
-  // bucket border.  Inserts of all N0 points advance in lock-step so their LDS atomics overlap. ----
+  // ---- collision flags: coll[j] = 1 iff some other finite Ψ lies within δ of Ψ_j (it shares Ψ_j's
+  // bucket, or sits across a bucket border close to it).  Inserts advance in lock-step so their LDS
+  // atomics overlap; duplicates are inserted too. -----------------------------------------------------
   double fq[N0], fr[N0];
 #pragma unroll
   for (int x0 = 0; x0 < N0; ++x0) {
@@ -301,16 +284,19 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   {
     uint4 *h4 = reinterpret_cast<uint4 *>(htab);
     for (int s2 = tid; s2 < PY_HS / 4; s2 += PY_T) h4[s2] = make_uint4(0u, 0u, 0u, 0u);
+    for (int s2 = tid; s2 < L; s2 += PY_T) coll[s2] = 0;
     if (colok) {
-      double2 *k2 = reinterpret_cast<double2 *>(keyarr + N0 * col);
+      double2 *p2 = reinterpret_cast<double2 *>(psiarr + N0 * col);
 #pragma unroll
-      for (int c = 0; c < N0 / 2; ++c) k2[c] = make_double2(fq[2 * c], fq[2 * c + 1]);
+      for (int c = 0; c < N0 / 2; ++c) p2[c] = make_double2(cur[2 * c], cur[2 * c + 1]);
     }
   }
-  if (tid == 0) nlist = 0;
+  if (tid == 0) {
+    nlist = 0;
+    nmulti = 0;
+  }
   PY_STAMP(2);
   __syncthreads();
-  bool dirty = false;
   {
     unsigned slot[N0], ent[N0];
 #pragma unroll
@@ -319,7 +305,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       py_hslot(fq[x0], slot[x0], tg);
       ent[x0] = tg << PY_RB | (unsigned)(x0 + N0 * col + 1);
     }
-    unsigned pend = fin;
+    unsigned pend = fin, hit = 0;
     while (pend) {
       unsigned old[N0];
 #pragma unroll
@@ -330,51 +316,32 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
         const unsigned o = old[x0];
         if (o == 0u) {
           pend &= ~(1u << x0);
-        } else if ((o >> PY_RB) == (ent[x0] >> PY_RB) && keyarr[(o & ((1u << PY_RB) - 1)) - 1] == fq[x0]) {
-          dirty = true;  // two Ψ in one bucket
-          pend &= ~(1u << x0);
-        } else {
-          slot[x0] = py_next(slot[x0]);
+          continue;
         }
+        if ((o >> PY_RB) == (ent[x0] >> PY_RB)) {
+          const int r = (int)(o & ((1u << PY_RB) - 1)) - 1;
+          if (py_bucket(psiarr[r], inv_w) == fq[x0]) {  // two Ψ in one bucket
+            coll[r] = 1;
+            hit |= 1u << x0;
+          }
+        }
+        slot[x0] = py_next(slot[x0]);
       }
     }
-  }
-  __syncthreads();
+    __syncthreads();  // every value is in the table
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {  // close to a bucket border: look at the neighbouring bucket
-    if (!(fin >> x0 & 1)) continue;
-    if (fr[x0] <= FR) dirty |= py_find(htab, keyarr, fq[x0] - 1.0) >= 0;
-    if (fr[x0] >= 1.0 - FR) dirty |= py_find(htab, keyarr, fq[x0] + 1.0) >= 0;
+    for (int x0 = 0; x0 < N0; ++x0) {  // close to a bucket border: the neighbouring bucket too
+      if (!(fin >> x0 & 1)) continue;
+      if (fr[x0] <= FR && py_mark_bucket(htab, psiarr, coll, fq[x0] - 1.0, inv_w)) hit |= 1u << x0;
+      if (fr[x0] >= 1.0 - FR && py_mark_bucket(htab, psiarr, coll, fq[x0] + 1.0, inv_w)) hit |= 1u << x0;
+    }
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0)
+      if (hit >> x0 & 1) coll[x0 + N0 * col] = 1;
   }
-  const bool row_dirty = py_any(dirty, anyd);
   PY_STAMP(3);
 
-  if (row_dirty) {
-    // exact scan of every (target, j) pair, Ψ and the target data staged in LDS
-    double *psi = lvl;      // [L]
-    double *t1s = lvl + L;  // [L]  (+Inf marks a target outside the trust region)
-    if (colok) {
-#pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
-        psi[x0 + N0 * col] = cur[x0];
-        t1s[x0 + N0 * col] = T1[x0];
-      }
-    }
-    __syncthreads();
-    for (int g = tid; g < L; g += PY_T) {
-      double bv = INFINITY;
-      int ba = -1;
-      const double t = t1s[g];
-      if (t < INFINITY) py_brute_target<M>(D, sc, t, g, psi, nullptr, nullptr, L, cp, &bv, &ba);
-      Sout[g] = bv;
-      if (ba >= 0) UU[g] = (uint16_t)ba;
-    }
-    if (tid == 0) atomicAdd(&counters[0], 1);
-    return;
-  }
-
   // ---- the pyramid (branch-free level loop) ------------------------------------------------------
-  const double beta = Lv.beta;
   double K[N0], best[N0], bmb[N0];
 #pragma unroll
   for (int x0 = 0; x0 < N0; ++x0) {
@@ -399,7 +366,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     multi = (multi & ~mlt) | meq;
     if (S == Smax) break;
     // can a deeper level still reach (or tie) the minimum of some target of this workgroup?
-    // (K_l(S) is non-decreasing in S for β >= 0; otherwise every level is visited)
+    // (K_l(S) is non-decreasing in S: the pyramid is only selected for β >= 0)
     const double cN = beta * (double)(S + 1);
     bool more = false;
 #pragma unroll
@@ -425,7 +392,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       col_load<N0>(buf, col - (((nbm >> (2 * m)) & 1) ? st : 0), nb[m - 1][0]);
       col_load<N0>(buf, col + (((nbm >> (2 * m + 1)) & 1) ? st : 0), nb[m - 1][1]);
     }
-    if (!go && early_exit) break;
+    if (!go) break;
     // dilate by the unit cross: BM_{S+1}(x) = min(BM_S(x), BM_S(x ± e_m)); a missing neighbour
     // reads the own column (min with itself is a no-op), so there is no divergence
     double nw[N0];
@@ -453,20 +420,19 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   if (tid == 0) g_pyr_stamps[blockIdx.x][6] = S;
 #endif
 
-  // ---- argmin by bucket lookup (lock-step probes); a target whose minimum is reached at two levels,
-  // or whose bucket is somehow missing, goes to the exact-scan list ----------------------------------
+  // ---- argmin.  A target whose minimum is reached at one level only, by a value with no close
+  // neighbour, has a unique minimiser: the source holding that value (lock-step hash probes).  Every
+  // other target with a finite minimum goes to the exact scan below. --------------------------------
   unsigned lpend = 0, lslot[N0], ltag[N0];
   int rk[N0];
-  double lfq[N0];
-  const unsigned done = valid & ~multi;
+  const unsigned fin_t = valid & ~multi;
 #pragma unroll
   for (int x0 = 0; x0 < N0; ++x0) {
     rk[x0] = -1;
-    lfq[x0] = floor(bmb[x0] * inv_w) + 0.0;
-    py_hslot(lfq[x0], lslot[x0], ltag[x0]);
-    lpend |= (unsigned)((done >> x0 & 1) && best[x0] < INFINITY) << x0;
+    py_hslot(py_bucket(bmb[x0], inv_w), lslot[x0], ltag[x0]);
+    lpend |= (unsigned)((fin_t >> x0 & 1) && best[x0] < INFINITY) << x0;
   }
-  unsigned lost = 0;
+  const unsigned want = lpend;
   while (lpend) {
     unsigned e[N0];
 #pragma unroll
@@ -476,7 +442,6 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       if (!(lpend >> x0 & 1)) continue;
       if (e[x0] == 0u) {
         lpend &= ~(1u << x0);
-        lost |= 1u << x0;
       } else if ((e[x0] >> PY_RB) == ltag[x0]) {
         rk[x0] = (int)(e[x0] & ((1u << PY_RB) - 1)) - 1;  // confirmed below
         lpend &= ~(1u << x0);
@@ -485,51 +450,105 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       }
     }
   }
+  unsigned tolist = valid & multi;
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {  // confirm tag matches against the exact bucket (one batch of reads)
-    if (rk[x0] >= 0 && keyarr[rk[x0]] != lfq[x0]) {
-      rk[x0] = py_find(htab, keyarr, lfq[x0]);
-      if (rk[x0] < 0) lost |= 1u << x0;
-    }
+  for (int x0 = 0; x0 < N0; ++x0) {  // confirm against the exact value (one batch of reads), then the flag
+    if (!(want >> x0 & 1)) continue;
+    if (rk[x0] >= 0 && psiarr[rk[x0]] != bmb[x0])
+      rk[x0] = py_find_value(htab, psiarr, py_next(lslot[x0]), ltag[x0], bmb[x0]);
+    if (rk[x0] < 0 || coll[rk[x0]]) tolist |= 1u << x0;
   }
-  __syncthreads();  // level buffers are free: the list lives there
+  __syncthreads();  // the level buffers are free: the list lives there
   int *list = reinterpret_cast<int *>(lvl);
-  const unsigned tolist = (valid & multi) | lost;
   if (colok) {
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
       const int g = x0 + N0 * col;
-      if (tolist >> x0 & 1) {
-        list[atomicAdd(&nlist, 1)] = g;
-        continue;
-      }
       Sout[g] = (valid >> x0 & 1) ? best[x0] : INFINITY;
-      if (rk[x0] >= 0) UU[g] = (uint16_t)rk[x0];
+      if (tolist >> x0 & 1)
+        list[atomicAdd(&nlist, 1)] = g;
+      else if (rk[x0] >= 0)
+        UU[g] = (uint16_t)rk[x0];
     }
   }
+  if (multi & valid) atomicAdd(&nmulti, __popc(multi & valid));
   __syncthreads();
   const int nl = nlist;
-  for (int e2 = tid; e2 < nl; e2 += PY_T) {
-    const int g = list[e2];
-    int gg = g;
+  if (nl) {  // operands of the scan, re-derived so they are not live across the level loop
+#pragma unroll
+    for (int m = 0; m < M; ++m) a[m] = P.dt * dfi[m];
+    int cc = col;
+#pragma unroll
+    for (int m = 1; m < M; ++m) {
+      xc[m] = cc % D.n[m];
+      cc /= D.n[m];
+    }
+  }
+  // exact scan of the listed targets, the reference loop (HelpFunctions.jl:60-77) for one cell at a
+  // time: every thread evaluates its own N0 sources, then a (value, rank) minimum over the workgroup
+  for (int e2 = 0; e2 < nl; ++e2) {
+    const int l = list[e2];
+    int xl[M];
+    {
+      int gg = l;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        xl[m] = gg % D.n[m];
+        gg /= D.n[m];
+      }
+    }
     double t = 0.0;
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int x = gg % D.n[m];
-      gg /= D.n[m];
-      t = t + a[m] * (double)(D.base[m] + x);
-    }
-    double bv = INFINITY;
-    int ba = -1;
-    double uo1v[M];
+    for (int m = 0; m < M; ++m) t = t + a[m] * (double)(D.base[m] + xl[m]);
+    int dcol = 0;
 #pragma unroll
-    for (int m = 0; m < M; ++m) uo1v[m] = uo1[m];
-    py_brute_target<M>(D, sc, t, g, nullptr, Sin, uo1v, L, cp, &bv, &ba);
-    Sout[g] = bv;
-    if (ba >= 0) UU[g] = (uint16_t)ba;
+    for (int m = 1; m < M; ++m) dcol += abs(xc[m] - xl[m]);
+    double bv = INFINITY;
+    int bj = -1;
+    if (colok) {
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        const double val = (t + beta * (double)(abs(x0 - xl[0]) + dcol)) + psiarr[x0 + N0 * col];
+        if (val < bv) {
+          bv = val;
+          bj = x0 + N0 * col;
+        }
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(bv, off);
+      const int oj = __shfl_xor(bj, off);
+      if (oj >= 0 && (bj < 0 || ov < bv || (ov == bv && oj < bj))) {
+        bv = ov;
+        bj = oj;
+      }
+    }
+    if ((tid & 63) == 0) {
+      scan_v[e2 & 1][tid >> 6] = bv;
+      scan_r[e2 & 1][tid >> 6] = bj;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double v0 = scan_v[e2 & 1][0];
+      int j0 = scan_r[e2 & 1][0];
+#pragma unroll
+      for (int w = 1; w < PY_NW; ++w) {
+        const double ov = scan_v[e2 & 1][w];
+        const int oj = scan_r[e2 & 1][w];
+        if (oj >= 0 && (j0 < 0 || ov < v0 || (ov == v0 && oj < j0))) {
+          v0 = ov;
+          j0 = oj;
+        }
+      }
+      if (j0 >= 0) UU[l] = (uint16_t)j0;
+    }
   }
   PY_STAMP(5);
-  if (tid == 0 && nl) atomicAdd(&counters[1], nl);
+  if (tid == 0 && nl) {
+    atomicAdd(&counters[0], nl - nmulti);
+    if (nmulti) atomicAdd(&counters[1], nmulti);
+  }
 }
 
 // terminal staging row: S_{n-1}[0][l] = T1(l, n-1) if b̃(l, n-1) <= B (HelpFunctions.jl:27-43), rows > 0 Inf
@@ -563,7 +582,8 @@ hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsD
 }
 
 size_t pyr_lds_bytes(const PyrGeom &G) {
-  return (size_t)3 * G.ncol * G.n[0] * sizeof(double) + (size_t)PY_HS * sizeof(unsigned);
+  return (size_t)3 * G.ncol * G.n[0] * sizeof(double) + (size_t)PY_HS * sizeof(unsigned) +
+         (size_t)G.ncol * G.n[0];
 }
 
 hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
@@ -571,10 +591,9 @@ hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
                            int32_t *counters) {
   const dim3 grid(P.B + 1, P.K), blk(PY_T);
   const size_t lds = pyr_lds_bytes(G);
-  const int early_exit = Lv.beta >= 0.0;
 #define PYR_CASE(MM, NN)                                                                                   \
   if (G.M == MM && G.n[0] == NN) {                                                                         \
-    hipLaunchKernelGGL((k_pyr_step<MM, NN>), grid, blk, lds, s, P, Lv, G, i, early_exit, Sin, Sout, UU, s_stride,      \
+    hipLaunchKernelGGL((k_pyr_step<MM, NN>), grid, blk, lds, s, P, Lv, G, i, Sin, Sout, UU, s_stride,      \
                        uu_stride_k, counters);                                                             \
     return hipGetLastError();                                                                              \
   }

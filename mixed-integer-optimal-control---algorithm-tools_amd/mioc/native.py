@@ -33,7 +33,7 @@ EXPORTED = [
     "mioc_version", "mioc_create", "mioc_destroy", "mioc_last_error", "mioc_set_option", "mioc_set_levels",
     "mioc_set_cost", "mioc_bellman", "mioc_backtrack", "mioc_bellman_batch_device",
     "mioc_backtrack_batch_device", "mioc_synchronize", "mioc_stream", "mioc_kernel_stats",
-    "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics",
+    "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics", "mioc_get_argmin_table",
 ]
 
 
@@ -86,6 +86,7 @@ def load_library(path=None):
         "mioc_reset_stats": (i32, [vp]),
         "mioc_last_algo": (i32, [vp]),
         "mioc_diagnostics": (i32, [vp, vp, i32]),
+        "mioc_get_argmin_table": (i32, [vp, i64, i64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -231,8 +232,16 @@ class Context:
     def last_algo(self):
         return self.lib.mioc_last_algo(self.h)
 
+    def argmin_table(self, step, k=0):
+        """U of step `step` in the reference layout: int32 (B+1, Lgrid), rank of the minimising source
+        (mioc_get_argmin_table; cells with Φ = +Inf are -1 below b̃ and unspecified above)."""
+        lg = int(np.prod(self.levels.counts))
+        out = np.empty((lg, self.B + 1), dtype=np.int32)
+        self._check(self.lib.mioc_get_argmin_table(self.h, int(k), int(step), _p(out)))
+        return out.T
+
     def diagnostics(self):
-        """[rows resolved by exact scan, targets resolved by exact scan, p=Inf walk fallbacks, errors]."""
+        """[value-collision targets scanned, multi-level targets scanned, p=Inf walk fallbacks, errors]."""
         out = np.zeros(4, dtype=np.int64)
         self._check(self.lib.mioc_diagnostics(self.h, _p(out), 4))
         return out.tolist()

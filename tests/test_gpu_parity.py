@@ -42,6 +42,17 @@ def _algos(p_kind, lt=None):
     return (native.MIOC_ALGO_GENERIC,)
 
 
+def _assert_U(ctx, U, n, tag):
+    """Every cell of the reference's U table (HelpFunctions.jl:74) that the reference writes equals the
+    device's argmin (mioc_get_argmin_table), step by step."""
+    for i in range(n - 1):
+        d = ctx.argmin_table(i)
+        o = U[:, :, i]
+        m = o >= 0
+        bad = np.argwhere(m & (d != o))
+        assert bad.size == 0, f"{tag} step {i}: (c, g) {bad[:5].tolist()} device {d[m & (d != o)][:5]} ref {o[m & (d != o)][:5]}"
+
+
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
 def test_golden_fixtures(path):
     g = load_golden(path)
@@ -91,6 +102,8 @@ def test_random_vs_oracle(oracle_c, seed):
     for algo in _algos(pk, lt):
         ctx = _ctx(lt, pk, beta, algo)
         ctx.bellman(df, uo, B, dt)
+        if algo != native.MIOC_ALGO_PINF:
+            _assert_U(ctx, U, df.shape[1], f"seed={seed} algo={algo}")
         for Bp in budgets:  # one DP, several budgets: the halving reuse of multi-trust.jl:108-110
             try:
                 ou, ops = oracle_c.backtrack(lv, uo, phi, U, B, Bp)
@@ -264,6 +277,23 @@ def test_error_codes():
     with pytest.raises(native.MiocNativeError) as e:
         ctx.backtrack(0)
     assert e.value.code == native.MIOC_EINFEASIBLE
+    with pytest.raises(native.MiocNativeError) as e:  # U has nt-1 steps
+        ctx.argmin_table(3)
+    assert e.value.code == native.MIOC_EINVAL
+    ctx.close()
+    # the p=Inf collapse keeps class tables, not U
+    ctx = _ctx(lt, P_INF, 0.1, native.MIOC_ALGO_PINF)
+    ctx.bellman(np.ones((1, 4)), np.zeros((1, 4)), 3, 0.1)
+    with pytest.raises(native.MiocNativeError) as e:
+        ctx.argmin_table(0)
+    assert e.value.code == native.MIOC_EINVAL
+    ctx.close()
+    # the L1-ball pyramid is exact only for a non-decreasing switching cost (beta >= 0)
+    lt2 = LevelTable([list(range(4))] * 2)
+    ctx = _ctx(lt2, P_ONE, -0.1, native.MIOC_ALGO_PYRAMID)
+    with pytest.raises(native.MiocNativeError) as e:
+        ctx.bellman(np.ones((2, 4)), np.zeros((2, 4)), 3, 0.1)
+    assert e.value.code == native.MIOC_EINVAL
     ctx.close()
 
 
@@ -304,13 +334,14 @@ def test_pyramid_vs_oracle_512_levels(oracle_c, mode):
     ctx = _ctx(lt, P_ONE, beta, native.MIOC_ALGO_PYRAMID)
     ctx.bellman(df, uo, B, dt)
     diag = ctx.diagnostics()
+    _assert_U(ctx, U, n, mode)
     for Bp in (B, B // 2, 3):
         ou, ops = oracle_c.backtrack(lv, uo, phi, U, B, Bp)
         u, ps, _ = ctx.backtrack(Bp)
         assert np.array_equal(u, ou), f"{mode} Bp={Bp} diag={diag}"
         assert ps == ops
     if mode in ("integer", "zero"):
-        assert diag[0] > 0  # the exact-scan path for rows with tied values was exercised
+        assert diag[0] > 0  # the exact scan for targets whose winning value is tied was exercised
     ctx.close()
 
 
