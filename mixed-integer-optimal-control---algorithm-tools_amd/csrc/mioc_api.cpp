@@ -87,7 +87,7 @@ void free_all(mioc_ctx *ctx) {
                   ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
-                  ctx->d_status_own, ctx->d_stage,    ctx->d_counters};
+                  ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (ctx->h_flags) hipHostFree(ctx->h_flags);
@@ -222,11 +222,14 @@ int run_bellman(mioc_ctx *ctx) {
     const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
     rc = grow(ctx, &ctx->d_U, &ctx->U_cap, K * uu_stride_k * sizeof(uint16_t), "argmin table U");
     if (rc) return rc;
+    rc = grow(ctx, &ctx->d_perm, &ctx->perm_cap, K * nt * L * sizeof(uint32_t), "sphere orders");
+    if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
-    HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, st[(nt - 1) & 1], s_stride));
+    HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm));
+    HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, st[(nt - 1) & 1], s_stride));
     ev_begin(ctx, 0, "k_pyr_step");
     for (int i = ctx->nt - 2; i >= 0; --i)
-      HIP_TRY(ctx, launch_pyr_step(ctx->stream, P, Lv, ctx->pyr, i, st[(i + 1) & 1], st[i & 1],
+      HIP_TRY(ctx, launch_pyr_step(ctx->stream, P, Lv, ctx->pyr, i, ctx->d_perm, st[(i + 1) & 1], st[i & 1],
                                    (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters));
     ev_end(ctx, 0, ctx->nt - 1);
   } else if (algo == MIOC_ALGO_GENERIC) {
@@ -287,7 +290,7 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
   if (ctx->algo == MIOC_ALGO_PYRAMID) {
     const size_t s_stride = (size_t)(ctx->B + 1) * ctx->L;
     const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
-    HIP_TRY(ctx, launch_stage_argmin0(ctx->stream, P, Lv, ctx->d_stage, s_stride, (int)B_use, ctx->d_start));
+    HIP_TRY(ctx, launch_stage_argmin0(ctx->stream, P, Lv, ctx->d_perm, ctx->d_stage, s_stride, (int)B_use, ctx->d_start));
     ev_begin(ctx, 1, "k_stage_walk");
     HIP_TRY(ctx, launch_stage_walk(ctx->stream, P, Lv, (const uint16_t *)ctx->d_U, uu_stride_k, ctx->d_start,
                                    ctx->d_ranks));

@@ -416,23 +416,24 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
 }
 
 // ---------------------------------------------------------------------------------------------
-// staging layout (pyramid path): Φ_0[l, c] = S_0[c - b̃_l(0)][l],  U_i[l, c] = UU_i[c - b̃_l(i)][l]
+// staging layout (pyramid path): Φ_0[l, c] = S_0[c - b̃_l(0)][pos_0(l)] (rows in sphere order of u_old(0)),
+// U_i[l, c] = UU_i[c - b̃_l(i)][l]
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_stage_argmin0(ProblemDev P, LevelsDev Lv, const double *S0_all,
-                                                        size_t s_stride, int Bu, Start *start) {
-  const int k = blockIdx.x, L = Lv.L, M = P.M;
+__global__ __launch_bounds__(1024) void k_stage_argmin0(ProblemDev P, LevelsDev Lv, const uint32_t *perm_all,
+                                                        const double *S0_all, size_t s_stride, int Bu, Start *start) {
+  const int k = blockIdx.x, L = Lv.L;
   const double *S0 = S0_all + (size_t)k * s_stride;
-  const double *uo0 = P.uold + (size_t)k * P.nt * M;
+  const uint32_t *perm = perm_all + (size_t)k * P.nt * L;  // sphere order of u_old(0): rank | b̃ << 16
   ArgKey best;
   best.v = ~0ull;
   best.pos = ~0ull;
   best.val = INFINITY;
   best.r = -1;
   best.c = 0;
-  for (int r = threadIdx.x; r < L; r += blockDim.x) {
-    const int b = bt_of(Lv.nuval + (size_t)r * M, uo0, M);
+  for (int p = threadIdx.x; p < L; p += blockDim.x) {
+    const int r = (int)(perm[p] & 0xFFFFu), b = (int)(perm[p] >> 16);
     for (int c = b; c <= Bu; ++c) {  // first minimum over c for this l, then (value, grid index, c)
-      const double v = S0[(size_t)(c - b) * L + r];
+      const double v = S0[(size_t)(c - b) * L + p];
       ArgKey a;
       a.v = jl_key(v);
       a.pos = ((uint64_t)(uint32_t)Lv.gidx[r] << 32) | (uint32_t)c;
@@ -454,9 +455,9 @@ __global__ __launch_bounds__(1024) void k_stage_argmin0(ProblemDev P, LevelsDev 
   }
 }
 
-hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const double *S0,
-                                size_t s_stride, int Bu, Start *start) {
-  hipLaunchKernelGGL(k_stage_argmin0, dim3(P.K), dim3(1024), 0, s, P, Lv, S0, s_stride, Bu, start);
+hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
+                                const double *S0, size_t s_stride, int Bu, Start *start) {
+  hipLaunchKernelGGL(k_stage_argmin0, dim3(P.K), dim3(1024), 0, s, P, Lv, perm, S0, s_stride, Bu, start);
   return hipGetLastError();
 }
 

@@ -75,13 +75,15 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
                          const int32_t *ranks, double *u_out, double *phi_star, int32_t *status);
 
 // ---- L1-ball pyramid (mioc_pyramid.hip) + staging-layout backtrack (mioc_generic.hip) -------------
-hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, double *S, size_t s_stride);
+hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm);
+hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm, double *S,
+                               size_t s_stride);
 hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
-                           const double *Sin, double *Sout, uint16_t *UU, size_t s_stride, size_t uu_stride_k,
-                           int32_t *counters);
+                           const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
+                           size_t uu_stride_k, int32_t *counters);
 size_t pyr_lds_bytes(const PyrGeom &G);
-hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const double *S0,
-                                size_t s_stride, int Bu, Start *start);
+hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
+                                const double *S0, size_t s_stride, int Bu, Start *start);
 hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,
                              size_t uu_stride_k, const Start *start, int32_t *ranks);
 
@@ -147,8 +149,10 @@ struct mioc_ctx {
   // pyramid (p = 1, product grid, unit gaps)
   bool pyr_ok = false;
   mioc::PyrGeom pyr;
-  double *d_stage = nullptr;       // [2][K][B+1][L] source-row-major fronts
+  double *d_stage = nullptr;       // [2][K][B+1][L] source-row-major fronts, each row in sphere order
   size_t stage_cap = 0;
+  uint32_t *d_perm = nullptr;      // [K][nt][L] sphere order of u_old(i): rank | (L1 distance << 16)
+  size_t perm_cap = 0;
   int32_t *d_counters = nullptr;   // [8] diagnostics: value-collision targets, multi-level targets, ...
 
   // generic buffers

@@ -144,6 +144,7 @@ __device__ __forceinline__ bool py_any(bool f, int *slots) {
 
 template <int M, int N0>
 __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i,
+                                                   const uint32_t *__restrict__ perm_all,
                                                    const double *__restrict__ Sin_all, double *__restrict__ Sout_all,
                                                    uint16_t *__restrict__ UU_all, size_t s_stride, size_t uu_stride_k,
                                                    int32_t *__restrict__ counters) {
@@ -171,7 +172,6 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   uint16_t *UU = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L) + (size_t)cp * L;
   const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
   const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
-  const double *uo1 = P.uold + ((size_t)k * P.nt + i + 1) * M;
   double *lvl = reinterpret_cast<double *>(pys);                             // [2][L] level buffers
   double *psiarr = lvl + (size_t)2 * L;                                      // [L] Ψ_j by rank j
   unsigned *htab = reinterpret_cast<unsigned *>(psiarr + L);                 // [PY_HS] bucket hash
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
 #pragma unroll
   for (int m = 0; m < M; ++m) a[m] = P.dt * dfi[m];
   int xc[M];
-  int bcl = 0, bcs = 0, nbm = 0;
+  int bcl = 0, nbm = 0;
   xc[0] = 0;
   {
     int cc = col;
@@ -197,25 +197,54 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       const double nu = (double)(D.base[m] + xm);
       pc[m] = a[m] * nu;
       bcl += (int)fabs(nu - uoi[m]);
-      bcs += (int)fabs(nu - uo1[m]);
       nbm |= (xm > 0 ? 1 : 0) << (2 * m);
       nbm |= (xm + 1 < D.n[m] ? 1 : 0) << (2 * m + 1);
     }
   }
-  const double u00 = uoi[0], u10 = uo1[0];
+  const double u00 = uoi[0];
 
-  // ---- own points: targets (T1, validity) and sources (Ψ); all N0 gathers issued together --------
+  // ---- sources: Ψ_j = Φ_{i+1}[j, c'] = S_{i+1}[c' - b̃_j(i+1)][pos(j)].  Rows are stored in the sphere
+  // order of u_old(i+1), so thread t reads positions N0·t .. N0·t+N0-1 -- one contiguous run of a
+  // row for all positions of one sphere -- and scatters them into Ψ-by-rank (psiarr) in LDS ----------
+  const uint32_t *pin = perm_all + ((size_t)k * P.nt + i + 1) * L;
+  const uint32_t *pout = perm_all + ((size_t)k * P.nt + i) * L;
+  if (colok) {
+    uint32_t e[N0];
+    const uint4 *p4 = reinterpret_cast<const uint4 *>(pin + N0 * col);
+#pragma unroll
+    for (int c = 0; c < N0 / 4; ++c) {
+      const uint4 t = p4[c];
+      e[4 * c] = t.x;
+      e[4 * c + 1] = t.y;
+      e[4 * c + 2] = t.z;
+      e[4 * c + 3] = t.w;
+    }
+    double v[N0];
+#pragma unroll
+    for (int q = 0; q < N0; ++q) {
+      const int row = cp - (int)(e[q] >> 16);
+      v[q] = Sin[(size_t)(row >= 0 ? row : 0) * L + N0 * col + q];
+      if (row < 0) v[q] = INFINITY;
+    }
+#pragma unroll
+    for (int q = 0; q < N0; ++q) psiarr[e[q] & 0xFFFFu] = v[q];
+  }
+  __syncthreads();
+  // ---- own points: targets (T1, validity) and sources (Ψ) -----------------------------------------
   // invalid targets carry T1 = +Inf and best = -Inf, so the level loop needs no branches
   double cur[N0], T1[N0];
   unsigned valid = 0, fin = 0;
+  if (colok) {
+    const double2 *p2 = reinterpret_cast<const double2 *>(psiarr + N0 * col);
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {
-    const double nu0 = (double)(D.base[0] + x0);
-    const int bs = (int)fabs(nu0 - u10) + bcs;
-    const int row = cp - bs;
-    const bool ok = colok && row >= 0;
-    cur[x0] = Sin[(size_t)(ok ? row : 0) * L + x0 + N0 * col];
-    if (!ok) cur[x0] = INFINITY;
+    for (int c = 0; c < N0 / 2; ++c) {
+      const double2 t = p2[c];
+      cur[2 * c] = t.x;
+      cur[2 * c + 1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) cur[x0] = INFINITY;
   }
 #pragma unroll
   for (int x0 = 0; x0 < N0; ++x0) {
@@ -285,11 +314,6 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     uint4 *h4 = reinterpret_cast<uint4 *>(htab);
     for (int s2 = tid; s2 < PY_HS / 4; s2 += PY_T) h4[s2] = make_uint4(0u, 0u, 0u, 0u);
     for (int s2 = tid; s2 < L; s2 += PY_T) coll[s2] = 0;
-    if (colok) {
-      double2 *p2 = reinterpret_cast<double2 *>(psiarr + N0 * col);
-#pragma unroll
-      for (int c = 0; c < N0 / 2; ++c) p2[c] = make_double2(cur[2 * c], cur[2 * c + 1]);
-    }
   }
   if (tid == 0) {
     nlist = 0;
@@ -458,21 +482,53 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       rk[x0] = py_find_value(htab, psiarr, py_next(lslot[x0]), ltag[x0], bmb[x0]);
     if (rk[x0] < 0 || coll[rk[x0]]) tolist |= 1u << x0;
   }
-  __syncthreads();  // the level buffers are free: the list lives there
+  __syncthreads();  // the level buffers are free: the list and the natural-order outputs live there
   int *list = reinterpret_cast<int *>(lvl);
+  double *outnat = lvl + L;
   if (colok) {
+    double2 *o2 = reinterpret_cast<double2 *>(outnat + N0 * col);
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
-      const int g = x0 + N0 * col;
-      Sout[g] = (valid >> x0 & 1) ? best[x0] : INFINITY;
-      if (tolist >> x0 & 1)
-        list[atomicAdd(&nlist, 1)] = g;
-      else if (rk[x0] >= 0)
-        UU[g] = (uint16_t)rk[x0];
+    for (int c = 0; c < N0 / 2; ++c)
+      o2[c] = make_double2((valid >> (2 * c) & 1) ? best[2 * c] : INFINITY,
+                           (valid >> (2 * c + 1) & 1) ? best[2 * c + 1] : INFINITY);
+    if (!tolist) {  // U row in natural order: one N0·2-byte store (cells with Φ = +Inf are unspecified)
+      uint32_t w[N0 / 2];
+#pragma unroll
+      for (int c = 0; c < N0 / 2; ++c)
+        w[c] = (uint32_t)(uint16_t)rk[2 * c] | ((uint32_t)(uint16_t)rk[2 * c + 1] << 16);
+      if constexpr (N0 == 8)
+        *reinterpret_cast<uint4 *>(UU + N0 * col) = make_uint4(w[0], w[1], w[2], w[3]);
+      else
+        *reinterpret_cast<uint2 *>(UU + N0 * col) = make_uint2(w[0], w[1]);
+    } else {
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        const int g = x0 + N0 * col;
+        if (tolist >> x0 & 1)
+          list[atomicAdd(&nlist, 1)] = g;
+        else if (rk[x0] >= 0)
+          UU[g] = (uint16_t)rk[x0];
+      }
     }
   }
   if (multi & valid) atomicAdd(&nmulti, __popc(multi & valid));
   __syncthreads();
+  // Φ_i row c' in the sphere order of u_old(i): gathered from LDS, written as one contiguous run
+  if (colok) {
+    const uint4 *p4 = reinterpret_cast<const uint4 *>(pout + N0 * col);
+    double o[N0];
+#pragma unroll
+    for (int c = 0; c < N0 / 4; ++c) {
+      const uint4 t = p4[c];
+      o[4 * c] = outnat[t.x & 0xFFFFu];
+      o[4 * c + 1] = outnat[t.y & 0xFFFFu];
+      o[4 * c + 2] = outnat[t.z & 0xFFFFu];
+      o[4 * c + 3] = outnat[t.w & 0xFFFFu];
+    }
+    double2 *s2 = reinterpret_cast<double2 *>(Sout + N0 * col);
+#pragma unroll
+    for (int c = 0; c < N0 / 2; ++c) s2[c] = make_double2(o[2 * c], o[2 * c + 1]);
+  }
   const int nl = nlist;
   if (nl) {  // operands of the scan, re-derived so they are not live across the level loop
 #pragma unroll
@@ -551,33 +607,80 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   }
 }
 
-// terminal staging row: S_{n-1}[0][l] = T1(l, n-1) if b̃(l, n-1) <= B (HelpFunctions.jl:27-43), rows > 0 Inf
-__global__ void k_pyr_terminal(ProblemDev P, LevelsDev Lv, double *S_all, size_t s_stride) {
+// Sphere order of u_old(i) for every step (one workgroup per (step, subproblem)): the ranks j grouped by
+// their L1 distance b̃_j(i) = Σ_m |ν_jm - u_old[m,i]| (HelpFunctions.jl:53-57), perm[p] = j | b̃_j << 16.
+// Staging rows of step i are stored in this order, so the L sources a workgroup of step i-1 reads from
+// row c' - s of S_i (the sphere s) form one contiguous run per sphere.  The order inside a sphere is
+// whatever the LDS atomics produce: producer and consumer read the same table.
+__global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all) {
+  __shared__ int hist[64];
+  const int i = blockIdx.x, k = blockIdx.y, L = G.ncol * G.n[0], M = G.M;
+  const double *uo = P.uold + ((size_t)k * P.nt + i) * M;
+  uint32_t *perm = perm_all + ((size_t)k * P.nt + i) * L;
+  int u[kMaxM];
+#pragma unroll
+  for (int m = 0; m < kMaxM; ++m) u[m] = m < M ? (int)uo[m] : 0;
+  if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+  __syncthreads();
+  auto dist = [&](int j) {
+    int d = 0;
+    for (int m = 0; m < M; ++m) {
+      const int x = j % G.n[m];
+      j /= G.n[m];
+      d += abs(G.base[m] + x - u[m]);
+    }
+    return min(d, 0xFFFF);
+  };
+  for (int j = threadIdx.x; j < L; j += blockDim.x) atomicAdd(&hist[min(dist(j), 63)], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int b = 0; b < 64; ++b) {
+      const int c = hist[b];
+      hist[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < L; j += blockDim.x) {
+    const int d = dist(j);
+    perm[atomicAdd(&hist[min(d, 63)], 1)] = (uint32_t)j | ((uint32_t)d << 16);
+  }
+}
+
+hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm) {
+  hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm);
+  return hipGetLastError();
+}
+
+// terminal staging row: S_{n-1}[0][pos(l)] = T1(l, n-1) if b̃(l, n-1) <= B (HelpFunctions.jl:27-43),
+// rows > 0 Inf
+__global__ void k_pyr_terminal(ProblemDev P, LevelsDev Lv, const uint32_t *perm_all, double *S_all,
+                               size_t s_stride) {
   const int k = blockIdx.y;
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t n = (size_t)(P.B + 1) * Lv.L;
   if (idx >= n) return;
-  const int cp = (int)(idx / Lv.L), l = (int)(idx % Lv.L);
+  const int cp = (int)(idx / Lv.L), p = (int)(idx % Lv.L);
   const int i = P.nt - 1, M = P.M;
   double v = INFINITY;
   if (cp == 0) {
+    const uint32_t e = perm_all[((size_t)k * P.nt + i) * Lv.L + p];
+    const int l = (int)(e & 0xFFFFu), b = (int)(e >> 16);
     const double *nuv = Lv.nuval + (size_t)l * M;
     const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
-    const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
     double t = 0.0;
-    int b = 0;
-    for (int m = 0; m < M; ++m) {
-      t = t + (P.dt * dfi[m]) * nuv[m];
-      b += (int)fabs(nuv[m] - uoi[m]);
-    }
+    for (int m = 0; m < M; ++m) t = t + (P.dt * dfi[m]) * nuv[m];
     if (b <= P.B) v = t;
   }
   S_all[(size_t)k * s_stride + idx] = v;
 }
 
-hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, double *S, size_t s_stride) {
+hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm, double *S,
+                               size_t s_stride) {
   const size_t n = (size_t)(P.B + 1) * Lv.L;
-  hipLaunchKernelGGL(k_pyr_terminal, dim3((unsigned)((n + 255) / 256), P.K), dim3(256), 0, s, P, Lv, S, s_stride);
+  hipLaunchKernelGGL(k_pyr_terminal, dim3((unsigned)((n + 255) / 256), P.K), dim3(256), 0, s, P, Lv, perm, S,
+                     s_stride);
   return hipGetLastError();
 }
 
@@ -587,13 +690,13 @@ size_t pyr_lds_bytes(const PyrGeom &G) {
 }
 
 hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
-                           const double *Sin, double *Sout, uint16_t *UU, size_t s_stride, size_t uu_stride_k,
-                           int32_t *counters) {
+                           const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
+                           size_t uu_stride_k, int32_t *counters) {
   const dim3 grid(P.B + 1, P.K), blk(PY_T);
   const size_t lds = pyr_lds_bytes(G);
 #define PYR_CASE(MM, NN)                                                                                   \
   if (G.M == MM && G.n[0] == NN) {                                                                         \
-    hipLaunchKernelGGL((k_pyr_step<MM, NN>), grid, blk, lds, s, P, Lv, G, i, Sin, Sout, UU, s_stride,      \
+    hipLaunchKernelGGL((k_pyr_step<MM, NN>), grid, blk, lds, s, P, Lv, G, i, perm, Sin, Sout, UU, s_stride,      \
                        uu_stride_k, counters);                                                             \
     return hipGetLastError();                                                                              \
   }
