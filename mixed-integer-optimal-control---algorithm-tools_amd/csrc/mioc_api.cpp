@@ -615,12 +615,12 @@ int32_t mioc_last_algo(mioc_ctx *ctx) { return ctx ? ctx->algo : MIOC_EINVAL; }
 int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
   if (!ctx || !counters || n < 0) return MIOC_EINVAL;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  int32_t c[4] = {0, 0, 0, 0}, f[4] = {0, 0, 0, 0};
+  int32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f[4] = {0, 0, 0, 0};
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->d_counters) HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
   HIP_TRY(ctx, hipMemcpy(f, ctx->d_flags, sizeof f, hipMemcpyDeviceToHost));
-  const int64_t all[4] = {c[0], c[1], f[2], f[3]};
-  for (int32_t q = 0; q < n && q < 4; ++q) counters[q] = all[q];
+  const int64_t all[8] = {c[0], c[1], f[2], f[3], c[4], c[5], c[6], c[7]};
+  for (int32_t q = 0; q < n && q < 8; ++q) counters[q] = all[q];
   return MIOC_OK;
 }
 

@@ -29,6 +29,7 @@ namespace mioc {
 constexpr int PY_T = 512;          // threads per workgroup: one grid column (dim-0 run) per thread
 constexpr int PY_NW = PY_T / 64;   // waves per workgroup
 constexpr int PY_HS = 12288;       // hash slots (uint32): <= 4096 sources, load <= 1/3
+constexpr int PY_NB = PY_HS / 4;   // 16-byte buckets of 4 slots; every key may live in one of two
 constexpr int PY_G = 8;            // bucket width = 2^PY_G · δ
 constexpr unsigned PY_RB = 13;     // hash entry = tag << PY_RB | (rank + 1); 0 = empty
 
@@ -42,7 +43,7 @@ __device__ __forceinline__ double vmin(double a, double b) {
 
 // Diagnostic build only (make stamps -> libmioc_stamps.so): per-workgroup phase clocks of the last launch.
 #ifdef MIOC_STAMPS
-__device__ unsigned long long g_pyr_stamps[4096][8];
+__device__ unsigned long long g_pyr_stamps[4096][16];
 #define PY_STAMP(k)                                                                          \
   do {                                                                                       \
     if (threadIdx.x == 0) g_pyr_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();         \
@@ -53,61 +54,98 @@ __device__ unsigned long long g_pyr_stamps[4096][8];
   } while (0)
 #endif
 
-// Bucket hash.  A bucket is an integer-valued double fq = floor(Ψ·2^k) (+0.0, so -0 and +0 agree); the
-// slot comes from the high bits of a 32-bit mix of its bit pattern, a 19-bit tag from the low bits.
-// A tag match is confirmed against the exact bucket kept per rank in LDS (keyarr), so false matches
-// only cost a probe.
-__device__ __forceinline__ void py_hslot(double fq, unsigned &slot, unsigned &tag) {
-  const unsigned long long u = (unsigned long long)__double_as_longlong(fq);
-  unsigned h = (unsigned)u * 0x9E3779B1u + (unsigned)(u >> 32) * 0x85EBCA77u;
-  h ^= h >> 15;
-  h *= 0x2C1B3C6Du;
-  h ^= h >> 12;
-  slot = __umulhi(h, (unsigned)PY_HS);
-  tag = h & ((1u << (32 - PY_RB)) - 1);
+// Bucket hash (bucketized two-choice).  A bucket of Ψ values is an integer-valued double fq = floor(Ψ·2^k)
+// (+0.0, so -0 and +0 agree).  Its key may sit in any of the 4 slots of two 16-byte hash buckets; a slot
+// holds tag << PY_RB | (rank + 1).  Every probe is one or two ds_read_b128, with no chains.  A tag match
+// is confirmed against the exact Ψ of that rank (psiarr), so false matches cost one read.
+struct PyKey {
+  unsigned b1, b2, tag;
+};
+__device__ __forceinline__ PyKey py_key(double fq) {
+  unsigned long long x = (unsigned long long)__double_as_longlong(fq);  // splitmix64 finaliser
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const unsigned lo = (unsigned)x, hi = (unsigned)(x >> 32);
+  PyKey k;
+  k.b1 = __umulhi(lo, (unsigned)PY_NB);
+  k.b2 = __umulhi(hi, (unsigned)PY_NB);
+  if (k.b2 == k.b1) k.b2 = k.b1 + 1 == (unsigned)PY_NB ? 0u : k.b1 + 1;
+  k.tag = lo & ((1u << (32 - PY_RB)) - 1);
+  return k;
 }
-__device__ __forceinline__ unsigned py_next(unsigned s) { return s + 1 == (unsigned)PY_HS ? 0u : s + 1; }
+__device__ __forceinline__ int py_erank(unsigned e) { return (int)(e & ((1u << PY_RB) - 1)) - 1; }
+__device__ __forceinline__ unsigned py_slot(const uint4 &b, int s) {
+  return s == 0 ? b.x : s == 1 ? b.y : s == 2 ? b.z : b.w;
+}
+__device__ __forceinline__ bool py_full(const uint4 &b) { return b.x && b.y && b.z && b.w; }
+__device__ __forceinline__ unsigned py_nextb(unsigned b) { return b + 1 == (unsigned)PY_NB ? 0u : b + 1; }
+
+__device__ __forceinline__ double py_bucket(double v, double inv_w) { return floor(v * inv_w) + 0.0; }
+
+// Overflow chain: a key whose two buckets were both full lives in the first bucket after b2 that had a
+// free slot.  Buckets only fill up, so a scan from b2+1 that stops at the first non-full bucket has
+// passed every such key.  All chain walks are cold paths, kept out of line.
+__device__ __noinline__ unsigned py_chain_free(const uint4 *tab4, unsigned b2) {
+  for (unsigned b = py_nextb(b2);; b = py_nextb(b)) {
+    const uint4 t = tab4[b];
+    if (!py_full(t)) return b * 4 + (!t.x ? 0 : !t.y ? 1 : !t.z ? 2 : 3);
+  }
+}
+
+// Mark every source other than `self` whose entry (in the two buckets of `key`, and on its chain when
+// both are full) holds bucket fq; true if there was one.
+__device__ __noinline__ bool py_mark_key(const uint4 *tab4, const double *psiarr, unsigned char *coll, PyKey key,
+                                         double fq, double inv_w, int self) {
+  bool found = false;
+  const uint4 b1 = tab4[key.b1], b2 = tab4[key.b2];
+  const bool chain = py_full(b1) && py_full(b2);
+  unsigned b = key.b1;
+  for (int n = 0;; ++n) {
+    const uint4 t = n == 0 ? b1 : n == 1 ? b2 : tab4[b];
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const unsigned e = py_slot(t, s2);
+      const int r = py_erank(e);
+      if (e != 0u && (e >> PY_RB) == key.tag && r != self && py_bucket(psiarr[r], inv_w) == fq) {
+        coll[r] = 1;
+        found = true;
+      }
+    }
+    if (n == 0) continue;
+    if (n == 1) {
+      if (!chain) return found;
+      b = key.b2;
+    } else if (!py_full(t)) {
+      return found;
+    }
+    b = py_nextb(b);
+  }
+}
+
+// First source (two buckets, then the chain) whose entry carries `tag` and whose Ψ equals v; -1 if none.
+__device__ __noinline__ int py_find_key(const uint4 *tab4, const double *psiarr, PyKey key, double v) {
+  const uint4 b1 = tab4[key.b1], b2 = tab4[key.b2];
+  const bool chain = py_full(b1) && py_full(b2);
+  unsigned b = key.b2;
+  for (int n = 0;; ++n) {
+    const uint4 t = n == 0 ? b1 : n == 1 ? b2 : tab4[b];
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const unsigned e = py_slot(t, s2);
+      if (e != 0u && (e >> PY_RB) == key.tag && psiarr[py_erank(e)] == v) return py_erank(e);
+    }
+    if (n == 0) continue;
+    if (n == 1 && !chain) return -1;
+    if (n >= 2 && !py_full(t)) return -1;
+    b = py_nextb(b);
+  }
+}
 
 struct PyrDims {  // geometry copied by value into registers (never escapes to memory)
   int n[kMaxM];
   int base[kMaxM];
 };
-
-__device__ __forceinline__ double py_bucket(double v, double inv_w) { return floor(v * inv_w) + 0.0; }
-
-// Mark every source holding bucket fq as colliding (and report whether there was one).
-__device__ __forceinline__ bool py_mark_bucket(const unsigned *htab, const double *psiarr, unsigned char *coll,
-                                               double fq, double inv_w) {
-  unsigned s, tag;
-  py_hslot(fq, s, tag);
-  bool found = false;
-  for (;;) {
-    const unsigned e = htab[s];
-    if (e == 0u) return found;
-    if ((e >> PY_RB) == tag) {
-      const int r = (int)(e & ((1u << PY_RB) - 1)) - 1;
-      if (py_bucket(psiarr[r], inv_w) == fq) {
-        coll[r] = 1;
-        found = true;
-      }
-    }
-    s = py_next(s);
-  }
-}
-
-// First source (probe order) whose Ψ equals v exactly, starting the walk at slot s; -1 if none.
-__device__ __forceinline__ int py_find_value(const unsigned *htab, const double *psiarr, unsigned s, unsigned tag,
-                                             double v) {
-  for (;;) {
-    const unsigned e = htab[s];
-    if (e == 0u) return -1;
-    if ((e >> PY_RB) == tag) {
-      const int r = (int)(e & ((1u << PY_RB) - 1)) - 1;
-      if (psiarr[r] == v) return r;
-    }
-    s = py_next(s);
-  }
-}
 
 // A column (N0 doubles = N0/2 16-byte chunks) is stored with its chunks XOR-swizzled by the column's
 // position inside a 256-byte LDS row, so the 16 lanes of every ds_read_b128 / ds_write_b128 lane group
@@ -156,7 +194,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   __shared__ int vote[2][PY_NW];        // per-wave early-exit votes, double-buffered by level parity
   __shared__ double scan_v[2][PY_NW];   // exact-scan reductions, double-buffered by list position parity
   __shared__ int scan_r[2][PY_NW];
-  __shared__ int nlist, nmulti;
+  __shared__ int nlist, nmulti, ovf;
   PyrDims D;
 #pragma unroll
   for (int m = 0; m < kMaxM; ++m) {
@@ -318,50 +356,87 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   if (tid == 0) {
     nlist = 0;
     nmulti = 0;
+    ovf = 0;
   }
   PY_STAMP(2);
   __syncthreads();
+  PY_STAMP(7);
+  const uint4 *tab4 = reinterpret_cast<const uint4 *>(htab);
   {
-    unsigned slot[N0], ent[N0];
+    PyKey key[N0];
+    unsigned ent[N0], tslot[N0];
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
-      unsigned tg;
-      py_hslot(fq[x0], slot[x0], tg);
-      ent[x0] = tg << PY_RB | (unsigned)(x0 + N0 * col + 1);
+      key[x0] = py_key(fq[x0]);
+      ent[x0] = key[x0].tag << PY_RB | (unsigned)(x0 + N0 * col + 1);
+      tslot[x0] = 0;
     }
-    unsigned pend = fin, hit = 0;
+    // insert into the emptier of the two buckets; a lost race re-reads both and tries again
+    unsigned pend = fin;
     while (pend) {
-      unsigned old[N0];
+      uint4 bk[N0][2];
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) old[x0] = (pend >> x0 & 1) ? atomicCAS(&htab[slot[x0]], 0u, ent[x0]) : 0u;
+      for (int x0 = 0; x0 < N0; ++x0)
+        if (pend >> x0 & 1) {
+          bk[x0][0] = tab4[key[x0].b1];
+          bk[x0][1] = tab4[key[x0].b2];
+        }
 #pragma unroll
       for (int x0 = 0; x0 < N0; ++x0) {
         if (!(pend >> x0 & 1)) continue;
-        const unsigned o = old[x0];
-        if (o == 0u) {
-          pend &= ~(1u << x0);
+        int e1 = 0, e2 = 0, f1 = -1, f2 = -1;
+#pragma unroll
+        for (int s2 = 3; s2 >= 0; --s2) {
+          if (py_slot(bk[x0][0], s2) == 0u) ++e1, f1 = s2;
+          if (py_slot(bk[x0][1], s2) == 0u) ++e2, f2 = s2;
+        }
+        if (e1 + e2 == 0) {  // both buckets full: the first bucket after b2 with a free slot (rare)
+          ovf = 1;
+          tslot[x0] = py_chain_free(tab4, key[x0].b2);
           continue;
         }
-        if ((o >> PY_RB) == (ent[x0] >> PY_RB)) {
-          const int r = (int)(o & ((1u << PY_RB) - 1)) - 1;
-          if (py_bucket(psiarr[r], inv_w) == fq[x0]) {  // two Ψ in one bucket
-            coll[r] = 1;
-            hit |= 1u << x0;
-          }
-        }
-        slot[x0] = py_next(slot[x0]);
+        tslot[x0] = e1 >= e2 ? key[x0].b1 * 4 + f1 : key[x0].b2 * 4 + f2;
       }
-    }
-    __syncthreads();  // every value is in the table
+      unsigned old[N0];
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {  // close to a bucket border: the neighbouring bucket too
+      for (int x0 = 0; x0 < N0; ++x0) old[x0] = (pend >> x0 & 1) ? atomicCAS(&htab[tslot[x0]], 0u, ent[x0]) : 1u;
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0)
+        if (old[x0] == 0u) pend &= ~(1u << x0);
+    }
+    PY_STAMP(8);
+    __syncthreads();  // every value is in the table
+    PY_STAMP(9);
+    // another source in my bucket (exact duplicates included), or close across a bucket border
+    unsigned hit = 0;
+    uint4 bk[N0][2];
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0)
+      if (fin >> x0 & 1) {
+        bk[x0][0] = tab4[key[x0].b1];
+        bk[x0][1] = tab4[key[x0].b2];
+      }
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) {
       if (!(fin >> x0 & 1)) continue;
-      if (fr[x0] <= FR && py_mark_bucket(htab, psiarr, coll, fq[x0] - 1.0, inv_w)) hit |= 1u << x0;
-      if (fr[x0] >= 1.0 - FR && py_mark_bucket(htab, psiarr, coll, fq[x0] + 1.0, inv_w)) hit |= 1u << x0;
+      const int me = x0 + N0 * col;
+      bool dup = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const unsigned e = py_slot(bk[x0][h], s2);
+          dup |= e != 0u && (e >> PY_RB) == key[x0].tag && py_erank(e) != me;
+        }
+      dup |= py_full(bk[x0][0]) && py_full(bk[x0][1]);
+      if (dup && py_mark_key(tab4, psiarr, coll, key[x0], fq[x0], inv_w, me)) hit |= 1u << x0;
+      if (fr[x0] <= FR && py_mark_key(tab4, psiarr, coll, py_key(fq[x0] - 1.0), fq[x0] - 1.0, inv_w, me)) hit |= 1u << x0;
+      if (fr[x0] >= 1.0 - FR && py_mark_key(tab4, psiarr, coll, py_key(fq[x0] + 1.0), fq[x0] + 1.0, inv_w, me)) hit |= 1u << x0;
     }
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0)
       if (hit >> x0 & 1) coll[x0 + N0 * col] = 1;
+    if (hit) atomicAdd(&counters[6], __popc(hit));
   }
   PY_STAMP(3);
 
@@ -445,43 +520,50 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
 #endif
 
   // ---- argmin.  A target whose minimum is reached at one level only, by a value with no close
-  // neighbour, has a unique minimiser: the source holding that value (lock-step hash probes).  Every
+  // neighbour, has a unique minimiser: the source holding that value (one bucket-pair read).  Every
   // other target with a finite minimum goes to the exact scan below. --------------------------------
-  unsigned lpend = 0, lslot[N0], ltag[N0];
   int rk[N0];
-  const unsigned fin_t = valid & ~multi;
+  unsigned want = 0;
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {
-    rk[x0] = -1;
-    py_hslot(py_bucket(bmb[x0], inv_w), lslot[x0], ltag[x0]);
-    lpend |= (unsigned)((fin_t >> x0 & 1) && best[x0] < INFINITY) << x0;
-  }
-  const unsigned want = lpend;
-  while (lpend) {
-    unsigned e[N0];
-#pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) e[x0] = (lpend >> x0 & 1) ? htab[lslot[x0]] : 0u;
+  for (int x0 = 0; x0 < N0; ++x0) want |= (unsigned)((valid >> x0 & 1) && !(multi >> x0 & 1) && best[x0] < INFINITY) << x0;
+  {
+    PyKey key[N0];
+    uint4 bk[N0][2];
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
-      if (!(lpend >> x0 & 1)) continue;
-      if (e[x0] == 0u) {
-        lpend &= ~(1u << x0);
-      } else if ((e[x0] >> PY_RB) == ltag[x0]) {
-        rk[x0] = (int)(e[x0] & ((1u << PY_RB) - 1)) - 1;  // confirmed below
-        lpend &= ~(1u << x0);
-      } else {
-        lslot[x0] = py_next(lslot[x0]);
+      rk[x0] = -1;
+      if (want >> x0 & 1) {
+        key[x0] = py_key(py_bucket(bmb[x0], inv_w));
+        bk[x0][0] = tab4[key[x0].b1];
+        bk[x0][1] = tab4[key[x0].b2];
       }
     }
-  }
-  unsigned tolist = valid & multi;
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {  // confirm against the exact value (one batch of reads), then the flag
-    if (!(want >> x0 & 1)) continue;
-    if (rk[x0] >= 0 && psiarr[rk[x0]] != bmb[x0])
-      rk[x0] = py_find_value(htab, psiarr, py_next(lslot[x0]), ltag[x0], bmb[x0]);
-    if (rk[x0] < 0 || coll[rk[x0]]) tolist |= 1u << x0;
+    for (int x0 = 0; x0 < N0; ++x0) {  // first tag match, confirmed below in one batch of reads
+      if (!(want >> x0 & 1)) continue;
+#pragma unroll
+      for (int h = 1; h >= 0; --h)
+#pragma unroll
+        for (int s2 = 3; s2 >= 0; --s2) {
+          const unsigned e = py_slot(bk[x0][h], s2);
+          if (e != 0u && (e >> PY_RB) == key[x0].tag) rk[x0] = py_erank(e);
+        }
+    }
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) {
+      if (!(want >> x0 & 1) || (rk[x0] >= 0 && psiarr[rk[x0]] == bmb[x0])) continue;
+      rk[x0] = py_find_key(tab4, psiarr, key[x0], bmb[x0]);  // foreign tag, or on the chain (rare)
+    }
   }
+  unsigned tolist = valid & multi, lost = 0;
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) {
+    if ((want >> x0 & 1) && (rk[x0] < 0 || coll[rk[x0]])) tolist |= 1u << x0;
+    if ((want >> x0 & 1) && rk[x0] < 0) lost |= 1u << x0;
+  }
+  if (lost) atomicAdd(&counters[5], __popc(lost));
+  if (tid == 0 && ovf) atomicAdd(&counters[4], 1);
+  PY_STAMP(10);
   __syncthreads();  // the level buffers are free: the list and the natural-order outputs live there
   int *list = reinterpret_cast<int *>(lvl);
   double *outnat = lvl + L;
@@ -513,6 +595,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   }
   if (multi & valid) atomicAdd(&nmulti, __popc(multi & valid));
   __syncthreads();
+  PY_STAMP(11);
   // Φ_i row c' in the sphere order of u_old(i): gathered from LDS, written as one contiguous run
   if (colok) {
     const uint4 *p4 = reinterpret_cast<const uint4 *>(pout + N0 * col);
@@ -529,6 +612,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
 #pragma unroll
     for (int c = 0; c < N0 / 2; ++c) s2[c] = make_double2(o[2 * c], o[2 * c + 1]);
   }
+  PY_STAMP(12);
   const int nl = nlist;
   if (nl) {  // operands of the scan, re-derived so they are not live across the level loop
 #pragma unroll
@@ -708,7 +792,7 @@ hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
 
 #ifdef MIOC_STAMPS
 extern "C" int32_t mioc_debug_pyr_stamps(unsigned long long *out, int64_t nblocks) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pyr_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long)) ==
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pyr_stamps), (size_t)nblocks * 16 * sizeof(unsigned long long)) ==
                  hipSuccess
              ? 0
              : -4;

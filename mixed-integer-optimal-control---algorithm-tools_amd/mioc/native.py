@@ -241,9 +241,10 @@ class Context:
         return out.T
 
     def diagnostics(self):
-        """[value-collision targets scanned, multi-level targets scanned, p=Inf walk fallbacks, errors]."""
-        out = np.zeros(4, dtype=np.int64)
-        self._check(self.lib.mioc_diagnostics(self.h, _p(out), 4))
+        """[value-collision targets scanned, multi-level targets scanned, p=Inf walk fallbacks, errors,
+        hash-overflow rows, targets whose value was not found, values flagged colliding, reserved]."""
+        out = np.zeros(8, dtype=np.int64)
+        self._check(self.lib.mioc_diagnostics(self.h, _p(out), 8))
         return out.tolist()
 
 

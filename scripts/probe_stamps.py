@@ -13,19 +13,21 @@ lt, df, uo = make_inputs(cfg, nt=nt)
 ctx = native.Context(0); ctx.set_levels(lt); ctx.set_cost(1, cfg.beta); ctx.set_option(native.MIOC_OPT_ALGO, 3)
 ctx.bellman(df, uo, cfg.B, cfg.dt)
 nb = cfg.B + 1
-buf = (ctypes.c_ulonglong * (nb * 8))()
+buf = (ctypes.c_ulonglong * (nb * 16))()
 lib = native.load_library()
 f = lib.mioc_debug_pyr_stamps; f.argtypes = [ctypes.c_void_p, ctypes.c_int64]; f.restype = ctypes.c_int32
 assert f(buf, nb) == 0
-st = np.array(buf, dtype=np.int64).reshape(nb, 8)
-names = ["load+T1 (0->1)", "reductions (1->2)", "hash+dirty (2->3)", "pyramid (3->4)", "lookup+store (4->5)"]
+st = np.array(buf, dtype=np.int64).reshape(nb, 16)
+# stamp slots in program order (6 holds the number of levels)
+seq = [(0, "start"), (1, "load+T1+reduce"), (2, "delta+fq+clears"), (7, "barrier"), (8, "inserts"),
+       (9, "barrier"), (3, "border marks"), (4, "pyramid"), (10, "lookups"), (11, "outnat+UU+barrier"),
+       (12, "Sout gather+store"), (5, "exact scans")]
 full = st[:, 5] > 0
 print("blocks with all stamps:", full.sum(), "of", nb)
 s = st[full]
-for k, nm in enumerate(names):
-    d = s[:, k + 1] - s[:, k]
+for (a, _), (b, nm) in zip(seq[:-1], seq[1:]):
+    d = s[:, b] - s[:, a]
     print(f"{nm:22s} cycles median {np.median(d):9.0f}  p90 {np.percentile(d, 90):9.0f}  max {d.max():9.0f}")
 tot = s[:, 5] - s[:, 0]
 print(f"{'total':22s} cycles median {np.median(tot):9.0f}  max {tot.max():9.0f}")
 print("levels executed: median", np.median(s[:, 6]), "max", s[:, 6].max(), "min", s[:, 6].min())
-print("start skew (cycles): ", (st[:, 0] - st[:, 0].min()).max(), " end spread:", (s[:, 5].max() - st[:, 0].min()))
