@@ -29,8 +29,9 @@ namespace mioc {
 constexpr int PY_T = 512;          // threads per workgroup: one grid column (dim-0 run) per thread
 constexpr int PY_NW = PY_T / 64;   // waves per workgroup
 constexpr int PY_HS = 12288;       // hash slots (uint32): <= 4096 sources, load <= 1/3
-constexpr int PY_NB = PY_HS / 4;   // 16-byte buckets of 4 slots; every key may live in one of two
-constexpr int PY_G = 8;            // bucket width = 2^PY_G · δ
+constexpr int PY_NB = PY_HS / 4;   // 16-byte buckets of 4 slots, each with a 16-bit arrival count
+constexpr int PY_OVF = 256;        // keys that found both of their buckets full
+constexpr int PY_G = 14;           // bucket width = 2^PY_G · δ (wide: few border checks; false collisions only cost exact scans)
 constexpr unsigned PY_RB = 13;     // hash entry = tag << PY_RB | (rank + 1); 0 = empty
 
 // v_min_f64 without the sNaN-quieting v_max_f64 x,x that llvm.minnum puts in front of every operand
@@ -54,10 +55,12 @@ __device__ unsigned long long g_pyr_stamps[4096][16];
   } while (0)
 #endif
 
-// Bucket hash (bucketized two-choice).  A bucket of Ψ values is an integer-valued double fq = floor(Ψ·2^k)
-// (+0.0, so -0 and +0 agree).  Its key may sit in any of the 4 slots of two 16-byte hash buckets; a slot
-// holds tag << PY_RB | (rank + 1).  Every probe is one or two ds_read_b128, with no chains.  A tag match
-// is confirmed against the exact Ψ of that rank (psiarr), so false matches cost one read.
+// Bucket hash.  A bucket of Ψ values is an integer-valued double fq = floor(Ψ·2^k) (+0.0, so -0 and +0
+// agree).  Its key has two 16-byte hash buckets of 4 slots; a slot holds tag << PY_RB | (rank + 1).
+// Insertion is first-fit without races: an atomicAdd on bucket b1's arrival count hands out slot
+// `count` (< 4), arrivals beyond 4 spill to b2 the same way, and beyond that to a small overflow list.
+// A count above 4 therefore says "also look at the next place".  Reads are one ds_read_b128 plus the
+// count; a tag match is confirmed against the exact Ψ of that rank (psiarr).
 struct PyKey {
   unsigned b1, b2, tag;
 };
@@ -73,73 +76,79 @@ __device__ __forceinline__ PyKey py_key(double fq) {
   k.b1 = __umulhi(lo, (unsigned)PY_NB);
   k.b2 = __umulhi(hi, (unsigned)PY_NB);
   if (k.b2 == k.b1) k.b2 = k.b1 + 1 == (unsigned)PY_NB ? 0u : k.b1 + 1;
-  k.tag = lo & ((1u << (32 - PY_RB)) - 1);
+  k.tag = (lo ^ (hi >> 7)) & ((1u << (32 - PY_RB)) - 1);
   return k;
 }
 __device__ __forceinline__ int py_erank(unsigned e) { return (int)(e & ((1u << PY_RB) - 1)) - 1; }
 __device__ __forceinline__ unsigned py_slot(const uint4 &b, int s) {
   return s == 0 ? b.x : s == 1 ? b.y : s == 2 ? b.z : b.w;
 }
-__device__ __forceinline__ bool py_full(const uint4 &b) { return b.x && b.y && b.z && b.w; }
-__device__ __forceinline__ unsigned py_nextb(unsigned b) { return b + 1 == (unsigned)PY_NB ? 0u : b + 1; }
-
+__device__ __forceinline__ unsigned py_count(const unsigned *hcnt, unsigned b) {
+  return (hcnt[b >> 1] >> ((b & 1) * 16)) & 0xFFFFu;
+}
 __device__ __forceinline__ double py_bucket(double v, double inv_w) { return floor(v * inv_w) + 0.0; }
 
-// Overflow chain: a key whose two buckets were both full lives in the first bucket after b2 that had a
-// free slot.  Buckets only fill up, so a scan from b2+1 that stops at the first non-full bucket has
-// passed every such key.  All chain walks are cold paths, kept out of line.
-__device__ __noinline__ unsigned py_chain_free(const uint4 *tab4, unsigned b2) {
-  for (unsigned b = py_nextb(b2);; b = py_nextb(b)) {
-    const uint4 t = tab4[b];
-    if (!py_full(t)) return b * 4 + (!t.x ? 0 : !t.y ? 1 : !t.z ? 2 : 3);
-  }
-}
+struct PyHash {
+  const uint4 *tab4;     // [PY_NB] buckets
+  const unsigned *hcnt;  // [PY_NB / 2] arrival counts, two 16-bit counts per word
+  const uint2 *hovf;     // [PY_OVF] {bucket b1, entry}
+  int novf;              // entries in hovf (<= PY_OVF; more means the row is resolved by exact scans)
+};
 
-// Mark every source other than `self` whose entry (in the two buckets of `key`, and on its chain when
-// both are full) holds bucket fq; true if there was one.
-__device__ __noinline__ bool py_mark_key(const uint4 *tab4, const double *psiarr, unsigned char *coll, PyKey key,
-                                         double fq, double inv_w, int self) {
-  bool found = false;
-  const uint4 b1 = tab4[key.b1], b2 = tab4[key.b2];
-  const bool chain = py_full(b1) && py_full(b2);
-  unsigned b = key.b1;
-  for (int n = 0;; ++n) {
-    const uint4 t = n == 0 ? b1 : n == 1 ? b2 : tab4[b];
-    for (int s2 = 0; s2 < 4; ++s2) {
-      const unsigned e = py_slot(t, s2);
-      const int r = py_erank(e);
-      if (e != 0u && (e >> PY_RB) == key.tag && r != self && py_bucket(psiarr[r], inv_w) == fq) {
+// Every entry of `key` beyond bucket b1: bucket b2 when b1 spilled, then the overflow list when b2 did
+// too.  Cold path, out of line.  Calls visit(e) as f(e) through a small state machine: returns the
+// first rank r != self whose entry carries key.tag and whose Ψ lies in bucket fq (mode 0, also marks
+// every such rank in coll), or whose Ψ equals v (mode 1).
+__device__ __forceinline__ int py_spill(PyHash H, const double *psiarr, unsigned char *coll, PyKey key, double fq,
+                                     double inv_w, double v, int self, int mode) {
+  int found = -1;
+  auto visit = [&](unsigned e) {
+    if ((e >> PY_RB) != key.tag) return;
+    const int r = py_erank(e);
+    if (r == self) return;
+    if (mode == 0) {
+      if (py_bucket(psiarr[r], inv_w) == fq) {
         coll[r] = 1;
-        found = true;
+        if (found < 0) found = r;
       }
+    } else if (found < 0 && psiarr[r] == v) {
+      found = r;
     }
-    if (n == 0) continue;
-    if (n == 1) {
-      if (!chain) return found;
-      b = key.b2;
-    } else if (!py_full(t)) {
-      return found;
-    }
-    b = py_nextb(b);
-  }
+  };
+  const unsigned c2 = py_count(H.hcnt, key.b2);
+  const uint4 t = H.tab4[key.b2];
+  for (int s2 = 0; s2 < 4 && s2 < (int)c2; ++s2) visit(py_slot(t, s2));
+  if (c2 > 4)
+    for (int o = 0; o < H.novf; ++o)
+      if (H.hovf[o].x == key.b1) visit(H.hovf[o].y);
+  return found;
 }
 
-// First source (two buckets, then the chain) whose entry carries `tag` and whose Ψ equals v; -1 if none.
-__device__ __noinline__ int py_find_key(const uint4 *tab4, const double *psiarr, PyKey key, double v) {
-  const uint4 b1 = tab4[key.b1], b2 = tab4[key.b2];
-  const bool chain = py_full(b1) && py_full(b2);
-  unsigned b = key.b2;
-  for (int n = 0;; ++n) {
-    const uint4 t = n == 0 ? b1 : n == 1 ? b2 : tab4[b];
-    for (int s2 = 0; s2 < 4; ++s2) {
-      const unsigned e = py_slot(t, s2);
-      if (e != 0u && (e >> PY_RB) == key.tag && psiarr[py_erank(e)] == v) return py_erank(e);
+// All entries of `key` (bucket b1, then the spill places): mode 0 marks every other source whose Ψ lies
+// in bucket fq and returns one of them, mode 1 returns the first source whose Ψ equals v.  Out of line.
+__device__ __forceinline__ int py_search(PyHash H, const double *psiarr, unsigned char *coll, PyKey key, double fq,
+                                      double inv_w, double v, int self, int mode) {
+  int found = -1;
+  const unsigned c1 = py_count(H.hcnt, key.b1);
+  const uint4 t = H.tab4[key.b1];
+  for (int s2 = 0; s2 < 4 && s2 < (int)c1; ++s2) {
+    const unsigned e = py_slot(t, s2);
+    const int r = py_erank(e);
+    if ((e >> PY_RB) != key.tag || r == self) continue;
+    if (mode == 0) {
+      if (py_bucket(psiarr[r], inv_w) == fq) {
+        coll[r] = 1;
+        if (found < 0) found = r;
+      }
+    } else if (found < 0 && psiarr[r] == v) {
+      found = r;
     }
-    if (n == 0) continue;
-    if (n == 1 && !chain) return -1;
-    if (n >= 2 && !py_full(t)) return -1;
-    b = py_nextb(b);
   }
+  if (c1 > 4 && (mode == 0 || found < 0)) {
+    const int f2 = py_spill(H, psiarr, coll, key, fq, inv_w, v, self, mode);
+    if (found < 0) found = f2;
+  }
+  return found;
 }
 
 struct PyrDims {  // geometry copied by value into registers (never escapes to memory)
@@ -194,7 +203,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   __shared__ int vote[2][PY_NW];        // per-wave early-exit votes, double-buffered by level parity
   __shared__ double scan_v[2][PY_NW];   // exact-scan reductions, double-buffered by list position parity
   __shared__ int scan_r[2][PY_NW];
-  __shared__ int nlist, nmulti, ovf;
+  __shared__ int nlist, nmulti, novf;
   PyrDims D;
 #pragma unroll
   for (int m = 0; m < kMaxM; ++m) {
@@ -212,8 +221,10 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
   double *lvl = reinterpret_cast<double *>(pys);                             // [2][L] level buffers
   double *psiarr = lvl + (size_t)2 * L;                                      // [L] Ψ_j by rank j
-  unsigned *htab = reinterpret_cast<unsigned *>(psiarr + L);                 // [PY_HS] bucket hash
-  unsigned char *coll = reinterpret_cast<unsigned char *>(htab + PY_HS);     // [L] Ψ_j has a close value
+  unsigned *htab = reinterpret_cast<unsigned *>(psiarr + L);                 // [PY_HS] hash buckets
+  unsigned *hcnt = htab + PY_HS;                                             // [PY_NB / 2] arrival counts
+  uint2 *hovf = reinterpret_cast<uint2 *>(hcnt + PY_NB / 2);                 // [PY_OVF] overflow list
+  unsigned char *coll = reinterpret_cast<unsigned char *>(hovf + PY_OVF);    // [L] Ψ_j has a close value
   PY_STAMP(0);
 
   // ---- this thread's grid column: coordinates 1..M-1 are shared by its N0 points ---------------
@@ -349,89 +360,80 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     fr[x0] = x - fq[x0];
   }
   {
-    uint4 *h4 = reinterpret_cast<uint4 *>(htab);
-    for (int s2 = tid; s2 < PY_HS / 4; s2 += PY_T) h4[s2] = make_uint4(0u, 0u, 0u, 0u);
+    uint4 *c4 = reinterpret_cast<uint4 *>(hcnt);
+    for (int s2 = tid; s2 < PY_NB / 8; s2 += PY_T) c4[s2] = make_uint4(0u, 0u, 0u, 0u);
     for (int s2 = tid; s2 < L; s2 += PY_T) coll[s2] = 0;
   }
   if (tid == 0) {
     nlist = 0;
     nmulti = 0;
-    ovf = 0;
+    novf = 0;
   }
   PY_STAMP(2);
   __syncthreads();
   PY_STAMP(7);
-  const uint4 *tab4 = reinterpret_cast<const uint4 *>(htab);
+  PyHash H;
+  H.tab4 = reinterpret_cast<const uint4 *>(htab);
+  H.hcnt = hcnt;
+  H.hovf = hovf;
   {
     PyKey key[N0];
-    unsigned ent[N0], tslot[N0];
+    unsigned ent[N0], cnt[N0];
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
       key[x0] = py_key(fq[x0]);
       ent[x0] = key[x0].tag << PY_RB | (unsigned)(x0 + N0 * col + 1);
-      tslot[x0] = 0;
     }
-    // insert into the emptier of the two buckets; a lost race re-reads both and tries again
-    unsigned pend = fin;
-    while (pend) {
-      uint4 bk[N0][2];
+    // first fit: slot `count` of b1, else of b2, else the overflow list (one atomic round each)
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0)
+      cnt[x0] = (fin >> x0 & 1) ? atomicAdd(&hcnt[key[x0].b1 >> 1], 1u << ((key[x0].b1 & 1) * 16)) : 0u;
+    unsigned spill = 0;
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) {
+      if (!(fin >> x0 & 1)) continue;
+      const unsigned c = (cnt[x0] >> ((key[x0].b1 & 1) * 16)) & 0xFFFFu;
+      if (c < 4)
+        htab[key[x0].b1 * 4 + c] = ent[x0];
+      else
+        spill |= 1u << x0;
+    }
+    if (spill) {
 #pragma unroll
       for (int x0 = 0; x0 < N0; ++x0)
-        if (pend >> x0 & 1) {
-          bk[x0][0] = tab4[key[x0].b1];
-          bk[x0][1] = tab4[key[x0].b2];
-        }
+        cnt[x0] = (spill >> x0 & 1) ? atomicAdd(&hcnt[key[x0].b2 >> 1], 1u << ((key[x0].b2 & 1) * 16)) : 0u;
 #pragma unroll
       for (int x0 = 0; x0 < N0; ++x0) {
-        if (!(pend >> x0 & 1)) continue;
-        int e1 = 0, e2 = 0, f1 = -1, f2 = -1;
-#pragma unroll
-        for (int s2 = 3; s2 >= 0; --s2) {
-          if (py_slot(bk[x0][0], s2) == 0u) ++e1, f1 = s2;
-          if (py_slot(bk[x0][1], s2) == 0u) ++e2, f2 = s2;
+        if (!(spill >> x0 & 1)) continue;
+        const unsigned c = (cnt[x0] >> ((key[x0].b2 & 1) * 16)) & 0xFFFFu;
+        if (c < 4) {
+          htab[key[x0].b2 * 4 + c] = ent[x0];
+        } else {
+          const int o = atomicAdd(&novf, 1);
+          if (o < PY_OVF) hovf[o] = make_uint2(key[x0].b1, ent[x0]);
         }
-        if (e1 + e2 == 0) {  // both buckets full: the first bucket after b2 with a free slot (rare)
-          ovf = 1;
-          tslot[x0] = py_chain_free(tab4, key[x0].b2);
-          continue;
-        }
-        tslot[x0] = e1 >= e2 ? key[x0].b1 * 4 + f1 : key[x0].b2 * 4 + f2;
       }
-      unsigned old[N0];
-#pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) old[x0] = (pend >> x0 & 1) ? atomicCAS(&htab[tslot[x0]], 0u, ent[x0]) : 1u;
-#pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0)
-        if (old[x0] == 0u) pend &= ~(1u << x0);
     }
     PY_STAMP(8);
     __syncthreads();  // every value is in the table
     PY_STAMP(9);
-    // another source in my bucket (exact duplicates included), or close across a bucket border
-    unsigned hit = 0;
-    uint4 bk[N0][2];
-#pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0)
-      if (fin >> x0 & 1) {
-        bk[x0][0] = tab4[key[x0].b1];
-        bk[x0][1] = tab4[key[x0].b2];
-      }
+    H.novf = min(novf, PY_OVF);
+    // close across a bucket border (same-bucket pairs are caught by the lookups below)
+    unsigned hit = 0, need = 0;
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
       if (!(fin >> x0 & 1)) continue;
+      need |= (unsigned)(fr[x0] <= FR) << (x0 + 8);
+      need |= (unsigned)(fr[x0] >= 1.0 - FR) << (x0 + 16);
+    }
+    // cold: full searches (bucket b1, spill places) -- one copy of the code, operands from LDS
+#pragma unroll 1
+    for (int q = 0; q < 3 * N0; ++q) {
+      const int x0 = q % N0, kind = q / N0;
+      if (!(need >> (x0 + 8 * kind) & 1)) continue;
       const int me = x0 + N0 * col;
-      bool dup = false;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          const unsigned e = py_slot(bk[x0][h], s2);
-          dup |= e != 0u && (e >> PY_RB) == key[x0].tag && py_erank(e) != me;
-        }
-      dup |= py_full(bk[x0][0]) && py_full(bk[x0][1]);
-      if (dup && py_mark_key(tab4, psiarr, coll, key[x0], fq[x0], inv_w, me)) hit |= 1u << x0;
-      if (fr[x0] <= FR && py_mark_key(tab4, psiarr, coll, py_key(fq[x0] - 1.0), fq[x0] - 1.0, inv_w, me)) hit |= 1u << x0;
-      if (fr[x0] >= 1.0 - FR && py_mark_key(tab4, psiarr, coll, py_key(fq[x0] + 1.0), fq[x0] + 1.0, inv_w, me)) hit |= 1u << x0;
+      const double fqs = py_bucket(psiarr[me], inv_w) + (kind == 1 ? -1.0 : kind == 2 ? 1.0 : 0.0);
+      if (py_search(H, psiarr, coll, py_key(fqs), fqs, inv_w, 0.0, me, 0) >= 0) hit |= 1u << x0;
     }
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0)
@@ -456,8 +458,8 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     for (int x0 = 0; x0 < N0; ++x0) {
       const double cand = K[x0] + cur[x0];
       const bool lt = cand < best[x0];
-      const bool eq = (cand == best[x0]) & (cand < INFINITY);
-      best[x0] = lt ? cand : best[x0];
+      const bool eq = cand == best[x0];  // Inf == Inf ties only mark targets left at +Inf (never listed)
+      best[x0] = vmin(cand, best[x0]);
       bmb[x0] = lt ? cur[x0] : bmb[x0];
       mlt |= (unsigned)lt << x0;
       meq |= (unsigned)eq << x0;
@@ -529,40 +531,69 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   {
     PyKey key[N0];
     uint4 bk[N0][2];
+    unsigned cc[N0][2];
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
       rk[x0] = -1;
       if (want >> x0 & 1) {
         key[x0] = py_key(py_bucket(bmb[x0], inv_w));
-        bk[x0][0] = tab4[key[x0].b1];
-        bk[x0][1] = tab4[key[x0].b2];
+        bk[x0][0] = H.tab4[key[x0].b1];
+        bk[x0][1] = H.tab4[key[x0].b2];
+        cc[x0][0] = py_count(hcnt, key[x0].b1);
+        cc[x0][1] = py_count(hcnt, key[x0].b2);
       }
     }
+    // the tag's entries in b1 (and b2 if b1 spilled): exactly one, holding bmb, is the clean case;
+    // a second one may be another source in the same bucket, and a double spill may hide more
+    unsigned redo = 0;
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {  // first tag match, confirmed below in one batch of reads
+    for (int x0 = 0; x0 < N0; ++x0) {
       if (!(want >> x0 & 1)) continue;
+      int nm = 0;
 #pragma unroll
       for (int h = 1; h >= 0; --h)
 #pragma unroll
         for (int s2 = 3; s2 >= 0; --s2) {
           const unsigned e = py_slot(bk[x0][h], s2);
-          if (e != 0u && (e >> PY_RB) == key[x0].tag) rk[x0] = py_erank(e);
+          if ((h == 0 || cc[x0][0] > 4) && s2 < (int)cc[x0][h] && (e >> PY_RB) == key[x0].tag) {
+            rk[x0] = py_erank(e);
+            ++nm;
+          }
         }
+      redo |= (unsigned)(nm != 1 || (cc[x0][0] > 4 && cc[x0][1] > 4)) << x0;
     }
 #pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0)  // confirm the single match (one batch of reads)
+      redo |= (unsigned)((want >> x0 & 1) && !(redo >> x0 & 1) && psiarr[rk[x0]] != bmb[x0]) << x0;
+    // cold: find the holder of bmb among all entries of the key, and whether another source shares
+    // its bucket -- one copy of the search code
+#pragma unroll 1
     for (int x0 = 0; x0 < N0; ++x0) {
-      if (!(want >> x0 & 1) || (rk[x0] >= 0 && psiarr[rk[x0]] == bmb[x0])) continue;
-      rk[x0] = py_find_key(tab4, psiarr, key[x0], bmb[x0]);  // foreign tag, or on the chain (rare)
+      if (!(redo >> x0 & 1)) continue;
+      double v = bmb[0];
+#pragma unroll
+      for (int q = 1; q < N0; ++q) v = q == x0 ? bmb[q] : v;
+      const double fqv = py_bucket(v, inv_w);
+      const PyKey kv = py_key(fqv);
+      int r = py_search(H, psiarr, coll, kv, 0.0, inv_w, v, -1, 1);
+      if (r >= 0 && py_search(H, psiarr, coll, kv, fqv, inv_w, 0.0, r, 0) >= 0) coll[r] = 1;  // not unique
+#pragma unroll
+      for (int q = 0; q < N0; ++q) rk[q] = q == x0 ? r : rk[q];
     }
   }
-  unsigned tolist = valid & multi, lost = 0;
+  unsigned finb = 0;
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) finb |= (unsigned)(best[x0] < INFINITY) << x0;
+  multi &= valid & finb;
+  unsigned tolist = multi, lost = 0;
 #pragma unroll
   for (int x0 = 0; x0 < N0; ++x0) {
     if ((want >> x0 & 1) && (rk[x0] < 0 || coll[rk[x0]])) tolist |= 1u << x0;
     if ((want >> x0 & 1) && rk[x0] < 0) lost |= 1u << x0;
   }
   if (lost) atomicAdd(&counters[5], __popc(lost));
-  if (tid == 0 && ovf) atomicAdd(&counters[4], 1);
+  if (novf > PY_OVF) tolist |= want;  // the overflow list itself overflowed: exact scans for this row
+  if (tid == 0 && novf) atomicAdd(&counters[4], 1);
   PY_STAMP(10);
   __syncthreads();  // the level buffers are free: the list and the natural-order outputs live there
   int *list = reinterpret_cast<int *>(lvl);
@@ -593,7 +624,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       }
     }
   }
-  if (multi & valid) atomicAdd(&nmulti, __popc(multi & valid));
+  if (multi) atomicAdd(&nmulti, __popc(multi));
   __syncthreads();
   PY_STAMP(11);
   // Φ_i row c' in the sphere order of u_old(i): gathered from LDS, written as one contiguous run
@@ -770,7 +801,7 @@ hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsD
 
 size_t pyr_lds_bytes(const PyrGeom &G) {
   return (size_t)3 * G.ncol * G.n[0] * sizeof(double) + (size_t)PY_HS * sizeof(unsigned) +
-         (size_t)G.ncol * G.n[0];
+         (size_t)(PY_NB / 2) * sizeof(unsigned) + (size_t)PY_OVF * sizeof(uint2) + (size_t)G.ncol * G.n[0];
 }
 
 hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
