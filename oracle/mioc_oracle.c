@@ -8,7 +8,7 @@
  * Parity status: the reference is Julia 1.10 (Manifest.toml:3); there is no Julia toolchain in
  * this image and the reference has no tests for this path, so this restatement is
  * "parity unpinned" by the reference itself.  It is pinned instead by
- *   (1) an exhaustive-enumeration known-answer test on dyadic inputs (tests/test_oracle_kat.py),
+ *   (1) an exhaustive-enumeration known-answer test on dyadic inputs (tests/test_oracle.py),
  *   (2) an independent pure-Python scalar twin (oracle/oracle.py) cross-checked bit for bit,
  *   (3) the TV_p docstring vectors of HelpFunctions.jl:235-249.
  *
