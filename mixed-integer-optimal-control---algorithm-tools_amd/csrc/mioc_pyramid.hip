@@ -8,15 +8,17 @@
 // BM_{S+1} is BM_S dilated by the unit cross (levels are consecutive integers, so value distance = index
 // distance): 2M neighbour minima per grid point per level instead of L candidates per target.
 //
-// Argmin (the reference's strict `>` over iterator order, HelpFunctions.jl:73): in a "clean" row -- every
-// pair of finite Ψ values more than δ apart, δ >= ulp of any candidate value -- the only j with
-// fl(K_l(d) + Ψ_j) == out(l) is the unique j holding BM at the first winning level (a value hash maps it
-// back to its rank).  A target whose minimum is reached at two levels, and every dirty row, is resolved by
-// the exact brute-force scan instead, so results are bit-identical to the reference in every case.
+// Argmin (the reference's strict `>` over iterator order, HelpFunctions.jl:73): the winner of a target is
+// the source holding BM at its first winning level.  It is the unique j with fl(K_l(d) + Ψ_j) == out(l)
+// unless another source's Ψ lies within δ >= ulp of any candidate value (rounding could tie), or the
+// minimum is reached at two levels.  Both cases are detected exactly -- a bucket hash over the row's Ψ
+// (same bucket, or close across a bucket border) and per-level tie tracking -- and those targets are
+// resolved by a workgroup-parallel exact scan, so results are bit-identical to the reference always.
 //
-// Layout ("staging"): S_i[c'][l] = Φ_i[l, c' + b̃_l(i)] (source row major, +Inf where c'+b̃_l > B);
-// UU_i[c'][l] = U_i[l, c' + b̃_l(i)] (uint16 rank).  One workgroup per source row; rows are dispatched
-// from c' = B downwards so the cheap high rows (few valid targets) never delay a full pyramid row.
+// Layout ("staging"): S_i[c'][pos_i(l)] = Φ_i[l, c' + b̃_l(i)] (+Inf where c'+b̃_l > B), each row in the
+// sphere order pos_i of u_old(i) (levels grouped by b̃_l(i)), so the sources a row of step i-1 needs
+// from row c'-s of S_i (the sphere s) are one contiguous run; UU_i[c'][l] = U_i[l, c' + b̃_l(i)] (uint16
+// rank, natural order).  One workgroup per source row, rows in ascending order (longest first).
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -32,6 +34,7 @@ constexpr int PY_HS = 12288;       // hash slots (uint32): <= 4096 sources, load
 constexpr int PY_NB = PY_HS / 4;   // 16-byte buckets of 4 slots, each with a 16-bit arrival count
 constexpr int PY_OVF = 256;        // keys that found both of their buckets full
 constexpr int PY_G = 14;           // bucket width = 2^PY_G · δ (wide: few border checks; false collisions only cost exact scans)
+constexpr int PY_FEW = 48;         // rows with at most this many targets in the trust region: exact scans
 constexpr unsigned PY_RB = 13;     // hash entry = tag << PY_RB | (rank + 1); 0 = empty
 
 // v_min_f64 without the sNaN-quieting v_max_f64 x,x that llvm.minnum puts in front of every operand
@@ -189,6 +192,86 @@ __device__ __forceinline__ bool py_any(bool f, int *slots) {
   return r != 0;
 }
 
+// Exact scan of listed targets, the reference loop (HelpFunctions.jl:60-77) for one cell: one wave per
+// target.  Lane k evaluates the sources of columns k, k+64, ... (N0 points each, Ψ by rank in LDS) in
+// increasing rank, then a (value, rank) minimum over the wave.  Writes UU[l] for a finite minimum, and
+// outv[l] (the minimum, +Inf if none) when outv is given.  No barriers; waves take targets round-robin.
+template <int M, int N0>
+__device__ __forceinline__ void py_scan_list(const int *list, int nl, const double *psiarr, const PyrDims &D,
+                                             int ncol, const double *dfi, double dt, double beta, uint16_t *UU,
+                                             double *outv) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w >= nl) return;
+  // this lane's columns, coordinates 1..M-1 packed 10 bits each (n_m <= ncol <= 512)
+  unsigned long long pk[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    int cc = lane + 64 * t;
+    unsigned long long v = 0;
+#pragma unroll
+    for (int m = 1; m < M; ++m) {
+      v |= (unsigned long long)(cc % D.n[m]) << (10 * (m - 1));
+      cc /= D.n[m];
+    }
+    pk[t] = v;
+  }
+  double a[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) a[m] = dt * dfi[m];
+  for (int e = w; e < nl; e += PY_NW) {
+    const int l = list[e];
+    int xl[M];
+    {
+      int gg = l;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        xl[m] = gg % D.n[m];
+        gg /= D.n[m];
+      }
+    }
+    double t1 = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) t1 = t1 + a[m] * (double)(D.base[m] + xl[m]);
+    double bv = INFINITY;
+    int bj = -1;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int c = lane + 64 * t;
+      if (c >= ncol) break;
+      int dcol = 0;
+#pragma unroll
+      for (int m = 1; m < M; ++m) dcol += abs((int)((pk[t] >> (10 * (m - 1))) & 1023u) - xl[m]);
+      const double2 *p2 = reinterpret_cast<const double2 *>(psiarr + N0 * c);
+#pragma unroll
+      for (int q = 0; q < N0 / 2; ++q) {
+        const double2 ps = p2[q];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int x0 = 2 * q + h;
+          const double val = (t1 + beta * (double)(abs(x0 - xl[0]) + dcol)) + (h ? ps.y : ps.x);
+          if (val < bv) {
+            bv = val;
+            bj = x0 + N0 * c;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(bv, off);
+      const int oj = __shfl_xor(bj, off);
+      if (oj >= 0 && (bj < 0 || ov < bv || (ov == bv && oj < bj))) {
+        bv = ov;
+        bj = oj;
+      }
+    }
+    if (lane == 0) {
+      if (bj >= 0) UU[l] = (uint16_t)bj;
+      if (outv) outv[l] = bj >= 0 ? bv : INFINITY;
+    }
+  }
+}
+
 template <int M, int N0>
 __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i,
                                                    const uint32_t *__restrict__ perm_all,
@@ -201,9 +284,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   __shared__ double red[2][PY_NW];
   __shared__ int anyv[PY_NW];
   __shared__ int vote[2][PY_NW];        // per-wave early-exit votes, double-buffered by level parity
-  __shared__ double scan_v[2][PY_NW];   // exact-scan reductions, double-buffered by list position parity
-  __shared__ int scan_r[2][PY_NW];
-  __shared__ int nlist, nmulti, novf;
+  __shared__ int nlist, nmulti, novf, nvalid;
   PyrDims D;
 #pragma unroll
   for (int m = 0; m < kMaxM; ++m) {
@@ -213,7 +294,9 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   const int k = blockIdx.y;
   const int L = Lv.L, B = P.B, tid = threadIdx.x, ncol = G.ncol, Smax = G.Smax;
   const double beta = Lv.beta;
-  const int cp = B - (int)blockIdx.x;  // source row: high rows first
+  // source row, ascending: rows near B have few targets inside the trust region and are the cheapest,
+  // so with B+1 > #CUs the rows that wait for a free CU are the short ones (longest-first order)
+  const int cp = (int)blockIdx.x;
   const double *Sin = Sin_all + (size_t)k * s_stride;
   double *Sout = Sout_all + (size_t)k * s_stride + (size_t)cp * L;
   uint16_t *UU = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L) + (size_t)cp * L;
@@ -226,6 +309,9 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   uint2 *hovf = reinterpret_cast<uint2 *>(hcnt + PY_NB / 2);                 // [PY_OVF] overflow list
   unsigned char *coll = reinterpret_cast<unsigned char *>(hovf + PY_OVF);    // [L] Ψ_j has a close value
   PY_STAMP(0);
+#ifdef MIOC_STAMPS
+  if (tid == 0) g_pyr_stamps[blockIdx.x][13] = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // ---- this thread's grid column: coordinates 1..M-1 are shared by its N0 points ---------------
   const bool colok = tid < ncol;
@@ -233,16 +319,13 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   double a[M], pc[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) a[m] = P.dt * dfi[m];
-  int xc[M];
   int bcl = 0, nbm = 0;
-  xc[0] = 0;
   {
     int cc = col;
 #pragma unroll
     for (int m = 1; m < M; ++m) {
       const int xm = cc % D.n[m];
       cc /= D.n[m];
-      xc[m] = xm;
       const double nu = (double)(D.base[m] + xm);
       pc[m] = a[m] * nu;
       bcl += (int)fabs(nu - uoi[m]);
@@ -257,6 +340,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   // row for all positions of one sphere -- and scatters them into Ψ-by-rank (psiarr) in LDS ----------
   const uint32_t *pin = perm_all + ((size_t)k * P.nt + i + 1) * L;
   const uint32_t *pout = perm_all + ((size_t)k * P.nt + i) * L;
+  if (tid == 0) nvalid = 0;
   if (colok) {
     uint32_t e[N0];
     const uint4 *p4 = reinterpret_cast<const uint4 *>(pin + N0 * col);
@@ -324,7 +408,8 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     red[0][tid >> 6] = psimax;
     red[1][tid >> 6] = psimin;
   }
-  const bool any_valid = py_any(valid != 0, anyv);  // its barrier also publishes red[][]
+  if (valid) atomicAdd(&nvalid, __popc(valid));
+  const bool any_valid = py_any(valid != 0, anyv);  // its barrier also publishes red[][] and nvalid
   double Pmax = red[0][0], Rmin = red[1][0];
 #pragma unroll
   for (int w = 1; w < PY_NW; ++w) {
@@ -336,6 +421,39 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     if (colok) {
 #pragma unroll
       for (int x0 = 0; x0 < N0; ++x0) Sout[x0 + N0 * col] = INFINITY;
+    }
+    return;
+  }
+  if (nvalid <= PY_FEW) {
+    // few targets inside the trust region (rows near B): exact scans instead of hash + pyramid
+    int *list = reinterpret_cast<int *>(lvl);
+    double *outnat = lvl + L;
+    if (tid == 0) nlist = 0;
+    __syncthreads();
+    if (colok) {
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        outnat[x0 + N0 * col] = INFINITY;
+        if (valid >> x0 & 1) list[atomicAdd(&nlist, 1)] = x0 + N0 * col;
+      }
+    }
+    __syncthreads();
+    py_scan_list<M, N0>(list, nlist, psiarr, D, ncol, dfi, P.dt, beta, UU, outnat);
+    __syncthreads();
+    if (colok) {
+      const uint4 *p4 = reinterpret_cast<const uint4 *>(pout + N0 * col);
+      double o[N0];
+#pragma unroll
+      for (int c = 0; c < N0 / 4; ++c) {
+        const uint4 t = p4[c];
+        o[4 * c] = outnat[t.x & 0xFFFFu];
+        o[4 * c + 1] = outnat[t.y & 0xFFFFu];
+        o[4 * c + 2] = outnat[t.z & 0xFFFFu];
+        o[4 * c + 3] = outnat[t.w & 0xFFFFu];
+      }
+      double2 *s2 = reinterpret_cast<double2 *>(Sout + N0 * col);
+#pragma unroll
+      for (int c = 0; c < N0 / 2; ++c) s2[c] = make_double2(o[2 * c], o[2 * c + 1]);
     }
     return;
   }
@@ -645,77 +763,12 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   }
   PY_STAMP(12);
   const int nl = nlist;
-  if (nl) {  // operands of the scan, re-derived so they are not live across the level loop
-#pragma unroll
-    for (int m = 0; m < M; ++m) a[m] = P.dt * dfi[m];
-    int cc = col;
-#pragma unroll
-    for (int m = 1; m < M; ++m) {
-      xc[m] = cc % D.n[m];
-      cc /= D.n[m];
-    }
-  }
-  // exact scan of the listed targets, the reference loop (HelpFunctions.jl:60-77) for one cell at a
-  // time: every thread evaluates its own N0 sources, then a (value, rank) minimum over the workgroup
-  for (int e2 = 0; e2 < nl; ++e2) {
-    const int l = list[e2];
-    int xl[M];
-    {
-      int gg = l;
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        xl[m] = gg % D.n[m];
-        gg /= D.n[m];
-      }
-    }
-    double t = 0.0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) t = t + a[m] * (double)(D.base[m] + xl[m]);
-    int dcol = 0;
-#pragma unroll
-    for (int m = 1; m < M; ++m) dcol += abs(xc[m] - xl[m]);
-    double bv = INFINITY;
-    int bj = -1;
-    if (colok) {
-#pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
-        const double val = (t + beta * (double)(abs(x0 - xl[0]) + dcol)) + psiarr[x0 + N0 * col];
-        if (val < bv) {
-          bv = val;
-          bj = x0 + N0 * col;
-        }
-      }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double ov = __shfl_xor(bv, off);
-      const int oj = __shfl_xor(bj, off);
-      if (oj >= 0 && (bj < 0 || ov < bv || (ov == bv && oj < bj))) {
-        bv = ov;
-        bj = oj;
-      }
-    }
-    if ((tid & 63) == 0) {
-      scan_v[e2 & 1][tid >> 6] = bv;
-      scan_r[e2 & 1][tid >> 6] = bj;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      double v0 = scan_v[e2 & 1][0];
-      int j0 = scan_r[e2 & 1][0];
-#pragma unroll
-      for (int w = 1; w < PY_NW; ++w) {
-        const double ov = scan_v[e2 & 1][w];
-        const int oj = scan_r[e2 & 1][w];
-        if (oj >= 0 && (j0 < 0 || ov < v0 || (ov == v0 && oj < j0))) {
-          v0 = ov;
-          j0 = oj;
-        }
-      }
-      if (j0 >= 0) UU[l] = (uint16_t)j0;
-    }
-  }
+  // exact scan of the listed targets (UU only: their values came out of the pyramid)
+  py_scan_list<M, N0>(list, nl, psiarr, D, ncol, dfi, P.dt, beta, UU, nullptr);
   PY_STAMP(5);
+#ifdef MIOC_STAMPS
+  if (tid == 0) g_pyr_stamps[blockIdx.x][14] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (tid == 0 && nl) {
     atomicAdd(&counters[0], nl - nmulti);
     if (nmulti) atomicAdd(&counters[1], nmulti);

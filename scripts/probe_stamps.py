@@ -31,3 +31,15 @@ for (a, _), (b, nm) in zip(seq[:-1], seq[1:]):
 tot = s[:, 5] - s[:, 0]
 print(f"{'total':22s} cycles median {np.median(tot):9.0f}  max {tot.max():9.0f}")
 print("levels executed: median", np.median(s[:, 6]), "max", s[:, 6].max(), "min", s[:, 6].min())
+# global timeline (s_memrealtime, 100 MHz): when each workgroup started / ended relative to the first start
+rt0, rt1 = st[:, 13], st[:, 14]
+ok = (rt0 > 0) & (rt1 > 0)
+t0 = rt0[ok].min()
+s_us, e_us = (rt0[ok] - t0) / 100.0, (rt1[ok] - t0) / 100.0
+print(f"realtime: kernel span {e_us.max():.1f} us; start spread {np.percentile(s_us, [50, 90, 99, 100])} us;"
+      f" end median {np.median(e_us):.1f} p90 {np.percentile(e_us, 90):.1f} max {e_us.max():.1f} us")
+order = np.argsort(s_us)
+print("latest starters (row, start us, dur us):", [(int(np.nonzero(ok)[0][i]), round(float(s_us[i]), 1),
+      round(float(e_us[i] - s_us[i]), 1)) for i in order[-3:]])
+print("longest rows (row, dur us):", sorted([(int(np.nonzero(ok)[0][i]), round(float(e_us[i] - s_us[i]), 1))
+      for i in range(len(s_us))], key=lambda t: -t[1])[:5])
