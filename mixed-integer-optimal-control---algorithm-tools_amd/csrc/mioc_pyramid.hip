@@ -23,6 +23,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 
 #include "mioc_internal.h"
 
@@ -34,6 +35,8 @@ constexpr int PY_HS = 12288;       // hash slots (uint32): <= 4096 sources, load
 constexpr int PY_NB = PY_HS / 4;   // 16-byte buckets of 4 slots, each with a 16-bit arrival count
 constexpr int PY_OVF = 256;        // keys that found both of their buckets full
 constexpr int PY_G = 14;           // bucket width = 2^PY_G · δ (wide: few border checks; false collisions only cost exact scans)
+constexpr int PY_CMAX = 512;       // grid columns per row at most (level-buffer chunk stride)
+constexpr int PY_LVLB = PY_CMAX * 16;  // level-buffer bytes per point of a column: 2 parities x 8 B x PY_CMAX
 constexpr int PY_FEW = 48;         // rows with at most this many targets in the trust region: exact scans
 constexpr unsigned PY_RB = 13;     // hash entry = tag << PY_RB | (rank + 1); 0 = empty
 
@@ -159,28 +162,6 @@ struct PyrDims {  // geometry copied by value into registers (never escapes to m
   int base[kMaxM];
 };
 
-// A column (N0 doubles = N0/2 16-byte chunks) is stored with its chunks XOR-swizzled by the column's
-// position inside a 256-byte LDS row, so the 16 lanes of every ds_read_b128 / ds_write_b128 lane group
-// (consecutive columns) hit 16 distinct 4-bank slots: conflict-free (64-byte stride alone is 4-way).
-template <int N0>
-__device__ __forceinline__ int col_swz(int col) {
-  return (col / (32 / N0)) & (N0 / 2 - 1);
-}
-template <int N0>
-__device__ __forceinline__ void col_store(double *buf, int col, const double *v) {
-  double2 *base = reinterpret_cast<double2 *>(buf + (size_t)col * N0);
-  const int sw = col_swz<N0>(col);
-#pragma unroll
-  for (int c = 0; c < N0 / 2; ++c) base[c ^ sw] = make_double2(v[2 * c], v[2 * c + 1]);
-}
-template <int N0>
-__device__ __forceinline__ void col_load(const double *buf, int col, double2 *t) {
-  const double2 *base = reinterpret_cast<const double2 *>(buf + (size_t)col * N0);
-  const int sw = col_swz<N0>(col);
-#pragma unroll
-  for (int c = 0; c < N0 / 2; ++c) t[c] = base[c ^ sw];
-}
-
 // workgroup-wide OR of one flag per thread: wave ballot, one LDS word per wave, one barrier
 __device__ __forceinline__ bool py_any(bool f, int *slots) {
   const unsigned long long bal = __ballot(f);
@@ -302,8 +283,8 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   uint16_t *UU = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L) + (size_t)cp * L;
   const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
   const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
-  double *lvl = reinterpret_cast<double *>(pys);                             // [2][L] level buffers
-  double *psiarr = lvl + (size_t)2 * L;                                      // [L] Ψ_j by rank j
+  double *lvl = reinterpret_cast<double *>(pys);                             // level buffers (below)
+  double *psiarr = reinterpret_cast<double *>(pys + PY_LVLB * N0);           // [L] Ψ_j by rank j
   unsigned *htab = reinterpret_cast<unsigned *>(psiarr + L);                 // [PY_HS] hash buckets
   unsigned *hcnt = htab + PY_HS;                                             // [PY_NB / 2] arrival counts
   uint2 *hovf = reinterpret_cast<uint2 *>(hcnt + PY_NB / 2);                 // [PY_OVF] overflow list
@@ -570,7 +551,21 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   }
   unsigned multi = 0;
   int S = 0;
-  for (;; ++S) {
+  // Level buffers, chunk-major: [parity][N0/2 chunks][PY_CMAX columns] of 16-byte chunks.  Consecutive
+  // columns are consecutive 16-byte slots (conflict-free ds_read_b128 / ds_write_b128 lane groups),
+  // and chunk and parity are immediate offsets: every neighbour column needs one loop-invariant
+  // address register, and the loop is unrolled by two for the parity.
+  double2 *lv2 = reinterpret_cast<double2 *>(pys);
+  int ncl[M - 1][2];  // neighbour columns (the own column where the grid ends)
+#pragma unroll
+  for (int m = 1; m < M; ++m) {
+    const int st = G.cstride[m];
+    ncl[m - 1][0] = col - (((nbm >> (2 * m)) & 1) ? st : 0);
+    ncl[m - 1][1] = col + (((nbm >> (2 * m + 1)) & 1) ? st : 0);
+  }
+  auto level = [&](auto par_tag) -> bool {  // one level; true when the loop is over
+    constexpr int PAR = decltype(par_tag)::value;
+    constexpr int HALF = (N0 / 2) * PY_CMAX;
     unsigned mlt = 0, meq = 0;
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
@@ -583,7 +578,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       meq |= (unsigned)eq << x0;
     }
     multi = (multi & ~mlt) | meq;
-    if (S == Smax) break;
+    if (S == Smax) return true;
     // can a deeper level still reach (or tie) the minimum of some target of this workgroup?
     // (K_l(S) is non-decreasing in S: the pyramid is only selected for β >= 0)
     const double cN = beta * (double)(S + 1);
@@ -593,27 +588,29 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       K[x0] = T1[x0] + cN;
       more |= (K[x0] + Rmin) <= best[x0];
     }
-    double *buf = lvl + (size_t)(S & 1) * L;
-    if (colok) col_store<N0>(buf, col, cur);
+    if (colok) {
+#pragma unroll
+      for (int c = 0; c < N0 / 2; ++c) lv2[PAR * HALF + c * PY_CMAX + col] = make_double2(cur[2 * c], cur[2 * c + 1]);
+    }
     {
       const unsigned long long bal = __ballot(more);
-      if ((tid & 63) == 0) vote[S & 1][tid >> 6] = bal != 0ull;
+      if ((tid & 63) == 0) vote[PAR][tid >> 6] = bal != 0ull;
     }
     __syncthreads();
     // every LDS read of this level is issued before the first use
     int go = 0;
 #pragma unroll
-    for (int w = 0; w < PY_NW; ++w) go |= vote[S & 1][w];
+    for (int w = 0; w < PY_NW; ++w) go |= vote[PAR][w];
     double2 nb[M - 1][2][N0 / 2];
 #pragma unroll
-    for (int m = 1; m < M; ++m) {
-      const int st = G.cstride[m];
-      col_load<N0>(buf, col - (((nbm >> (2 * m)) & 1) ? st : 0), nb[m - 1][0]);
-      col_load<N0>(buf, col + (((nbm >> (2 * m + 1)) & 1) ? st : 0), nb[m - 1][1]);
-    }
-    if (!go) break;
+    for (int m = 0; m < M - 1; ++m)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int c = 0; c < N0 / 2; ++c) nb[m][s2][c] = lv2[PAR * HALF + c * PY_CMAX + ncl[m][s2]];
     // dilate by the unit cross: BM_{S+1}(x) = min(BM_S(x), BM_S(x ± e_m)); a missing neighbour
-    // reads the own column (min with itself is a no-op), so there is no divergence
+    // reads the own column (min with itself is a no-op), so there is no divergence.  The dilation
+    // runs before the exit test so the neighbour reads are issued together with the vote reads.
     double nw[N0];
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
@@ -633,6 +630,12 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
         }
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) cur[x0] = nw[x0];
+    ++S;
+    return !go;
+  };
+  for (;;) {
+    if (level(std::integral_constant<int, 0>{})) break;
+    if (level(std::integral_constant<int, 1>{})) break;
   }
   PY_STAMP(4);
 #ifdef MIOC_STAMPS
@@ -853,7 +856,7 @@ hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsD
 }
 
 size_t pyr_lds_bytes(const PyrGeom &G) {
-  return (size_t)3 * G.ncol * G.n[0] * sizeof(double) + (size_t)PY_HS * sizeof(unsigned) +
+  return (size_t)PY_LVLB * G.n[0] + (size_t)G.ncol * G.n[0] * sizeof(double) + (size_t)PY_HS * sizeof(unsigned) +
          (size_t)(PY_NB / 2) * sizeof(unsigned) + (size_t)PY_OVF * sizeof(uint2) + (size_t)G.ncol * G.n[0];
 }
 
