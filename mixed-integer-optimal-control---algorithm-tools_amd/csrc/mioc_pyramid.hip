@@ -266,6 +266,10 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   __shared__ int anyv[PY_NW];
   __shared__ int vote[2][PY_NW];        // per-wave early-exit votes, double-buffered by level parity
   __shared__ int nlist, nmulti, novf, nvalid;
+#ifdef MIOC_STAMPS
+  __shared__ int dbg_lv[2];
+  if (threadIdx.x == 0) dbg_lv[0] = dbg_lv[1] = 0;
+#endif
   PyrDims D;
 #pragma unroll
   for (int m = 0; m < kMaxM; ++m) {
@@ -628,6 +632,18 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
           nw[2 * c] = vmin(nw[2 * c], nb[m][s2][c].x);
           nw[2 * c + 1] = vmin(nw[2 * c + 1], nb[m][s2][c].y);
         }
+#ifdef MIOC_STAMPS
+    {
+      bool ch = false;
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) ch |= nw[x0] < cur[x0];
+      const unsigned long long bc = __ballot(ch);
+      if ((tid & 63) == 0) {
+        atomicAdd(&dbg_lv[0], 1);
+        if (bc) atomicAdd(&dbg_lv[1], 1);
+      }
+    }
+#endif
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) cur[x0] = nw[x0];
     ++S;
@@ -639,6 +655,8 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   }
   PY_STAMP(4);
 #ifdef MIOC_STAMPS
+  __syncthreads();
+  if (tid == 0) g_pyr_stamps[blockIdx.x][15] = ((unsigned long long)dbg_lv[0] << 32) | (unsigned)dbg_lv[1];
   if (tid == 0) g_pyr_stamps[blockIdx.x][6] = S;
 #endif
 

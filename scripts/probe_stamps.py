@@ -43,3 +43,6 @@ print("latest starters (row, start us, dur us):", [(int(np.nonzero(ok)[0][i]), r
       round(float(e_us[i] - s_us[i]), 1)) for i in order[-3:]])
 print("longest rows (row, dur us):", sorted([(int(np.nonzero(ok)[0][i]), round(float(e_us[i] - s_us[i]), 1))
       for i in range(len(s_us))], key=lambda t: -t[1])[:5])
+dl = st[full, 15]
+tot_wl, chg_wl = dl >> 32, dl & 0xFFFFFFFF
+print(f"wave-levels with a BM change: {chg_wl.sum()} of {tot_wl.sum()} ({100.0 * chg_wl.sum() / max(1, tot_wl.sum()):.1f}%)")
