@@ -196,13 +196,14 @@ int run_bellman(mioc_ctx *ctx) {
   const int bmax = ctx->h_flags[1];
 
   int algo = (int)ctx->opt_algo;
-  const bool pinf_ok = ctx->p_kind == MIOC_P_INF && bmax + 1 <= 64;
+  // the p=Inf recursion keeps two budget rows and the staged class rows in LDS
+  const bool pinf_ok = ctx->p_kind == MIOC_P_INF && bmax + 1 <= 64 && ctx->RP <= 7936;
   // the L1-ball identity min_j fl(K(d(l,j)) + Ψ_j) = min_S fl(K(S) + BM_S(l)) needs K non-decreasing in S
   const bool pyr_ok = ctx->p_kind == MIOC_P_ONE && ctx->pyr_ok && ctx->beta >= 0.0;
   if (algo == MIOC_ALGO_AUTO)
     algo = pinf_ok ? MIOC_ALGO_PINF : (pyr_ok && ctx->L >= 256 ? MIOC_ALGO_PYRAMID : MIOC_ALGO_GENERIC);
   if (algo == MIOC_ALGO_PINF && !pinf_ok)
-    return fail(ctx, MIOC_EINVAL, "p=Inf collapse needs p_kind MIOC_P_INF and <= 64 budget classes");
+    return fail(ctx, MIOC_EINVAL, "p=Inf collapse needs p_kind MIOC_P_INF, <= 64 budget classes and B < 7936");
   if (algo == MIOC_ALGO_PYRAMID && !pyr_ok)
     return fail(ctx, MIOC_EINVAL, "the L1-ball pyramid needs p = 1, beta >= 0 and a product grid of consecutive "
                                   "integer levels (first dimension 4 or 8 levels, <= 4096 tuples)");

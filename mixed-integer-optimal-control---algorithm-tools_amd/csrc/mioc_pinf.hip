@@ -126,58 +126,86 @@ __device__ __forceinline__ double dpp_swap_pair(double x) {  // value of lane ^ 
   return __hiloint2double(hi, lo);
 }
 
+// v_min_f64 without llvm.minnum's operand canonicalisation (inputs are finite or +Inf, never NaN)
+__device__ __forceinline__ double pvmin(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // ---------------------------------------------------------------------------------------------
 // sequential recursion over steps, one workgroup per subproblem.
 //   R_i[c] = min_{b < BWP} fl(Kmin_i[b] + R_{i+1}[c - b])      (padding: Kmin = +Inf, R[<0] = +Inf)
-// Two threads per budget row c split the classes (b even-half / odd-half) and combine through DPP.
-// Class rows for CH steps at a time are staged into LDS by LDS-DMA one chunk ahead; the barrier per
-// step waits only on LDS (lgkmcnt), so the streamed R_i stores and the next chunk's DMA stay in flight.
+// Thread t computes the budget rows c = 2t and 2t+1: its window R_{i+1}[2t-BWP+1 .. 2t+1] is BWP+1
+// consecutive values.  R is kept in LDS shifted by one (A[k] = R[k + 1 - BWP]), so every window
+// starts 16-byte aligned and is read with BWP/2 + 1 ds_read_b128; the class row Kmin_i is a broadcast
+// read.  Class rows for CH steps at a time are staged into LDS by LDS-DMA one chunk ahead; the barrier
+// per step waits only on LDS (lgkmcnt), so the streamed R_i stores and the next chunk's DMA stay in
+// flight.  Four independent min accumulators per output keep the dependency chain short.
 // ---------------------------------------------------------------------------------------------
 template <int BWP>
-__global__ __launch_bounds__(1024) void k_pinf_recur(ProblemDev P, PinfDev D, int CH) {
+__global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int CH) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  constexpr int HB = BWP / 2;
+  constexpr int NP = BWP / 2 + 1;  // 16-byte pieces of a window
   const int RP = P.RP, B = P.B, nt = P.nt, k = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
-  double *Ra = sm, *Rb = sm + (BWP + RP), *Kbuf = Rb + (BWP + RP);  // Kbuf: [2][CH][BWP]
+  const int AW = RP + BWP;                     // even: RP is a multiple of 64
+  double *A = sm, *Kbuf = sm + 2 * AW;         // A: [2 parities][AW]; Kbuf: [2][CH][BWP]
   const double *kmin = D.kmin + (size_t)k * nt * BWP;
   double *R = D.R + (size_t)k * nt * RP;
-  for (int c = tid; c < BWP + RP; c += nthr) {
-    const int cc = c - BWP;
-    const double v = (cc >= 0 && cc < BWP) ? kmin[(size_t)(nt - 1) * BWP + cc] : INFINITY;
-    Ra[c] = v;
-    Rb[c] = INFINITY;
-    if (cc >= 0) R[(size_t)(nt - 1) * RP + cc] = (cc <= B) ? v : INFINITY;
+  {
+    const int pt = (nt - 1) & 1;  // terminal row R_{n-1}[c] = Kmin_{n-1}[c] (class minima of T1, no β)
+    for (int q = tid; q < 2 * AW; q += nthr) {
+      const int par = q / AW, kk = q % AW, c = kk + 1 - BWP;
+      double v = INFINITY;
+      if (par == pt && c >= 0 && c < BWP) v = kmin[(size_t)(nt - 1) * BWP + c];
+      A[q] = v;
+      if (par == pt && c >= 0 && c < RP) R[(size_t)(nt - 1) * RP + c] = c <= B ? v : INFINITY;
+    }
   }
   if (nt < 2) return;
   int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
   glds_copy(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, tid, nthr);
   vm_drain();
   lds_barrier();
-  double *Rp = Ra, *Rn = Rb;
-  const int h = tid & 1;
   for (int q = 0; hi >= 0; ++q) {
-    double *Kc = Kbuf + (size_t)(q & 1) * CH * BWP;
+    const double *Kc = Kbuf + (size_t)(q & 1) * CH * BWP;
     const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
     if (nhi >= 0)
       glds_copy(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8, tid,
                 nthr);
     for (int i = hi; i >= lo; --i) {
-      const double *Krow = Kc + (i - lo) * BWP + h * HB;
-      for (int c = tid >> 1; c < RP; c += nthr >> 1) {
-        const double *Rrow = Rp + BWP + c - h * HB;
-        double m = INFINITY;
+      for (int c0 = 2 * tid; c0 < RP; c0 += 2 * nthr) {
+        const double2 *win = reinterpret_cast<const double2 *>(A + (size_t)((i + 1) & 1) * AW + c0);
+        const double2 *kr = reinterpret_cast<const double2 *>(Kc + (size_t)(i - lo) * BWP);
+        double w[2 * NP], kv[BWP];
 #pragma unroll
-        for (int j = 0; j < HB; ++j) m = fmin(m, Krow[j] + Rrow[-j]);
-        m = fmin(m, dpp_swap_pair(m));
-        if (h == 0 && c <= B) {
-          Rn[BWP + c] = m;
-          R[(size_t)i * RP + c] = m;
+        for (int p2 = 0; p2 < NP; ++p2) {
+          const double2 x = win[p2];
+          w[2 * p2] = x.x;
+          w[2 * p2 + 1] = x.y;
         }
+#pragma unroll
+        for (int p2 = 0; p2 < BWP / 2; ++p2) {
+          const double2 y = kr[p2];
+          kv[2 * p2] = y.x;
+          kv[2 * p2 + 1] = y.y;
+        }
+        // row 2t:   R_{i+1}[2t - b]   = w[BWP - 1 - b];   row 2t+1: R_{i+1}[2t + 1 - b] = w[BWP - b]
+        double m0[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, m1[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+#pragma unroll
+        for (int b2 = 0; b2 < BWP; ++b2) {
+          m0[b2 & 3] = pvmin(m0[b2 & 3], kv[b2] + w[BWP - 1 - b2]);
+          m1[b2 & 3] = pvmin(m1[b2 & 3], kv[b2] + w[BWP - b2]);
+        }
+        const double r0 = pvmin(pvmin(m0[0], m0[1]), pvmin(m0[2], m0[3]));
+        const double r1 = pvmin(pvmin(m1[0], m1[1]), pvmin(m1[2], m1[3]));
+        double *Aout = A + (size_t)(i & 1) * AW;
+        Aout[c0 + BWP - 1] = r0;
+        Aout[c0 + BWP] = r1;
+        R[(size_t)i * RP + c0] = c0 <= B ? r0 : INFINITY;
+        R[(size_t)i * RP + c0 + 1] = c0 + 1 <= B ? r1 : INFINITY;
       }
       lds_barrier();
-      double *t = Rp;
-      Rp = Rn;
-      Rn = t;
     }
     vm_drain();
     lds_barrier();
@@ -189,8 +217,8 @@ __global__ __launch_bounds__(1024) void k_pinf_recur(ProblemDev P, PinfDev D, in
 int pinf_chunk_recur(int BWP) { return BWP <= 16 ? 64 : 32; }
 
 hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D) {
-  int threads = 2 * P.RP;
-  if (threads > 1024) threads = 1024;
+  int threads = ((P.RP / 2 + 63) / 64) * 64;  // one thread per two budget rows
+  if (threads > 512) threads = 512;
   const int CH = pinf_chunk_recur(D.BWP);
   size_t lds = (size_t)(2 * (D.BWP + P.RP) + 2 * CH * D.BWP) * sizeof(double);
   switch (D.BWP) {

@@ -734,6 +734,12 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   if (novf > PY_OVF) tolist |= want;  // the overflow list itself overflowed: exact scans for this row
   if (tid == 0 && novf) atomicAdd(&counters[4], 1);
   PY_STAMP(10);
+  uint4 po[N0 / 4];  // sphere order of step i for the output row, fetched before the barrier
+  if (colok) {
+    const uint4 *p4 = reinterpret_cast<const uint4 *>(pout + N0 * col);
+#pragma unroll
+    for (int c = 0; c < N0 / 4; ++c) po[c] = p4[c];
+  }
   __syncthreads();  // the level buffers are free: the list and the natural-order outputs live there
   int *list = reinterpret_cast<int *>(lvl);
   double *outnat = lvl + L;
@@ -768,11 +774,10 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   PY_STAMP(11);
   // Φ_i row c' in the sphere order of u_old(i): gathered from LDS, written as one contiguous run
   if (colok) {
-    const uint4 *p4 = reinterpret_cast<const uint4 *>(pout + N0 * col);
     double o[N0];
 #pragma unroll
     for (int c = 0; c < N0 / 4; ++c) {
-      const uint4 t = p4[c];
+      const uint4 t = po[c];
       o[4 * c] = outnat[t.x & 0xFFFFu];
       o[4 * c + 1] = outnat[t.y & 0xFFFFu];
       o[4 * c + 2] = outnat[t.z & 0xFFFFu];
