@@ -91,16 +91,19 @@ def run(args, rank, world, device, dist, torch):
             _, df, uo = make_inputs(cfg, k=k, nt=nt, levels=levels)
             dfs.append(df)
             uos.append(uo)
-    d_df = torch.tensor(np.stack([d.T for d in dfs]), dtype=torch.float64, device=device).reshape(nsets, K, nt, -1)
-    d_uo = torch.tensor(np.stack([d.T for d in uos]), dtype=torch.float64, device=device).reshape(nsets, K, nt, -1)
+    # (sets, K, nt, nx) C-contiguous: each subproblem's nx x nt block column-major (mioc_bellman_batch_device)
+    d_df = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in dfs])), dtype=torch.float64,
+                        device=device).reshape(nsets, K, nt, -1).contiguous()
+    d_uo = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in uos])), dtype=torch.float64,
+                        device=device).reshape(nsets, K, nt, -1).contiguous()
     d_u = torch.empty((K, nt, levels.M), dtype=torch.float64, device=device)
     d_phi = torch.empty(K, dtype=torch.float64, device=device)
     d_st = torch.empty(K, dtype=torch.int32, device=device)
     nuval = torch.tensor(levels.nuval, dtype=torch.float64, device=device)
 
     def step(s):
-        ctx.bellman_batch_device(K, d_df[s].data_ptr(), d_uo[s].data_ptr(), levels.M, nt, B, dt)
-        ctx.backtrack_batch_device(B, d_u.data_ptr(), d_phi.data_ptr(), d_st.data_ptr())
+        ctx.bellman_batch_tensors(d_df[s], d_uo[s], B, dt)
+        ctx.backtrack_batch_tensors(B, d_u, d_phi, d_st)
         if world > 1:
             ctx.synchronize()
             # controls as level ranks (uint16 payload) + Φ*, gathered to rank 0 over RCCL

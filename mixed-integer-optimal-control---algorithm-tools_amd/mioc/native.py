@@ -212,6 +212,28 @@ class Context:
                                                          ctypes.c_void_p(phi_ptr or None),
                                                          ctypes.c_void_p(status_ptr or None)))
 
+    # -- the same, from torch tensors (shape/contiguity checked: the raw-pointer API cannot check) --
+    def bellman_batch_tensors(self, df, u_old, B, dt):
+        """df, u_old: float64 CUDA tensors of shape (K, nt, nx), C-contiguous (each subproblem's nx x nt
+        column-major block, the layout of mioc_bellman_batch_device)."""
+        for name, t in (("df", df), ("u_old", u_old)):
+            if t.dim() != 3 or not t.is_contiguous() or not t.is_cuda or str(t.dtype) != "torch.float64":
+                raise ValueError(f"{name} must be a contiguous float64 CUDA tensor of shape (K, nt, nx)")
+        if tuple(df.shape) != tuple(u_old.shape):
+            raise ValueError("df and u_old must have the same shape (K, nt, nx)")
+        K, nt, nx = df.shape
+        self.bellman_batch_device(K, df.data_ptr(), u_old.data_ptr(), nx, nt, B, dt)
+
+    def backtrack_batch_tensors(self, B_use, u, phi=None, status=None):
+        """u: float64 CUDA tensor (K, nt, nx), contiguous; phi: (K,) float64; status: (K,) int32."""
+        if u.dim() != 3 or not u.is_contiguous() or not u.is_cuda or str(u.dtype) != "torch.float64":
+            raise ValueError("u must be a contiguous float64 CUDA tensor of shape (K, nt, nx)")
+        for name, t, dt_ in (("phi", phi, "torch.float64"), ("status", status, "torch.int32")):
+            if t is not None and (not t.is_contiguous() or str(t.dtype) != dt_ or t.numel() != u.shape[0]):
+                raise ValueError(f"{name} must be a contiguous {dt_} tensor with K entries")
+        self.backtrack_batch_device(B_use, u.data_ptr(), 0 if phi is None else phi.data_ptr(),
+                                    0 if status is None else status.data_ptr())
+
     def synchronize(self):
         self._check(self.lib.mioc_synchronize(self.h))
 

@@ -221,6 +221,58 @@ def test_full_size_c4_properties(p):
     ctx.close()
 
 
+def test_pyramid_batch_equals_single(oracle_c):
+    """K=3 subproblems through the batch API on the pyramid: per-subproblem staging, U and sphere-order
+    strides.  Controls, Φ* and every written U cell equal three single runs."""
+    import torch
+    lt = LevelTable([list(range(8))] * 3)
+    lv = _oracle_levels(lt)
+    K, nt, B, beta, dt = 3, 14, 24, 1e-3, 2.0 ** -9
+    rng = np.random.default_rng(42)
+    dfs = [rng.standard_normal((3, nt)) for _ in range(K)]
+    uos = [np.array([lt.nuval[rng.integers(lt.L)] for _ in range(nt)], dtype=np.float64).T for _ in range(K)]
+    ctx = _ctx(lt, P_ONE, beta, native.MIOC_ALGO_PYRAMID)
+    ddf = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in dfs])), dtype=torch.float64, device="cuda")
+    duo = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in uos])), dtype=torch.float64, device="cuda")
+    du = torch.empty_like(ddf)
+    dphi = torch.empty(K, dtype=torch.float64, device="cuda")
+    dst = torch.empty(K, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.bellman_batch_tensors(ddf, duo, B, dt)
+    ctx.backtrack_batch_tensors(B, du, dphi, dst)
+    ctx.synchronize()
+    assert ctx.last_algo() == native.MIOC_ALGO_PYRAMID
+    ub = du.cpu().numpy()
+    for k in range(K):
+        single = _ctx(lt, P_ONE, beta, native.MIOC_ALGO_PYRAMID)
+        single.bellman(dfs[k], uos[k], B, dt)
+        u, ps, _ = single.backtrack(B)
+        assert np.array_equal(ub[k].T, u) and dphi[k].item() == ps and dst[k].item() == 0, f"k={k}"
+        phi, U = oracle_c.bellman(lv, dfs[k], uos[k], B, P_ONE, beta, dt)
+        for i in range(nt - 1):  # every cell the reference writes
+            d, o = ctx.argmin_table(i, k=k), U[:, :, i]
+            m = o >= 0
+            assert np.array_equal(d[m], o[m]), f"k={k} step {i}"
+        single.close()
+    ctx.close()
+
+
+def test_batch_tensor_api_rejects_strided_inputs():
+    """np.stack of transposed views is Fortran-ordered and torch.tensor keeps those strides: the raw
+    pointer would address a permuted layout, so the tensor API must refuse it."""
+    import torch
+    lt = LevelTable([[0, 1, 2]] * 2)
+    ctx = _ctx(lt, P_ONE, 0.1, native.MIOC_ALGO_GENERIC)
+    d = np.zeros((2, 5))
+    bad = torch.tensor(np.stack([d.T]), dtype=torch.float64, device="cuda")
+    assert not bad.is_contiguous()
+    with pytest.raises(ValueError):
+        ctx.bellman_batch_tensors(bad, bad, 2, 0.1)
+    good = bad.contiguous()
+    ctx.bellman_batch_tensors(good, good, 2, 0.1)
+    ctx.close()
+
+
 def test_batch_device_api_equals_single():
     import torch
     cfg = CONFIGS["C5"]
@@ -234,8 +286,8 @@ def test_batch_device_api_equals_single():
     for pk, algos in ((P_ONE, (native.MIOC_ALGO_GENERIC,)), (P_INF, ALGOS_PINF)):
         for algo in algos:
             ctx = _ctx(lt, pk, cfg.beta, algo)
-            ddf = torch.tensor(np.stack([d.T for d in dfs]), dtype=torch.float64, device="cuda")
-            duo = torch.tensor(np.stack([d.T for d in uos]), dtype=torch.float64, device="cuda")
+            ddf = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in dfs])), dtype=torch.float64, device="cuda")
+            duo = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in uos])), dtype=torch.float64, device="cuda")
             du = torch.empty_like(ddf)
             dphi = torch.empty(K, dtype=torch.float64, device="cuda")
             dst = torch.empty(K, dtype=torch.int32, device="cuda")
