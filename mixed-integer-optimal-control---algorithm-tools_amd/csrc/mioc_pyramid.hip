@@ -553,7 +553,11 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     best[x0] = (valid >> x0 & 1) ? INFINITY : -INFINITY;
     bmb[x0] = INFINITY;
   }
-  unsigned multi = 0;
+  // per point: the wave's lanes whose minimum was tied at a later level (wave-uniform 64-bit masks, so
+  // the bookkeeping is scalar and issues beside the vector work)
+  unsigned long long mm[N0];
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) mm[x0] = 0ull;
   int S = 0;
   // Level buffers, chunk-major: [parity][N0/2 chunks][PY_CMAX columns] of 16-byte chunks.  Consecutive
   // columns are consecutive 16-byte slots (conflict-free ds_read_b128 / ds_write_b128 lane groups),
@@ -570,7 +574,6 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   auto level = [&](auto par_tag) -> bool {  // one level; true when the loop is over
     constexpr int PAR = decltype(par_tag)::value;
     constexpr int HALF = (N0 / 2) * PY_CMAX;
-    unsigned mlt = 0, meq = 0;
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
       const double cand = K[x0] + cur[x0];
@@ -578,10 +581,8 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       const bool eq = cand == best[x0];  // Inf == Inf ties only mark targets left at +Inf (never listed)
       best[x0] = vmin(cand, best[x0]);
       bmb[x0] = lt ? cur[x0] : bmb[x0];
-      mlt |= (unsigned)lt << x0;
-      meq |= (unsigned)eq << x0;
+      mm[x0] = (mm[x0] & ~__ballot(lt)) | __ballot(eq);
     }
-    multi = (multi & ~mlt) | meq;
     if (S == Smax) return true;
     // can a deeper level still reach (or tie) the minimum of some target of this workgroup?
     // (K_l(S) is non-decreasing in S: the pyramid is only selected for β >= 0)
@@ -663,6 +664,9 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   // ---- argmin.  A target whose minimum is reached at one level only, by a value with no close
   // neighbour, has a unique minimiser: the source holding that value (one bucket-pair read).  Every
   // other target with a finite minimum goes to the exact scan below. --------------------------------
+  unsigned multi = 0;
+#pragma unroll
+  for (int x0 = 0; x0 < N0; ++x0) multi |= (unsigned)((mm[x0] >> (tid & 63)) & 1ull) << x0;
   int rk[N0];
   unsigned want = 0;
 #pragma unroll
