@@ -15,3 +15,6 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/pmc -o p1_write --output-form
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/pmc -o pinf_fetch --output-format csv -- python3 bench.py $A --p inf > $O/pmc/pinf_fetch.txt 2>&1 &&
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/pmc -o pinf_write --output-format csv -- python3 bench.py $A --p inf > $O/pmc/pinf_write.txt 2>&1
 rc=$?; echo "pmc exit=$rc"; ls $O/pmc
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES -d $O/pmc -o lds1 --output-format csv -- python3 scripts/probe_pyr.py 64 > $O/pmc/lds1.txt 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_SALU -d $O/pmc -o lds2 --output-format csv -- python3 scripts/probe_pyr.py 64 > $O/pmc/lds2.txt 2>&1
+echo "pmc-lds exit=$?"
