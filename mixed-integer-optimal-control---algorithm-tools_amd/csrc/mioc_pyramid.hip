@@ -29,14 +29,16 @@
 
 namespace mioc {
 
-constexpr int PY_T = 512;          // threads per workgroup: one grid column (dim-0 run) per thread
+constexpr int PY_T = 1024;         // threads per workgroup: 16 waves, 4 per SIMD
+constexpr int PY_TPC = 2;          // threads per grid column (dim-0 run): each owns N0 / PY_TPC points
 constexpr int PY_NW = PY_T / 64;   // waves per workgroup
 constexpr int PY_HS = 12288;       // hash slots (uint32): <= 4096 sources, load <= 1/3
 constexpr int PY_NB = PY_HS / 4;   // 16-byte buckets of 4 slots, each with a 16-bit arrival count
 constexpr int PY_OVF = 256;        // keys that found both of their buckets full
 constexpr int PY_G = 14;           // bucket width = 2^PY_G · δ (wide: few border checks; false collisions only cost exact scans)
 constexpr int PY_CMAX = 512;       // grid columns per row at most (level-buffer chunk stride)
-constexpr int PY_LVLB = PY_CMAX * 16;  // level-buffer bytes per point of a column: 2 parities x 8 B x PY_CMAX
+constexpr int PY_CS2 = PY_CMAX + 4;    // level-buffer chunk stride in 16-byte slots (64-byte pad: bank groups)
+constexpr int PY_LVLB = PY_CS2 * 16;   // level-buffer bytes per point of a column: 2 parities x 8 B x PY_CS2
 constexpr int PY_FEW = 48;         // rows with at most this many targets in the trust region: exact scans
 constexpr unsigned PY_RB = 13;     // hash entry = tag << PY_RB | (rank + 1); 0 = empty
 
@@ -162,6 +164,25 @@ struct PyrDims {  // geometry copied by value into registers (never escapes to m
   int base[kMaxM];
 };
 
+// PT consecutive uint32 (PT = 2 or 4) with one vector load
+template <int PT>
+__device__ __forceinline__ void py_load_u32(const uint32_t *p, uint32_t *e) {
+  if constexpr (PT == 4) {
+    const uint4 t = *reinterpret_cast<const uint4 *>(p);
+    e[0] = t.x, e[1] = t.y, e[2] = t.z, e[3] = t.w;
+  } else {
+    const uint2 t = *reinterpret_cast<const uint2 *>(p);
+    e[0] = t.x, e[1] = t.y;
+  }
+}
+
+// value of lane ^ 1 (DPP quad_perm [1,0,3,2]): the other half of the thread pair's grid column
+__device__ __forceinline__ double py_swap_pair(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
 // workgroup-wide OR of one flag per thread: wave ballot, one LDS word per wave, one barrier
 __device__ __forceinline__ bool py_any(bool f, int *slots) {
   const unsigned long long bal = __ballot(f);
@@ -261,6 +282,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
                                                    int32_t *__restrict__ counters) {
   static_assert(N0 == 4 || N0 == 8, "column length");
   static_assert(M >= 2, "product grid");
+  constexpr int PT = N0 / PY_TPC;  // points per thread: thread pairs share a grid column
   extern __shared__ __attribute__((aligned(16))) unsigned char pys[];
   __shared__ double red[2][PY_NW];
   __shared__ int anyv[PY_NW];
@@ -298,9 +320,12 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   if (tid == 0) g_pyr_stamps[blockIdx.x][13] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-  // ---- this thread's grid column: coordinates 1..M-1 are shared by its N0 points ---------------
-  const bool colok = tid < ncol;
-  const int col = colok ? tid : 0;
+  // ---- this thread's half column: coordinates 1..M-1 are shared by the column's N0 points; thread h of
+  // the pair owns x0 = PT*h .. PT*h + PT-1, ranks pbase .. pbase + PT-1 -----------------------------
+  const int h = tid & (PY_TPC - 1);
+  const bool colok = (tid / PY_TPC) < ncol;
+  const int col = colok ? tid / PY_TPC : 0;
+  const int pbase = N0 * col + PT * h;
   double a[M], pc[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) a[m] = P.dt * dfi[m];
@@ -319,54 +344,51 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     }
   }
   const double u00 = uoi[0];
+  // δ >= 2 ulp of any candidate fl(K + Ψ):  |K| <= sum_m |Δt·df_m|·max|ν_m| + β·Smax (so a[] dies early)
+  double kb = beta * (double)Smax;
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+    kb += fabs(a[m]) * fmax(fabs((double)D.base[m]), fabs((double)(D.base[m] + D.n[m] - 1)));
 
   // ---- sources: Ψ_j = Φ_{i+1}[j, c'] = S_{i+1}[c' - b̃_j(i+1)][pos(j)].  Rows are stored in the sphere
-  // order of u_old(i+1), so thread t reads positions N0·t .. N0·t+N0-1 -- one contiguous run of a
+  // order of u_old(i+1), so thread t reads positions PT·t .. PT·t+PT-1 -- one contiguous run of a
   // row for all positions of one sphere -- and scatters them into Ψ-by-rank (psiarr) in LDS ----------
   const uint32_t *pin = perm_all + ((size_t)k * P.nt + i + 1) * L;
   const uint32_t *pout = perm_all + ((size_t)k * P.nt + i) * L;
   if (tid == 0) nvalid = 0;
   if (colok) {
-    uint32_t e[N0];
-    const uint4 *p4 = reinterpret_cast<const uint4 *>(pin + N0 * col);
+    uint32_t e[PT];
+    py_load_u32<PT>(pin + pbase, e);
+    double v[PT];
 #pragma unroll
-    for (int c = 0; c < N0 / 4; ++c) {
-      const uint4 t = p4[c];
-      e[4 * c] = t.x;
-      e[4 * c + 1] = t.y;
-      e[4 * c + 2] = t.z;
-      e[4 * c + 3] = t.w;
-    }
-    double v[N0];
-#pragma unroll
-    for (int q = 0; q < N0; ++q) {
+    for (int q = 0; q < PT; ++q) {
       const int row = cp - (int)(e[q] >> 16);
-      v[q] = Sin[(size_t)(row >= 0 ? row : 0) * L + N0 * col + q];
+      v[q] = Sin[(size_t)(row >= 0 ? row : 0) * L + pbase + q];
       if (row < 0) v[q] = INFINITY;
     }
 #pragma unroll
-    for (int q = 0; q < N0; ++q) psiarr[e[q] & 0xFFFFu] = v[q];
+    for (int q = 0; q < PT; ++q) psiarr[e[q] & 0xFFFFu] = v[q];
   }
   __syncthreads();
   // ---- own points: targets (T1, validity) and sources (Ψ) -----------------------------------------
   // invalid targets carry T1 = +Inf and best = -Inf, so the level loop needs no branches
-  double cur[N0], T1[N0];
+  double cur[PT], T1[PT];
   unsigned valid = 0, fin = 0;
   if (colok) {
-    const double2 *p2 = reinterpret_cast<const double2 *>(psiarr + N0 * col);
+    const double2 *p2 = reinterpret_cast<const double2 *>(psiarr + pbase);
 #pragma unroll
-    for (int c = 0; c < N0 / 2; ++c) {
+    for (int c = 0; c < PT / 2; ++c) {
       const double2 t = p2[c];
       cur[2 * c] = t.x;
       cur[2 * c + 1] = t.y;
     }
   } else {
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) cur[x0] = INFINITY;
+    for (int x0 = 0; x0 < PT; ++x0) cur[x0] = INFINITY;
   }
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {
-    const double nu0 = (double)(D.base[0] + x0);
+  for (int x0 = 0; x0 < PT; ++x0) {
+    const double nu0 = (double)(D.base[0] + PT * h + x0);
     double t = 0.0;
     t = t + a[0] * nu0;  // ((0 + (Δt*df_1)*ν_1) + ...), HelpFunctions.jl:52-57
 #pragma unroll
@@ -379,7 +401,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   }
   double psimax = 0.0, psimin = INFINITY;
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {
+  for (int x0 = 0; x0 < PT; ++x0) {
     const bool f = fin >> x0 & 1;
     psimax = fmax(psimax, f ? fabs(cur[x0]) : 0.0);
     psimin = fmin(psimin, cur[x0]);
@@ -405,7 +427,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   if (!any_valid || !(Rmin < INFINITY)) {  // no target in the trust region, or nothing reachable
     if (colok) {
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) Sout[x0 + N0 * col] = INFINITY;
+      for (int x0 = 0; x0 < PT; ++x0) Sout[pbase + x0] = INFINITY;
     }
     return;
   }
@@ -417,36 +439,26 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     __syncthreads();
     if (colok) {
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
-        outnat[x0 + N0 * col] = INFINITY;
-        if (valid >> x0 & 1) list[atomicAdd(&nlist, 1)] = x0 + N0 * col;
+      for (int x0 = 0; x0 < PT; ++x0) {
+        outnat[pbase + x0] = INFINITY;
+        if (valid >> x0 & 1) list[atomicAdd(&nlist, 1)] = pbase + x0;
       }
     }
     __syncthreads();
     py_scan_list<M, N0>(list, nlist, psiarr, D, ncol, dfi, P.dt, beta, UU, outnat);
     __syncthreads();
     if (colok) {
-      const uint4 *p4 = reinterpret_cast<const uint4 *>(pout + N0 * col);
-      double o[N0];
+      uint32_t e[PT];
+      py_load_u32<PT>(pout + pbase, e);
+      double o[PT];
 #pragma unroll
-      for (int c = 0; c < N0 / 4; ++c) {
-        const uint4 t = p4[c];
-        o[4 * c] = outnat[t.x & 0xFFFFu];
-        o[4 * c + 1] = outnat[t.y & 0xFFFFu];
-        o[4 * c + 2] = outnat[t.z & 0xFFFFu];
-        o[4 * c + 3] = outnat[t.w & 0xFFFFu];
-      }
-      double2 *s2 = reinterpret_cast<double2 *>(Sout + N0 * col);
+      for (int q = 0; q < PT; ++q) o[q] = outnat[e[q] & 0xFFFFu];
+      double2 *s2 = reinterpret_cast<double2 *>(Sout + pbase);
 #pragma unroll
-      for (int c = 0; c < N0 / 2; ++c) s2[c] = make_double2(o[2 * c], o[2 * c + 1]);
+      for (int c = 0; c < PT / 2; ++c) s2[c] = make_double2(o[2 * c], o[2 * c + 1]);
     }
     return;
   }
-  // δ >= 2 ulp of any candidate fl(K + Ψ):  |K| <= sum_m |Δt·df_m|·max|ν_m| + β·Smax
-  double kb = beta * (double)Smax;
-#pragma unroll
-  for (int m = 0; m < M; ++m)
-    kb += fabs(a[m]) * fmax(fabs((double)D.base[m]), fabs((double)(D.base[m] + D.n[m] - 1)));
   const double Y = (Pmax + kb) * (1.0 + 0x1p-40) + 0x1p-1000;
   const int E = ilogb(Y) + 1;                                  // |y| < 2^E for every candidate y
   const double inv_w = ldexp(1.0, min(52 - PY_G - E, 1000));  // bucket width 2^(E-52+G) >= δ = 2^(E-52)
@@ -455,9 +467,9 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   // ---- collision flags: coll[j] = 1 iff some other finite Ψ lies within δ of Ψ_j (it shares Ψ_j's
   // bucket, or sits across a bucket border close to it).  Inserts advance in lock-step so their LDS
   // atomics overlap; duplicates are inserted too. -----------------------------------------------------
-  double fq[N0], fr[N0];
+  double fq[PT], fr[PT];
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {
+  for (int x0 = 0; x0 < PT; ++x0) {
     const double x = (fin >> x0 & 1) ? cur[x0] * inv_w : 0.0;
     fq[x0] = floor(x) + 0.0;
     fr[x0] = x - fq[x0];
@@ -480,20 +492,20 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   H.hcnt = hcnt;
   H.hovf = hovf;
   {
-    PyKey key[N0];
-    unsigned ent[N0], cnt[N0];
+    PyKey key[PT];
+    unsigned ent[PT], cnt[PT];
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
+    for (int x0 = 0; x0 < PT; ++x0) {
       key[x0] = py_key(fq[x0]);
-      ent[x0] = key[x0].tag << PY_RB | (unsigned)(x0 + N0 * col + 1);
+      ent[x0] = key[x0].tag << PY_RB | (unsigned)(pbase + x0 + 1);
     }
     // first fit: slot `count` of b1, else of b2, else the overflow list (one atomic round each)
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0)
+    for (int x0 = 0; x0 < PT; ++x0)
       cnt[x0] = (fin >> x0 & 1) ? atomicAdd(&hcnt[key[x0].b1 >> 1], 1u << ((key[x0].b1 & 1) * 16)) : 0u;
     unsigned spill = 0;
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
+    for (int x0 = 0; x0 < PT; ++x0) {
       if (!(fin >> x0 & 1)) continue;
       const unsigned c = (cnt[x0] >> ((key[x0].b1 & 1) * 16)) & 0xFFFFu;
       if (c < 4)
@@ -503,10 +515,10 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     }
     if (spill) {
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0)
+      for (int x0 = 0; x0 < PT; ++x0)
         cnt[x0] = (spill >> x0 & 1) ? atomicAdd(&hcnt[key[x0].b2 >> 1], 1u << ((key[x0].b2 & 1) * 16)) : 0u;
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
+      for (int x0 = 0; x0 < PT; ++x0) {
         if (!(spill >> x0 & 1)) continue;
         const unsigned c = (cnt[x0] >> ((key[x0].b2 & 1) * 16)) & 0xFFFFu;
         if (c < 4) {
@@ -524,59 +536,62 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     // close across a bucket border (same-bucket pairs are caught by the lookups below)
     unsigned hit = 0, need = 0;
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
+    for (int x0 = 0; x0 < PT; ++x0) {
       if (!(fin >> x0 & 1)) continue;
       need |= (unsigned)(fr[x0] <= FR) << (x0 + 8);
       need |= (unsigned)(fr[x0] >= 1.0 - FR) << (x0 + 16);
     }
     // cold: full searches (bucket b1, spill places) -- one copy of the code, operands from LDS
 #pragma unroll 1
-    for (int q = 0; q < 3 * N0; ++q) {
-      const int x0 = q % N0, kind = q / N0;
+    for (int q = 0; q < 3 * PT; ++q) {
+      const int x0 = q % PT, kind = q / PT;
       if (!(need >> (x0 + 8 * kind) & 1)) continue;
-      const int me = x0 + N0 * col;
+      const int me = pbase + x0;
       const double fqs = py_bucket(psiarr[me], inv_w) + (kind == 1 ? -1.0 : kind == 2 ? 1.0 : 0.0);
       if (py_search(H, psiarr, coll, py_key(fqs), fqs, inv_w, 0.0, me, 0) >= 0) hit |= 1u << x0;
     }
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0)
-      if (hit >> x0 & 1) coll[x0 + N0 * col] = 1;
+    for (int x0 = 0; x0 < PT; ++x0)
+      if (hit >> x0 & 1) coll[pbase + x0] = 1;
     if (hit) atomicAdd(&counters[6], __popc(hit));
   }
   PY_STAMP(3);
 
   // ---- the pyramid (branch-free level loop) ------------------------------------------------------
-  double K[N0], best[N0], bmb[N0];
+  double best[PT], bmb[PT];
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {
-    K[x0] = T1[x0] + beta * 0.0;  // K_l(0) = fl(T1 + fl(β·0))
+  for (int x0 = 0; x0 < PT; ++x0) {
     best[x0] = (valid >> x0 & 1) ? INFINITY : -INFINITY;
     bmb[x0] = INFINITY;
   }
   // per point: the wave's lanes whose minimum was tied at a later level (wave-uniform 64-bit masks, so
   // the bookkeeping is scalar and issues beside the vector work)
-  unsigned long long mm[N0];
+  unsigned long long mm[PT];
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) mm[x0] = 0ull;
+  for (int x0 = 0; x0 < PT; ++x0) mm[x0] = 0ull;
   int S = 0;
-  // Level buffers, chunk-major: [parity][N0/2 chunks][PY_CMAX columns] of 16-byte chunks.  Consecutive
-  // columns are consecutive 16-byte slots (conflict-free ds_read_b128 / ds_write_b128 lane groups),
-  // and chunk and parity are immediate offsets: every neighbour column needs one loop-invariant
-  // address register, and the loop is unrolled by two for the parity.
+  // Level buffers, chunk-major: [parity][N0/2 chunks][PY_CS2 columns] of 16-byte chunks.  Consecutive
+  // columns are consecutive 16-byte slots and the chunk stride is padded by 64 bytes, so the two
+  // halves of a column (chunks 0..PT/2-1 and PT/2..) fall in different bank groups: conflict-free
+  // ds_read_b128 / ds_write_b128 lane groups.  Chunk and parity are immediate offsets: every neighbour
+  // column needs one loop-invariant address register, and the loop is unrolled by two for the parity.
   double2 *lv2 = reinterpret_cast<double2 *>(pys);
-  int ncl[M - 1][2];  // neighbour columns (the own column where the grid ends)
+  const int hoff = h * (PT / 2) * PY_CS2;  // this thread's half column: its first chunk
+  int ncl[M - 1][2];  // neighbour half columns (the own column where the grid ends)
 #pragma unroll
   for (int m = 1; m < M; ++m) {
     const int st = G.cstride[m];
-    ncl[m - 1][0] = col - (((nbm >> (2 * m)) & 1) ? st : 0);
-    ncl[m - 1][1] = col + (((nbm >> (2 * m + 1)) & 1) ? st : 0);
+    ncl[m - 1][0] = hoff + col - (((nbm >> (2 * m)) & 1) ? st : 0);
+    ncl[m - 1][1] = hoff + col + (((nbm >> (2 * m + 1)) & 1) ? st : 0);
   }
+  const int own = hoff + col;
   auto level = [&](auto par_tag) -> bool {  // one level; true when the loop is over
     constexpr int PAR = decltype(par_tag)::value;
-    constexpr int HALF = (N0 / 2) * PY_CMAX;
+    constexpr int HALF = (N0 / 2) * PY_CS2;
+    const double cS = beta * (double)S;
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
-      const double cand = K[x0] + cur[x0];
+    for (int x0 = 0; x0 < PT; ++x0) {
+      const double cand = (T1[x0] + cS) + cur[x0];  // fl(K_l(S) + BM_S), K_l(S) = fl(T1 + fl(β·S))
       const bool lt = cand < best[x0];
       const bool eq = cand == best[x0];  // Inf == Inf ties only mark targets left at +Inf (never listed)
       best[x0] = vmin(cand, best[x0]);
@@ -589,13 +604,12 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     const double cN = beta * (double)(S + 1);
     bool more = false;
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
-      K[x0] = T1[x0] + cN;
-      more |= (K[x0] + Rmin) <= best[x0];
+    for (int x0 = 0; x0 < PT; ++x0) {
+      more |= ((T1[x0] + cN) + Rmin) <= best[x0];
     }
     if (colok) {
 #pragma unroll
-      for (int c = 0; c < N0 / 2; ++c) lv2[PAR * HALF + c * PY_CMAX + col] = make_double2(cur[2 * c], cur[2 * c + 1]);
+      for (int c = 0; c < PT / 2; ++c) lv2[PAR * HALF + c * PY_CS2 + own] = make_double2(cur[2 * c], cur[2 * c + 1]);
     }
     {
       const unsigned long long bal = __ballot(more);
@@ -606,30 +620,35 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     int go = 0;
 #pragma unroll
     for (int w = 0; w < PY_NW; ++w) go |= vote[PAR][w];
-    double2 nb[M - 1][2][N0 / 2];
+    double2 nb[M - 1][2][PT / 2];
 #pragma unroll
     for (int m = 0; m < M - 1; ++m)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int c = 0; c < N0 / 2; ++c) nb[m][s2][c] = lv2[PAR * HALF + c * PY_CMAX + ncl[m][s2]];
+        for (int c = 0; c < PT / 2; ++c) nb[m][s2][c] = lv2[PAR * HALF + c * PY_CS2 + ncl[m][s2]];
     // dilate by the unit cross: BM_{S+1}(x) = min(BM_S(x), BM_S(x ± e_m)); a missing neighbour
     // reads the own column (min with itself is a no-op), so there is no divergence.  The dilation
     // runs before the exit test so the neighbour reads are issued together with the vote reads.
-    double nw[N0];
+    double nw[PT];
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
+    for (int x0 = 0; x0 < PT; ++x0) {
       double v = cur[x0];
       if (x0 > 0) v = vmin(v, cur[x0 - 1]);
-      if (x0 + 1 < N0) v = vmin(v, cur[x0 + 1]);
+      if (x0 + 1 < PT) v = vmin(v, cur[x0 + 1]);
       nw[x0] = v;
+    }
+    {  // across the half-column boundary: the partner lane (lane ^ 1) holds the other half
+      const double r = py_swap_pair(h ? cur[0] : cur[PT - 1]);
+      nw[0] = vmin(nw[0], h ? r : INFINITY);
+      nw[PT - 1] = vmin(nw[PT - 1], h ? INFINITY : r);
     }
 #pragma unroll
     for (int m = 0; m < M - 1; ++m)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int c = 0; c < N0 / 2; ++c) {
+        for (int c = 0; c < PT / 2; ++c) {
           nw[2 * c] = vmin(nw[2 * c], nb[m][s2][c].x);
           nw[2 * c + 1] = vmin(nw[2 * c + 1], nb[m][s2][c].y);
         }
@@ -637,7 +656,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     {
       bool ch = false;
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) ch |= nw[x0] < cur[x0];
+      for (int x0 = 0; x0 < PT; ++x0) ch |= nw[x0] < cur[x0];
       const unsigned long long bc = __ballot(ch);
       if ((tid & 63) == 0) {
         atomicAdd(&dbg_lv[0], 1);
@@ -646,7 +665,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     }
 #endif
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) cur[x0] = nw[x0];
+    for (int x0 = 0; x0 < PT; ++x0) cur[x0] = nw[x0];
     ++S;
     return !go;
   };
@@ -666,17 +685,17 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   // other target with a finite minimum goes to the exact scan below. --------------------------------
   unsigned multi = 0;
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) multi |= (unsigned)((mm[x0] >> (tid & 63)) & 1ull) << x0;
-  int rk[N0];
+  for (int x0 = 0; x0 < PT; ++x0) multi |= (unsigned)((mm[x0] >> (tid & 63)) & 1ull) << x0;
+  int rk[PT];
   unsigned want = 0;
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) want |= (unsigned)((valid >> x0 & 1) && !(multi >> x0 & 1) && best[x0] < INFINITY) << x0;
+  for (int x0 = 0; x0 < PT; ++x0) want |= (unsigned)((valid >> x0 & 1) && !(multi >> x0 & 1) && best[x0] < INFINITY) << x0;
   {
-    PyKey key[N0];
-    uint4 bk[N0][2];
-    unsigned cc[N0][2];
+    PyKey key[PT];
+    uint4 bk[PT][2];
+    unsigned cc[PT][2];
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
+    for (int x0 = 0; x0 < PT; ++x0) {
       rk[x0] = -1;
       if (want >> x0 & 1) {
         key[x0] = py_key(py_bucket(bmb[x0], inv_w));
@@ -690,7 +709,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
     // a second one may be another source in the same bucket, and a double spill may hide more
     unsigned redo = 0;
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
+    for (int x0 = 0; x0 < PT; ++x0) {
       if (!(want >> x0 & 1)) continue;
       int nm = 0;
 #pragma unroll
@@ -706,31 +725,31 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
       redo |= (unsigned)(nm != 1 || (cc[x0][0] > 4 && cc[x0][1] > 4)) << x0;
     }
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0)  // confirm the single match (one batch of reads)
+    for (int x0 = 0; x0 < PT; ++x0)  // confirm the single match (one batch of reads)
       redo |= (unsigned)((want >> x0 & 1) && !(redo >> x0 & 1) && psiarr[rk[x0]] != bmb[x0]) << x0;
     // cold: find the holder of bmb among all entries of the key, and whether another source shares
     // its bucket -- one copy of the search code
 #pragma unroll 1
-    for (int x0 = 0; x0 < N0; ++x0) {
+    for (int x0 = 0; x0 < PT; ++x0) {
       if (!(redo >> x0 & 1)) continue;
       double v = bmb[0];
 #pragma unroll
-      for (int q = 1; q < N0; ++q) v = q == x0 ? bmb[q] : v;
+      for (int q = 1; q < PT; ++q) v = q == x0 ? bmb[q] : v;
       const double fqv = py_bucket(v, inv_w);
       const PyKey kv = py_key(fqv);
       int r = py_search(H, psiarr, coll, kv, 0.0, inv_w, v, -1, 1);
       if (r >= 0 && py_search(H, psiarr, coll, kv, fqv, inv_w, 0.0, r, 0) >= 0) coll[r] = 1;  // not unique
 #pragma unroll
-      for (int q = 0; q < N0; ++q) rk[q] = q == x0 ? r : rk[q];
+      for (int q = 0; q < PT; ++q) rk[q] = q == x0 ? r : rk[q];
     }
   }
   unsigned finb = 0;
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) finb |= (unsigned)(best[x0] < INFINITY) << x0;
+  for (int x0 = 0; x0 < PT; ++x0) finb |= (unsigned)(best[x0] < INFINITY) << x0;
   multi &= valid & finb;
   unsigned tolist = multi, lost = 0;
 #pragma unroll
-  for (int x0 = 0; x0 < N0; ++x0) {
+  for (int x0 = 0; x0 < PT; ++x0) {
     if ((want >> x0 & 1) && (rk[x0] < 0 || coll[rk[x0]])) tolist |= 1u << x0;
     if ((want >> x0 & 1) && rk[x0] < 0) lost |= 1u << x0;
   }
@@ -738,34 +757,30 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   if (novf > PY_OVF) tolist |= want;  // the overflow list itself overflowed: exact scans for this row
   if (tid == 0 && novf) atomicAdd(&counters[4], 1);
   PY_STAMP(10);
-  uint4 po[N0 / 4];  // sphere order of step i for the output row, fetched before the barrier
-  if (colok) {
-    const uint4 *p4 = reinterpret_cast<const uint4 *>(pout + N0 * col);
-#pragma unroll
-    for (int c = 0; c < N0 / 4; ++c) po[c] = p4[c];
-  }
+  uint32_t po[PT];  // sphere order of step i for the output row, fetched before the barrier
+  if (colok) py_load_u32<PT>(pout + pbase, po);
   __syncthreads();  // the level buffers are free: the list and the natural-order outputs live there
   int *list = reinterpret_cast<int *>(lvl);
   double *outnat = lvl + L;
   if (colok) {
-    double2 *o2 = reinterpret_cast<double2 *>(outnat + N0 * col);
+    double2 *o2 = reinterpret_cast<double2 *>(outnat + pbase);
 #pragma unroll
-    for (int c = 0; c < N0 / 2; ++c)
+    for (int c = 0; c < PT / 2; ++c)
       o2[c] = make_double2((valid >> (2 * c) & 1) ? best[2 * c] : INFINITY,
                            (valid >> (2 * c + 1) & 1) ? best[2 * c + 1] : INFINITY);
-    if (!tolist) {  // U row in natural order: one N0·2-byte store (cells with Φ = +Inf are unspecified)
-      uint32_t w[N0 / 2];
+    if (!tolist) {  // U in natural order: one PT·2-byte store (cells with Φ = +Inf are unspecified)
+      uint32_t w[PT / 2];
 #pragma unroll
-      for (int c = 0; c < N0 / 2; ++c)
+      for (int c = 0; c < PT / 2; ++c)
         w[c] = (uint32_t)(uint16_t)rk[2 * c] | ((uint32_t)(uint16_t)rk[2 * c + 1] << 16);
-      if constexpr (N0 == 8)
-        *reinterpret_cast<uint4 *>(UU + N0 * col) = make_uint4(w[0], w[1], w[2], w[3]);
+      if constexpr (PT == 4)
+        *reinterpret_cast<uint2 *>(UU + pbase) = make_uint2(w[0], w[1]);
       else
-        *reinterpret_cast<uint2 *>(UU + N0 * col) = make_uint2(w[0], w[1]);
+        *reinterpret_cast<uint32_t *>(UU + pbase) = w[0];
     } else {
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
-        const int g = x0 + N0 * col;
+      for (int x0 = 0; x0 < PT; ++x0) {
+        const int g = pbase + x0;
         if (tolist >> x0 & 1)
           list[atomicAdd(&nlist, 1)] = g;
         else if (rk[x0] >= 0)
@@ -778,18 +793,12 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
   PY_STAMP(11);
   // Φ_i row c' in the sphere order of u_old(i): gathered from LDS, written as one contiguous run
   if (colok) {
-    double o[N0];
+    double o[PT];
 #pragma unroll
-    for (int c = 0; c < N0 / 4; ++c) {
-      const uint4 t = po[c];
-      o[4 * c] = outnat[t.x & 0xFFFFu];
-      o[4 * c + 1] = outnat[t.y & 0xFFFFu];
-      o[4 * c + 2] = outnat[t.z & 0xFFFFu];
-      o[4 * c + 3] = outnat[t.w & 0xFFFFu];
-    }
-    double2 *s2 = reinterpret_cast<double2 *>(Sout + N0 * col);
+    for (int q = 0; q < PT; ++q) o[q] = outnat[po[q] & 0xFFFFu];
+    double2 *s2 = reinterpret_cast<double2 *>(Sout + pbase);
 #pragma unroll
-    for (int c = 0; c < N0 / 2; ++c) s2[c] = make_double2(o[2 * c], o[2 * c + 1]);
+    for (int c = 0; c < PT / 2; ++c) s2[c] = make_double2(o[2 * c], o[2 * c + 1]);
   }
   PY_STAMP(12);
   const int nl = nlist;
