@@ -134,8 +134,9 @@ int32_t mioc_last_algo(mioc_ctx *ctx);
 /*
  * Diagnostics of the last bellman/backtrack: counters[0] pyramid targets resolved by the exact scan because
  * their winning value has another source value within rounding distance, [1] pyramid targets resolved by
- * the exact scan because their minimum is reached at two levels, [2] p=Inf walk steps resolved by the
- * exact scan, [3] internal consistency failures (must be 0); [4..7] pyramid internals: rows whose
+ * the exact scan because their minimum is reached at two levels, [2] backtrack: p=Inf walk steps resolved
+ * by the exact scan, or for the U-table walks (generic, pyramid) the run-ahead rounds taken (each round
+ * settles up to 64 steps), [3] internal consistency failures (must be 0); [4..7] pyramid internals: rows whose
  * value hash overflowed, targets whose value was not found, values flagged as colliding, reserved.
  */
 int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n);

@@ -61,6 +61,9 @@ LevelsDev levels_dev(const mioc_ctx *ctx) {
   Lv.nuval = ctx->d_nuval;
   Lv.nuint = ctx->d_nuint;
   Lv.gidx = ctx->d_gidx;
+  Lv.vals = ctx->d_vals;
+  Lv.voff = ctx->d_voff;
+  Lv.g2r = ctx->d_g2r;
   Lv.p_kind = ctx->p_kind;
   Lv.p_int = (int)ctx->p_int;
   Lv.beta = ctx->beta;
@@ -82,18 +85,20 @@ ProblemDev problem_dev(const mioc_ctx *ctx) {
   return P;
 }
 
+void ev_collect(mioc_ctx *ctx);
+
 void free_all(mioc_ctx *ctx) {
   void *ptrs[] = {ctx->d_nuval, ctx->d_nuint,  ctx->d_gidx,      ctx->d_numin,       ctx->d_numax,
                   ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
-                  ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm};
+                  ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm,
+                  ctx->d_vals,  ctx->d_voff,    ctx->d_g2r};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (ctx->h_flags) hipHostFree(ctx->h_flags);
-  for (auto &pair : ctx->ev)
-    for (auto &e : pair)
-      if (e) hipEventDestroy(e);
+  ev_collect(ctx);
+  for (auto &pr : ctx->ev_pool) hipEventDestroy(pr.begin), hipEventDestroy(pr.end);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
 }
 
@@ -149,33 +154,44 @@ int build_cost_tables(mioc_ctx *ctx) {
   return MIOC_OK;
 }
 
+// Per-kernel timing (MIOC_OPT_TIMING): an event pair around each timed launch (or launch sequence),
+// folded into the totals at the next synchronising call.  Pairs are pooled, so every launch between two
+// collections is counted.
+void ev_collect(mioc_ctx *ctx) {
+  for (int w = 0; w < kStats; ++w) {
+    for (auto &pr : ctx->ev_pending[w]) {
+      hipEventSynchronize(pr.end);
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, pr.begin, pr.end) == hipSuccess) {
+        ctx->stat_ms[w] += ms;
+        ctx->stat_launches[w] += pr.launches;
+      }
+      ctx->ev_pool.push_back(pr);
+    }
+    ctx->ev_pending[w].clear();
+  }
+}
 void ev_begin(mioc_ctx *ctx, int which, const char *name) {
   if (!ctx->timing) return;
-  if (!ctx->ev[which][0]) {
-    hipEventCreate(&ctx->ev[which][0]);
-    hipEventCreate(&ctx->ev[which][1]);
+  if (ctx->ev_pending[which].size() >= 256) ev_collect(ctx);
+  mioc_ctx::EvPair pr;
+  if (!ctx->ev_pool.empty()) {
+    pr = ctx->ev_pool.back();
+    ctx->ev_pool.pop_back();
+  } else {
+    hipEventCreate(&pr.begin);
+    hipEventCreate(&pr.end);
   }
-  hipEventRecord(ctx->ev[which][0], ctx->stream);
+  hipEventRecord(pr.begin, ctx->stream);
+  ctx->ev_open[which] = pr;
   ctx->stat_name[which] = name;
 }
 void ev_end(mioc_ctx *ctx, int which, int64_t launches) {
   if (!ctx->timing) return;
-  hipEventRecord(ctx->ev[which][1], ctx->stream);
-  // fold the measurement in at the next synchronising call (no host sync here)
-  ctx->ev_pending[which] = true;
-  ctx->pending_launches[which] = launches;
-}
-void ev_collect(mioc_ctx *ctx) {
-  for (int w = 0; w < kStats; ++w) {
-    if (!ctx->ev_pending[w]) continue;
-    hipEventSynchronize(ctx->ev[w][1]);
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, ctx->ev[w][0], ctx->ev[w][1]) == hipSuccess) {
-      ctx->stat_ms[w] += ms;
-      ctx->stat_launches[w] += ctx->pending_launches[w];
-    }
-    ctx->ev_pending[w] = false;
-  }
+  mioc_ctx::EvPair pr = ctx->ev_open[which];
+  hipEventRecord(pr.end, ctx->stream);
+  pr.launches = launches;
+  ctx->ev_pending[which].push_back(pr);
 }
 
 // --------------------------------------------------------------------------------------------------
@@ -286,15 +302,18 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
     if (rc) return rc;
   }
   if (K > 4096) return fail(ctx, MIOC_EINVAL, "batch larger than 4096 subproblems");
-  int rc = grow(ctx, &ctx->d_ranks, &ctx->ranks_cap, K * nt * sizeof(int32_t), "rank path");
+  int rc = grow(ctx, &ctx->d_ranks, &ctx->ranks_cap, 2 * K * nt * sizeof(int32_t), "rank path");
   if (rc) return rc;
+  int32_t *d_urank = ctx->d_ranks + K * nt;
+  if (ctx->algo != MIOC_ALGO_PINF) HIP_TRY(ctx, launch_uold_rank(ctx->stream, P, Lv, d_urank));
+  HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags + 2, 0, 2 * sizeof(int32_t), ctx->stream));
   if (ctx->algo == MIOC_ALGO_PYRAMID) {
     const size_t s_stride = (size_t)(ctx->B + 1) * ctx->L;
     const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
     HIP_TRY(ctx, launch_stage_argmin0(ctx->stream, P, Lv, ctx->d_perm, ctx->d_stage, s_stride, (int)B_use, ctx->d_start));
     ev_begin(ctx, 1, "k_stage_walk");
     HIP_TRY(ctx, launch_stage_walk(ctx->stream, P, Lv, (const uint16_t *)ctx->d_U, uu_stride_k, ctx->d_start,
-                                   ctx->d_ranks));
+                                   d_urank, ctx->d_ranks, ctx->d_flags + 2));
     ev_end(ctx, 1, 1);
   } else if (ctx->algo == MIOC_ALGO_GENERIC) {
     const size_t front_stride = (size_t)ctx->L * ctx->RP;
@@ -302,11 +321,10 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
     HIP_TRY(ctx, launch_generic_argmin0(ctx->stream, P, Lv, ctx->d_front, front_stride, (int)B_use, ctx->d_start));
     ev_begin(ctx, 1, "k_generic_walk");
     HIP_TRY(ctx, launch_generic_walk(ctx->stream, P, Lv, ctx->d_U, ctx->ubytes, u_stride_k, ctx->d_start,
-                                     ctx->d_ranks));
+                                     d_urank, ctx->d_ranks, ctx->d_flags + 2));
     ev_end(ctx, 1, 1);
   } else {
     HIP_TRY(ctx, launch_pinf_start(ctx->stream, P, Lv, ctx->pinf, (int)B_use, ctx->d_start));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags + 2, 0, 2 * sizeof(int32_t), ctx->stream));
     ev_begin(ctx, 1, "k_pinf_walk");
     HIP_TRY(ctx, launch_pinf_walk(ctx->stream, P, Lv, ctx->pinf, ctx->d_start, ctx->d_ranks, ctx->d_flags + 2));
     ev_end(ctx, 1, 1);
@@ -447,16 +465,35 @@ int32_t mioc_set_levels(mioc_ctx *ctx, int64_t M, const int64_t *counts, const i
   }
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   size_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
-  void *olds[] = {ctx->d_nuval, ctx->d_nuint, ctx->d_gidx, ctx->d_numin, ctx->d_numax};
+  void *olds[] = {ctx->d_nuval, ctx->d_nuint, ctx->d_gidx, ctx->d_numin, ctx->d_numax,
+                  ctx->d_vals,  ctx->d_voff,  ctx->d_g2r};
   for (void *p : olds)
     if (p) hipFree(p);
   ctx->d_nuval = nullptr, ctx->d_nuint = nullptr, ctx->d_gidx = nullptr, ctx->d_numin = nullptr, ctx->d_numax = nullptr;
+  ctx->d_vals = nullptr, ctx->d_voff = nullptr, ctx->d_g2r = nullptr;
+  // grid tuple -> rank, for the backtrack's guess "the level equal to u_old" (only where it is small)
+  const bool want_g2r = Lgrid <= ((int64_t)1 << 22);
+  std::vector<int32_t> vals32(off[M]), voff32(M + 1), g2r;
+  for (int64_t q = 0; q < off[M]; ++q) vals32[q] = (int32_t)values[q];
+  for (int64_t m = 0; m <= M; ++m) voff32[m] = (int32_t)off[m];
+  if (want_g2r) {
+    g2r.assign(Lgrid, -1);
+    for (int64_t r = L - 1; r >= 0; --r) g2r[gidx[r]] = (int32_t)r;
+  }
+  size_t c5 = 0, c6 = 0, c7 = 0;
   int rc = grow(ctx, &ctx->d_nuval, &c0, L * M * sizeof(double), "levels");
   if (!rc) rc = grow(ctx, &ctx->d_nuint, &c1, L * M * sizeof(int32_t), "levels");
   if (!rc) rc = grow(ctx, &ctx->d_gidx, &c2, L * sizeof(int32_t), "levels");
   if (!rc) rc = grow(ctx, &ctx->d_numin, &c3, M * sizeof(double), "levels");
   if (!rc) rc = grow(ctx, &ctx->d_numax, &c4, M * sizeof(double), "levels");
+  if (!rc) rc = grow(ctx, &ctx->d_vals, &c5, off[M] * sizeof(int32_t), "levels");
+  if (!rc) rc = grow(ctx, &ctx->d_voff, &c6, (M + 1) * sizeof(int32_t), "levels");
+  if (!rc && want_g2r) rc = grow(ctx, &ctx->d_g2r, &c7, Lgrid * sizeof(int32_t), "levels");
   if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpy(ctx->d_vals, vals32.data(), off[M] * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIP_TRY(ctx, hipMemcpy(ctx->d_voff, voff32.data(), (M + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (want_g2r)
+    HIP_TRY(ctx, hipMemcpy(ctx->d_g2r, g2r.data(), Lgrid * sizeof(int32_t), hipMemcpyHostToDevice));
   HIP_TRY(ctx, hipMemcpy(ctx->d_nuval, ctx->nuval_h.data(), L * M * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(ctx, hipMemcpy(ctx->d_nuint, nuint.data(), L * M * sizeof(int32_t), hipMemcpyHostToDevice));
   HIP_TRY(ctx, hipMemcpy(ctx->d_gidx, gidx.data(), L * sizeof(int32_t), hipMemcpyHostToDevice));

@@ -351,38 +351,126 @@ hipError_t launch_generic_argmin0(hipStream_t s, const ProblemDev &P, const Leve
 
 // ---------------------------------------------------------------------------------------------
 // forward walk (HelpFunctions.jl:115-122): l <- U_i[c, l]; c <- c - ||ν(l_i) - u_old_i||_1.
-// One lane per subproblem: nt-1 dependent reads of the compact U table.
+//
+// Sequentially that is one dependent HBM read per step (nt-1 reads ≈ 0.8 µs each).  One wave per
+// subproblem runs the chain ahead instead: lanes t = 0..63 read the argmin cells of steps i..i+63
+// along two guessed paths at once,
+//   B: the level r of step i is kept (the budget drops by its distance to u_old at every step),
+//   A: from step i+1 on, the level equal to u_old (distance 0, the budget stays),
+// and a ballot finds the first step where the true path leaves the guess.  Lane 0's cell on path B is
+// the true cell of step i, and a cell is accepted only when every earlier accepted cell put the walk
+// into exactly the guessed state, so the result is the sequential walk's bit for bit.  A round costs
+// one read latency and advances up to 64 steps: A covers the stretches where the solution follows
+// u_old (the trust-region budget bounds the deviations), B the deviations themselves.
 // ---------------------------------------------------------------------------------------------
+__global__ void k_uold_rank(ProblemDev P, LevelsDev Lv, int32_t *urank) {
+  const int k = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.nt) return;
+  const double *uo = P.uold + ((size_t)k * P.nt + i) * P.M;
+  int g = 0, stride = 1;
+  bool ok = Lv.g2r != nullptr;
+  for (int m = 0; ok && m < P.M; ++m) {
+    const double v = uo[m];
+    const int q0 = Lv.voff[m], q1 = Lv.voff[m + 1];
+    int q = q0;
+    while (q < q1 && (double)Lv.vals[q] != v) ++q;
+    ok = q < q1;
+    g += (q - q0) * stride;
+    stride *= q1 - q0;
+  }
+  urank[(size_t)k * P.nt + i] = ok ? Lv.g2r[g] : -1;
+}
+
+hipError_t launch_uold_rank(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, int32_t *urank) {
+  dim3 grid((P.nt + 255) / 256, P.K);
+  hipLaunchKernelGGL(k_uold_rank, grid, dim3(256), 0, s, P, Lv, urank);
+  return hipGetLastError();
+}
+
+__device__ __forceinline__ int wave_incl_sum(int x, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  return x;
+}
+
+// first lane t in [1, n) whose guess failed, else n
+__device__ __forceinline__ int first_fail(bool ok, int lane, int n) {
+  const unsigned long long bad = __ballot(!ok && lane >= 1 && lane < n);
+  return bad ? __builtin_ffsll((long long)bad) - 1 : n;
+}
+
+// cell(s, c, b, r): the argmin rank stored for step s, budget c, level r (b = distance of r to u_old_s)
+template <class Cell>
+__device__ void spec_walk(const ProblemDev &P, const LevelsDev &Lv, int k, const Start &st, const int32_t *urk,
+                          int32_t *rk, int32_t *counters, Cell cell) {
+  const int lane = threadIdx.x & 63, M = P.M, nt = P.nt;
+  const double *uok = P.uold + (size_t)k * nt * M;
+  int i = 0, r = st.r, c = st.c, rounds = 0;
+  if (lane == 0) rk[0] = r;
+  while (i + 1 < nt) {
+    ++rounds;
+    const int n = min(64, nt - 1 - i);  // this round resolves the cells of steps i .. i+n-1
+    const int s = i + lane;
+    const bool act = lane < n;
+    const int bB = act ? bt_of(Lv.nuval + (size_t)r * M, uok + (size_t)s * M, M) : 0;
+    const int inc = wave_incl_sum(bB, lane);
+    const int cB = c - (inc - bB);  // budget at step s on path B
+    const int c1 = c - __shfl(bB, 0);
+    const int g = (urk && act) ? urk[s] : -1;
+    int vB = -1, vA = -1;
+    if (act && cB >= bB) vB = cell(s, cB, bB, r);
+    if (lane >= 1 && g >= 0 && c1 >= 0) vA = cell(s, c1, 0, g);
+    if (__shfl(vB, 0) < 0) {  // the true cell of step i is unreachable: inconsistent tables
+      if (lane == 0) atomicAdd(counters + 1, 1);
+      return;
+    }
+    const int vAx = lane == 0 ? vB : vA;  // path A's cells (lane 0: the true cell of step i)
+    const int fB = first_fail(__shfl_up(vB, 1) == r, lane, n);
+    const int fA = first_fail(g >= 0 && __shfl_up(vAx, 1) == g, lane, n);
+    const bool useA = fA > fB;
+    const int f = useA ? fA : fB;        // steps i+1 .. i+f are now known
+    const int v = useA ? vAx : vB;       // lane t < f: the level of step i+t+1
+    if (lane < f) rk[i + lane + 1] = v;
+    const int rn = __shfl(v, f - 1);
+    const int cn = useA ? c1 : __shfl(c - inc, f - 1);
+    if (rn < 0 || rn >= Lv.L || cn < 0) {
+      if (lane == 0) atomicAdd(counters + 1, 1);
+      return;
+    }
+    i += f;
+    r = rn;
+    c = cn;
+  }
+  if (lane == 0) atomicAdd(counters, rounds);
+}
+
 template <typename UT>
-__global__ void k_generic_walk(ProblemDev P, LevelsDev Lv, const UT *__restrict__ U, size_t u_stride_k,
-                               const Start *start, int32_t *ranks) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= P.K) return;
+__global__ __launch_bounds__(64) void k_generic_walk(ProblemDev P, LevelsDev Lv, const UT *__restrict__ U,
+                                                     size_t u_stride_k, const Start *start, const int32_t *urank,
+                                                     int32_t *ranks, int32_t *counters) {
+  const int k = blockIdx.x;
   const Start st = start[k];
-  int32_t *rk = ranks + (size_t)k * P.nt;
   if (st.status != MIOC_OK) return;
-  int r = st.r, c = st.c;
-  rk[0] = r;
   const UT *Uk = U + (size_t)k * u_stride_k;
   const size_t step = (size_t)Lv.L * (P.B + 1);
-  for (int i = 0; i + 1 < P.nt; ++i) {
-    const int s = (int)Uk[(size_t)i * step + (size_t)r * (P.B + 1) + c];
-    const double *uoi = P.uold + ((size_t)k * P.nt + i) * P.M;
-    c -= bt_of(Lv.nuval + (size_t)r * P.M, uoi, P.M);
-    r = s;
-    rk[i + 1] = r;
-  }
+  const int R = P.B + 1;
+  spec_walk(P, Lv, k, st, urank ? urank + (size_t)k * P.nt : nullptr, ranks + (size_t)k * P.nt, counters,
+            [&](int s, int c, int, int r) { return (int)Uk[(size_t)s * step + (size_t)r * R + c]; });
 }
 
 hipError_t launch_generic_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const void *U, int ubytes,
-                               size_t u_stride_k, const Start *start, int32_t *ranks) {
-  dim3 grid((P.K + 63) / 64);
+                               size_t u_stride_k, const Start *start, const int32_t *urank, int32_t *ranks,
+                               int32_t *counters) {
   if (ubytes == 1)
-    hipLaunchKernelGGL(k_generic_walk<uint8_t>, grid, dim3(64), 0, s, P, Lv, (const uint8_t *)U, u_stride_k,
-                       start, ranks);
+    hipLaunchKernelGGL(k_generic_walk<uint8_t>, dim3(P.K), dim3(64), 0, s, P, Lv, (const uint8_t *)U, u_stride_k,
+                       start, urank, ranks, counters);
   else
-    hipLaunchKernelGGL(k_generic_walk<uint16_t>, grid, dim3(64), 0, s, P, Lv, (const uint16_t *)U, u_stride_k,
-                       start, ranks);
+    hipLaunchKernelGGL(k_generic_walk<uint16_t>, dim3(P.K), dim3(64), 0, s, P, Lv, (const uint16_t *)U, u_stride_k,
+                       start, urank, ranks, counters);
   return hipGetLastError();
 }
 
@@ -461,30 +549,25 @@ hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const Levels
   return hipGetLastError();
 }
 
-__global__ void k_stage_walk(ProblemDev P, LevelsDev Lv, const uint16_t *__restrict__ UU, size_t uu_stride_k,
-                             const Start *start, int32_t *ranks) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= P.K) return;
+// the staging layout's argmin table: UU_i[c - b][r] (source row c - b̃, level rank r)
+__global__ __launch_bounds__(64) void k_stage_walk(ProblemDev P, LevelsDev Lv, const uint16_t *__restrict__ UU,
+                                                   size_t uu_stride_k, const Start *start, const int32_t *urank,
+                                                   int32_t *ranks, int32_t *counters) {
+  const int k = blockIdx.x;
   const Start st = start[k];
-  int32_t *rk = ranks + (size_t)k * P.nt;
   if (st.status != MIOC_OK) return;
-  int r = st.r, c = st.c;
-  rk[0] = r;
   const uint16_t *Uk = UU + (size_t)k * uu_stride_k;
   const size_t step = (size_t)(P.B + 1) * Lv.L;
-  for (int i = 0; i + 1 < P.nt; ++i) {
-    const double *uoi = P.uold + ((size_t)k * P.nt + i) * P.M;
-    const int b = bt_of(Lv.nuval + (size_t)r * P.M, uoi, P.M);
-    const int s = (int)Uk[(size_t)i * step + (size_t)(c - b) * Lv.L + r];
-    c -= b;
-    r = s;
-    rk[i + 1] = r;
-  }
+  const int L = Lv.L;
+  spec_walk(P, Lv, k, st, urank ? urank + (size_t)k * P.nt : nullptr, ranks + (size_t)k * P.nt, counters,
+            [&](int s, int c, int b, int r) { return (int)Uk[(size_t)s * step + (size_t)(c - b) * L + r]; });
 }
 
 hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,
-                             size_t uu_stride_k, const Start *start, int32_t *ranks) {
-  hipLaunchKernelGGL(k_stage_walk, dim3((P.K + 63) / 64), dim3(64), 0, s, P, Lv, UU, uu_stride_k, start, ranks);
+                             size_t uu_stride_k, const Start *start, const int32_t *urank, int32_t *ranks,
+                             int32_t *counters) {
+  hipLaunchKernelGGL(k_stage_walk, dim3(P.K), dim3(64), 0, s, P, Lv, UU, uu_stride_k, start, urank, ranks,
+                     counters);
   return hipGetLastError();
 }
 

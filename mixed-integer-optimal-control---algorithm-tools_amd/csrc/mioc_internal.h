@@ -22,6 +22,9 @@ struct LevelsDev {
   const double *nuval = nullptr;   // [L][M] level values per iterator rank
   const int32_t *nuint = nullptr;  // [L][M] same, as int32 (distance keys)
   const int32_t *gidx = nullptr;   // [L] grid linear index per rank (argmin tie-break)
+  const int32_t *vals = nullptr;   // [Σ counts] level values per dimension, concatenated
+  const int32_t *voff = nullptr;   // [M+1] offsets of each dimension's values in vals
+  const int32_t *g2r = nullptr;    // [Lgrid] rank of each grid tuple (-1: not admissible); null if too large
   int p_kind = MIOC_P_INF;
   int p_int = 1;
   double beta = 0.0;
@@ -69,8 +72,10 @@ hipError_t launch_generic_step(hipStream_t s, const ProblemDev &P, const LevelsD
                                size_t u_stride_k);
 hipError_t launch_generic_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const double *front0,
                                   size_t front_stride, int Bu, Start *start);
+hipError_t launch_uold_rank(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, int32_t *urank);
 hipError_t launch_generic_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const void *U, int ubytes,
-                               size_t u_stride_k, const Start *start, int32_t *ranks);
+                               size_t u_stride_k, const Start *start, const int32_t *urank, int32_t *ranks,
+                               int32_t *counters);
 hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const Start *start,
                          const int32_t *ranks, double *u_out, double *phi_star, int32_t *status);
 
@@ -85,7 +90,8 @@ size_t pyr_lds_bytes(const PyrGeom &G);
 hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
                                 const double *S0, size_t s_stride, int Bu, Start *start);
 hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,
-                             size_t uu_stride_k, const Start *start, int32_t *ranks);
+                             size_t uu_stride_k, const Start *start, const int32_t *urank, int32_t *ranks,
+                             int32_t *counters);
 
 // ---- p = Inf collapse (mioc_pinf.hip) -----------------------------------------------------------
 struct PinfDev {
@@ -124,6 +130,7 @@ struct mioc_ctx {
   double *d_nuval = nullptr;
   int32_t *d_nuint = nullptr;
   int32_t *d_gidx = nullptr;
+  int32_t *d_vals = nullptr, *d_voff = nullptr, *d_g2r = nullptr;
   double *d_numin = nullptr, *d_numax = nullptr;
 
   // cost
@@ -168,7 +175,7 @@ struct mioc_ctx {
 
   // backtrack scratch
   mioc::Start *d_start = nullptr;
-  int32_t *d_ranks = nullptr;
+  int32_t *d_ranks = nullptr;      // [K][nt] level ranks of the path, then [K][nt] ranks of u_old
   size_t ranks_cap = 0;
   int32_t *d_flags = nullptr;      // [4] validation flags / counters
   int32_t *h_flags = nullptr;      // pinned mirror
@@ -178,10 +185,13 @@ struct mioc_ctx {
   size_t uout_cap = 0;
 
   // timing
-  hipEvent_t ev[4][2] = {};
+  struct EvPair {
+    hipEvent_t begin = nullptr, end = nullptr;
+    int64_t launches = 0;
+  };
+  std::vector<EvPair> ev_pool, ev_pending[4];
+  EvPair ev_open[4];
   double stat_ms[4] = {};
   int64_t stat_launches[4] = {};
-  bool ev_pending[4] = {};
-  int64_t pending_launches[4] = {};
   const char *stat_name[4] = {"", "", "", ""};
 };

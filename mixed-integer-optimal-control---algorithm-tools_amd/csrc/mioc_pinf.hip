@@ -143,6 +143,15 @@ __device__ __forceinline__ double pvmin(double a, double b) {
 // per step waits only on LDS (lgkmcnt), so the streamed R_i stores and the next chunk's DMA stay in
 // flight.  Four independent min accumulators per output keep the dependency chain short.
 // ---------------------------------------------------------------------------------------------
+#ifdef MIOC_STAMPS
+// diagnostic build: per-wave phase cycles of workgroup 0 (s_memtime): [0] window + class reads waited,
+// [1] min-plus VALU + stores, [2] barrier, [3] steps, [4] total
+__device__ unsigned long long g_pinf_stamps[16][8];
+#define PI_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define PI_T(v)
+#endif
+
 template <int BWP>
 __global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int CH) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -174,6 +183,7 @@ __global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int
       glds_copy(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8, tid,
                 nthr);
     for (int i = hi; i >= lo; --i) {
+      PI_T(t0);
       for (int c0 = 2 * tid; c0 < RP; c0 += 2 * nthr) {
         const double2 *win = reinterpret_cast<const double2 *>(A + (size_t)((i + 1) & 1) * AW + c0);
         const double2 *kr = reinterpret_cast<const double2 *>(Kc + (size_t)(i - lo) * BWP);
@@ -190,6 +200,11 @@ __global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int
           kv[2 * p2] = y.x;
           kv[2 * p2 + 1] = y.y;
         }
+#ifdef MIOC_STAMPS
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PI_T(t1);
+        if (blockIdx.x == 0 && (tid & 63) == 0 && c0 == 2 * tid) g_pinf_stamps[tid >> 6][0] += t1 - t0;
+#endif
         // row 2t:   R_{i+1}[2t - b]   = w[BWP - 1 - b];   row 2t+1: R_{i+1}[2t + 1 - b] = w[BWP - b]
         double m0[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, m1[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
 #pragma unroll
@@ -205,7 +220,18 @@ __global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int
         R[(size_t)i * RP + c0] = c0 <= B ? r0 : INFINITY;
         R[(size_t)i * RP + c0 + 1] = c0 + 1 <= B ? r1 : INFINITY;
       }
+      PI_T(t2);
       lds_barrier();
+#ifdef MIOC_STAMPS
+      PI_T(t3);
+      if (blockIdx.x == 0 && (tid & 63) == 0) {
+        unsigned long long *g = g_pinf_stamps[tid >> 6];
+        g[1] += t2 - t0;  // minus slot 0 afterwards
+        g[2] += t3 - t2;
+        g[3] += 1;
+        g[4] += t3 - t0;
+      }
+#endif
     }
     vm_drain();
     lds_barrier();
@@ -321,13 +347,15 @@ hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev
 }
 
 // ---------------------------------------------------------------------------------------------
-// forward walk, one wave per subproblem.  State at step i: (c, l, K_l(i), b̃_l(i), Φ_i[c, l]).
+// forward walk, one workgroup per subproblem: wave 0 walks, all four waves stage.  State at step i:
+// (c, l, K_l(i), b̃_l(i), Φ_i[c, l]).
 // Lane b examines budget class b of step j = i+1: the levels of the class with K == Kmin give
 // Φ_j[c', ·] = V_b = fl(Kmin + R_{j+1}[c' - b]) and the first of them is kfirst; a level with a
 // larger K gives at least fl(K2 + R_{j+1}[c' - b]).  If that second value could still satisfy
 // fl(K_l + ·) == Φ_i[c, l], the step is resolved by an exact scan over all levels instead.
 // Class rows and R rows for CH steps are staged into LDS by LDS-DMA one chunk ahead, and the winner
-// is selected with a ballot + readlane (scalar), so a step costs two LDS reads and a few VALU ops.
+// is selected with a ballot + readlane (scalar).  Only the window read R_{j+1}[c' - b] depends on the
+// walk; the three class-row reads of a step are independent of it and issue beside it.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ double readlane_f64(double x, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
@@ -335,14 +363,16 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
   return __hiloint2double(hi, lo);
 }
 
-__global__ __launch_bounds__(64) void k_pinf_walk(ProblemDev P, LevelsDev Lv, PinfDev D, const Start *start,
-                                                  int32_t *ranks, int32_t *nfallback, int CH) {
+__global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, PinfDev D, const Start *start,
+                                                   int32_t *ranks, int32_t *nfallback, int CH) {
   extern __shared__ __attribute__((aligned(16))) double wsm[];
-  const int k = blockIdx.x, lane = threadIdx.x, M = P.M, nt = P.nt, RP = P.RP, BWP = D.BWP;
+  const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, nthr = blockDim.x;
+  const int M = P.M, nt = P.nt, RP = P.RP, BWP = D.BWP;
+  const bool walker = tid < 64;  // wave 0 walks; every wave stages
   const Start st = start[k];
   if (st.status != MIOC_OK) return;
   int32_t *rk = ranks + (size_t)k * nt;
-  if (lane == 0) rk[0] = st.r;
+  if (tid == 0) rk[0] = st.r;
   if (nt == 1) return;
   // LDS: Rb[2][CH][RP], Km[2][CH][BWP], K2[2][CH][BWP] (doubles), Kf[2][CH][BWP] (int32)
   double *Rb = wsm;
@@ -360,13 +390,13 @@ __global__ __launch_bounds__(64) void k_pinf_walk(ProblemDev P, LevelsDev Lv, Pi
     const int i0 = q * CH;
     const int ni = (i0 + CH <= nsteps ? CH : nsteps - i0);
     // class rows j = i0+1 .. i0+ni
-    glds_copy(D.kmin + crow0 + (size_t)(i0 + 1) * BWP, Km + (size_t)buf * CH * BWP, ni * BWP * 8, lane, 64);
-    glds_copy(D.k2 + crow0 + (size_t)(i0 + 1) * BWP, K2 + (size_t)buf * CH * BWP, ni * BWP * 8, lane, 64);
-    glds_copy(D.kfirst + crow0 + (size_t)(i0 + 1) * BWP, Kf + (size_t)buf * CH * BWP, ni * BWP * 4, lane, 64);
+    glds_copy(D.kmin + crow0 + (size_t)(i0 + 1) * BWP, Km + (size_t)buf * CH * BWP, ni * BWP * 8, tid, nthr);
+    glds_copy(D.k2 + crow0 + (size_t)(i0 + 1) * BWP, K2 + (size_t)buf * CH * BWP, ni * BWP * 8, tid, nthr);
+    glds_copy(D.kfirst + crow0 + (size_t)(i0 + 1) * BWP, Kf + (size_t)buf * CH * BWP, ni * BWP * 4, tid, nthr);
     // R rows j+1 = i0+2 .. i0+ni+1 (row nt does not exist: the terminal step needs none)
     int nr = ni;
     if (i0 + 1 + nr > nt - 1) nr = nt - 1 - (i0 + 1);
-    if (nr > 0) glds_copy(R + (size_t)(i0 + 2) * RP, Rb + (size_t)buf * CH * RP, nr * RP * 8, lane, 64);
+    if (nr > 0) glds_copy(R + (size_t)(i0 + 2) * RP, Rb + (size_t)buf * CH * RP, nr * RP * 8, tid, nthr);
   };
 
   int r = st.r, c = st.c, br;
@@ -377,42 +407,45 @@ __global__ __launch_bounds__(64) void k_pinf_walk(ProblemDev P, LevelsDev Lv, Pi
     br = p_bt(nuv, uok, M);
   }
   int fallbacks = 0;
+  bool dead = false;
   stage(0, 0);
   vm_drain();
   lds_barrier();
   const int nq = (nsteps + CH - 1) / CH;
   for (int q = 0; q < nq; ++q) {
     const int buf = q & 1;
+    PI_T(w0);
     if (q + 1 < nq) stage(q + 1, buf ^ 1);
     const int i0 = q * CH, i1 = (i0 + CH <= nsteps ? i0 + CH : nsteps);
     const double *KmB = Km + (size_t)buf * CH * BWP;
     const double *K2B = K2 + (size_t)buf * CH * BWP;
     const int32_t *KfB = Kf + (size_t)buf * CH * BWP;
     const double *RbB = Rb + (size_t)buf * CH * RP;
-    for (int i = i0; i < i1; ++i) {
+    const bool inb = lane < BWP;
+    for (int i = i0; walker && !dead && i < i1; ++i) {
       const int row = i - i0, j = i + 1, cp = c - br;
       const bool term = (j == nt - 1);
-      const bool inb = lane < BWP;
-      const double km = inb ? KmB[row * BWP + lane] : INFINITY;
-      double x = INFINITY;
-      if (term)
-        x = (lane == cp) ? 0.0 : INFINITY;
-      else if (inb && lane <= cp)
-        x = RbB[(size_t)row * RP + cp - lane];
+      // Branch-free: every lane reads an in-bounds slot and masks afterwards.  The class row does not
+      // depend on the walk, so its three reads issue beside the window read.
+      const int lb = lane & (BWP - 1), xi = cp - lane;
+      const double kmr = KmB[row * BWP + lb];
+      const double k2r = K2B[row * BWP + lb];
+      const int kfr = KfB[row * BWP + lb];
+      const double xr = RbB[(size_t)row * RP + (xi > 0 ? xi : 0)];
+      const double km = inb ? kmr : INFINITY;
+      const double k2 = inb ? k2r : INFINITY;
+      const int kf = inb ? kfr : INT_MAX;
+      const double x = term ? (lane == cp ? 0.0 : INFINITY) : (inb && xi >= 0 ? xr : INFINITY);
       const bool ok = km < INFINITY && x < INFINITY;
       const double V = term ? km : km + x;
+      const double V2 = term ? k2 : k2 + x;
       const bool match = ok && (Kr + V == target);
+      const bool amb = match && k2 < INFINITY && (Kr + V2 == target);
       const unsigned long long mm = __ballot(match);
-      bool amb = false;
-      if (match) {
-        const double k2 = K2B[row * BWP + lane];
-        amb = k2 < INFINITY && (Kr + (term ? k2 : k2 + x) == target);
-      }
       const unsigned long long am = __ballot(amb);
       int win, winb;
       double winV, winK;
       if (mm != 0 && am == 0) {
-        const int kf = inb ? KfB[row * BWP + lane] : INT_MAX;
         winb = __builtin_ffsll((long long)mm) - 1;
         win = __builtin_amdgcn_readlane(kf, winb);
         for (unsigned long long rest = mm & (mm - 1); rest; rest &= rest - 1) {
@@ -455,7 +488,8 @@ __global__ __launch_bounds__(64) void k_pinf_walk(ProblemDev P, LevelsDev Lv, Pi
         const unsigned long long bal = __ballot(sbest == m2 && m2 != INT_MAX);
         if (bal == 0) {  // inconsistent tables: cannot happen for a consistent DP
           if (lane == 0) atomicAdd(nfallback + 1, 1);
-          return;
+          dead = true;  // stop walking, but keep joining the staging barriers
+          break;
         }
         const int src = __builtin_ffsll((long long)bal) - 1;
         win = m2;
@@ -470,11 +504,21 @@ __global__ __launch_bounds__(64) void k_pinf_walk(ProblemDev P, LevelsDev Lv, Pi
       Kr = winK;
       br = winb;
     }
+    PI_T(w1);
     vm_drain();
     lds_barrier();
+#ifdef MIOC_STAMPS
+    PI_T(w2);
+    if (blockIdx.x == 0 && tid == 0) {  // walker: [8][0] staging issue + steps, [8][1] chunk-end wait
+      g_pinf_stamps[8][0] += w1 - w0;
+      g_pinf_stamps[8][1] += w2 - w1;
+      g_pinf_stamps[8][2] += 1;
+      g_pinf_stamps[8][3] += i1 - i0;
+    }
+#endif
   }
   (void)r;
-  if (lane == 0 && fallbacks) atomicAdd(nfallback, fallbacks);
+  if (tid == 0 && fallbacks) atomicAdd(nfallback, fallbacks);
 }
 
 int pinf_chunk_walk(int RP, int BWP) {
@@ -488,8 +532,14 @@ hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev 
   if (D.BWP > 64) return hipErrorInvalidValue;
   const int CH = pinf_chunk_walk(P.RP, D.BWP);
   size_t lds = (size_t)2 * CH * ((size_t)P.RP * 8 + (size_t)D.BWP * 20);
-  hipLaunchKernelGGL(k_pinf_walk, dim3(P.K), dim3(64), lds, s, P, Lv, D, start, ranks, nfallback, CH);
+  hipLaunchKernelGGL(k_pinf_walk, dim3(P.K), dim3(256), lds, s, P, Lv, D, start, ranks, nfallback, CH);
   return hipGetLastError();
 }
+
+#ifdef MIOC_STAMPS
+extern "C" int32_t mioc_debug_pinf_stamps(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pinf_stamps), sizeof(g_pinf_stamps)) == hipSuccess ? 0 : -4;
+}
+#endif
 
 }  // namespace mioc

@@ -263,7 +263,8 @@ class Context:
         return out.T
 
     def diagnostics(self):
-        """[value-collision targets scanned, multi-level targets scanned, p=Inf walk fallbacks, errors,
+        """[value-collision targets scanned, multi-level targets scanned, p=Inf walk fallbacks or U-table walk
+        run-ahead rounds, errors,
         hash-overflow rows, targets whose value was not found, values flagged colliding, reserved]."""
         out = np.zeros(8, dtype=np.int64)
         self._check(self.lib.mioc_diagnostics(self.h, _p(out), 8))

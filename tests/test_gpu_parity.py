@@ -397,6 +397,46 @@ def test_pyramid_vs_oracle_512_levels(oracle_c, mode):
     ctx.close()
 
 
+@pytest.mark.parametrize("pk", [P_ONE, P_INF])
+@pytest.mark.parametrize("uo_mode", ["piecewise", "random", "outside"])
+def test_run_ahead_walk_vs_oracle(oracle_c, uo_mode, pk):
+    """Backtrack chains several 64-step rounds long, on and off the walk's two guesses (keep the level;
+    follow u_old): u_old piecewise constant, a new random level every step, and partly outside the
+    level grid (integral but not admissible, so there is no u_old level to follow)."""
+    rng = np.random.default_rng({"piecewise": 11, "random": 12, "outside": 13}[uo_mode] + 10 * (pk == P_INF))
+    lv = Levels.product([list(range(4))] * 3)
+    lt = LevelTable(lv.nu, [tuple(t) for t in lv.tuples])
+    n, B, beta, dt = 333, 24, 1e-3, 2.0 ** -6
+    df = rng.standard_normal((3, n))
+    if uo_mode == "piecewise":
+        idx = np.repeat(rng.integers(lv.L, size=n // 10 + 1), 10)[:n]
+    else:
+        idx = rng.integers(lv.L, size=n)
+    uo = np.array([lv.nuval[j] for j in idx], dtype=np.float64).T.copy()
+    if uo_mode == "outside":
+        for i in rng.choice(n, size=12, replace=False):
+            uo[rng.integers(3), i] = float(rng.choice([-1, 4]))
+    phi, U = oracle_c.bellman(lv, df, uo, B, pk, beta, dt)
+    for algo in _algos(pk, lt):
+        ctx = _ctx(lt, pk, beta, algo)
+        ctx.bellman(df, uo, B, dt)
+        for Bp in (B, B // 3, 0):
+            try:
+                ou, ops = oracle_c.backtrack(lv, uo, phi, U, B, Bp)
+            except Exception:
+                with pytest.raises(native.MiocNativeError):
+                    ctx.backtrack(Bp)
+                continue
+            u, ps, _ = ctx.backtrack(Bp)
+            d = ctx.diagnostics()
+            assert np.array_equal(u, ou), f"{uo_mode} algo={algo} Bp={Bp} diag={d}"
+            assert ps == ops
+            assert d[3] == 0
+            if algo != native.MIOC_ALGO_PINF:
+                assert math.ceil((n - 1) / 64) <= d[2] <= n - 1, d
+        ctx.close()
+
+
 def test_pyramid_equals_generic_at_c4_scale():
     """4096 levels, B=256, p=1: the pyramid and the generic sweep are independent algorithms."""
     cfg = CONFIGS["C4"]
