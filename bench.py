@@ -139,7 +139,7 @@ def run(args, rank, world, device, dist, torch):
     algo = ctx.last_algo()
     res = dict(elapsed=elapsed, K=K, nt=nt, B=B, p=p, algo=algo, dom_ms=dom_ms, dom_n=dom_n, dom_name=dom_name,
                walk_ms=walk_ms, walk_n=walk_n, walk_name=walk_name, levels=levels, uo=uos[-1],
-               phi=d_phi.cpu().numpy().tolist())
+               phi=d_phi.cpu().numpy().tolist(), diag=ctx.diagnostics())
     ctx.close()
     return res
 
@@ -177,6 +177,17 @@ def roofline_of(res, args):
         roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
                      "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
                      "candidates_per_launch": ncand}
+    elif res["dom_name"] == "k_sdt_step":
+        # the same algorithmic traffic as the reference DP step: front in + front out + compact U
+        bytes_per_launch = K * (B + 1) * L * (8 + 8 + 2)
+        M = lv.M
+        # per pass and 8-point line: 20 merges (7 forward, 6 backward, 7 combine), each add + min + sub + cmp
+        ops = 1.0 * K * (B + 1) * L * M * (20 / 8) * 4
+        ncand = K * candidates_per_step(lv, res["uo"], B)
+        roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
+                     "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
+                     "note": "separable transform FP64 ops (4 per merge); brute-force-equivalent candidates/s "
+                             f"= {ncand / avg_s:.4g}"}
     elif res["dom_name"] == "k_pyr_step":
         # the same algorithmic traffic as the reference DP step: front in + front out + compact U
         bytes_per_launch = K * (B + 1) * L * (8 + 8 + 2)
@@ -272,6 +283,9 @@ def main():
             "roofline": roof,
             "roofline_valu": valu,
             "backtrack_ms": round(res["walk_ms"] / max(1, args.steps), 3),
+            "exact_scan_targets": {"near_tie": res["diag"][0], "direct_rows": res["diag"][1],
+                                   "of_cells": res["K"] * (res["nt"] - 1) * (res["B"] + 1) * res["levels"].L,
+                                   "note": "last bellman call (mioc_diagnostics[0..1])"},
         }
         if variant:
             out["variant_p_inf"] = variant
@@ -283,8 +297,8 @@ def main():
 
 
 def native_name(algo):
-    return {1: "generic min-plus sweep", 2: "p=Inf exact collapse", 3: "p=1 exact L1-ball pyramid"}.get(algo,
-                                                                                                  str(algo))
+    return {1: "generic min-plus sweep", 2: "p=Inf exact collapse", 3: "p=1 exact L1-ball pyramid",
+            4: "p=1 separable L1 transform, certified argmin"}.get(algo, str(algo))
 
 
 if __name__ == "__main__":

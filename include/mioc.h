@@ -48,11 +48,14 @@ extern "C" {
 
 /* ---- algorithm selection (mioc_set_option(MIOC_OPT_ALGO, ...)) ----------------------------- */
 #define MIOC_OPT_ALGO 1
-#define MIOC_ALGO_AUTO 0    /* p=Inf -> class collapse; p=1 on a large product grid -> pyramid;
+#define MIOC_ALGO_AUTO 0    /* p=Inf -> class collapse; p=1, beta>0 on an 8^3 or 8^4 product grid ->
+                               separable transform; other large product grids at p=1 -> pyramid;
                                otherwise the generic min-plus sweep */
 #define MIOC_ALGO_GENERIC 1 /* per-step min-plus sweep over every (c, l, j): any p */
 #define MIOC_ALGO_PINF 2    /* exact p=Inf collapse onto per-budget row minima */
 #define MIOC_ALGO_PYRAMID 3 /* p=1 on product grids of consecutive levels: exact L1-ball pyramid */
+#define MIOC_ALGO_SEPARABLE 4 /* p=1, beta>0, 8^3 / 8^4 product grid of consecutive levels: separable L1
+                                 distance transform in exact fixed point with a certified argmin */
 #define MIOC_OPT_TIMING 2   /* 1: record HIP events around the dominant kernel (mioc_kernel_stats) */
 
 typedef struct mioc_ctx mioc_ctx;
@@ -132,9 +135,10 @@ int32_t mioc_reset_stats(mioc_ctx *ctx);
 int32_t mioc_last_algo(mioc_ctx *ctx);
 
 /*
- * Diagnostics of the last bellman/backtrack: counters[0] pyramid targets resolved by the exact scan because
- * their winning value has another source value within rounding distance, [1] pyramid targets resolved by
- * the exact scan because their minimum is reached at two levels, [2] backtrack: p=Inf walk steps resolved
+ * Diagnostics of the last bellman/backtrack: counters[0] pyramid / separable-transform targets resolved by
+ * the exact scan because their winning value has another source value within rounding distance, [1] pyramid
+ * targets resolved by the exact scan because their minimum is reached at two levels (separable transform:
+ * targets of rows sent straight to the exact scan: few targets, or a value scale outside its binade), [2] backtrack: p=Inf walk steps resolved
  * by the exact scan, or for the U-table walks (generic, pyramid) the run-ahead rounds taken (each round
  * settles up to 64 steps), [3] internal consistency failures (must be 0); [4..7] pyramid internals: rows whose
  * value hash overflowed, targets whose value was not found, values flagged as colliding, reserved.

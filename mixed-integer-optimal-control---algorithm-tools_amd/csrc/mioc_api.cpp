@@ -216,13 +216,20 @@ int run_bellman(mioc_ctx *ctx) {
   const bool pinf_ok = ctx->p_kind == MIOC_P_INF && bmax + 1 <= 64 && ctx->RP <= 7936;
   // the L1-ball identity min_j fl(K(d(l,j)) + Ψ_j) = min_S fl(K(S) + BM_S(l)) needs K non-decreasing in S
   const bool pyr_ok = ctx->p_kind == MIOC_P_ONE && ctx->pyr_ok && ctx->beta >= 0.0;
+  // the separable transform works in units of beta (exact unit steps): beta > 0, 8^3 / 8^4 grids
+  const bool sdt_ok = pyr_ok && ctx->beta > 0.0 && sdt_supported(ctx->pyr);
   if (algo == MIOC_ALGO_AUTO)
-    algo = pinf_ok ? MIOC_ALGO_PINF : (pyr_ok && ctx->L >= 256 ? MIOC_ALGO_PYRAMID : MIOC_ALGO_GENERIC);
+    algo = pinf_ok  ? MIOC_ALGO_PINF
+           : sdt_ok ? MIOC_ALGO_SEPARABLE
+                    : (pyr_ok && ctx->L >= 256 ? MIOC_ALGO_PYRAMID : MIOC_ALGO_GENERIC);
   if (algo == MIOC_ALGO_PINF && !pinf_ok)
     return fail(ctx, MIOC_EINVAL, "p=Inf collapse needs p_kind MIOC_P_INF, <= 64 budget classes and B < 7936");
   if (algo == MIOC_ALGO_PYRAMID && !pyr_ok)
     return fail(ctx, MIOC_EINVAL, "the L1-ball pyramid needs p = 1, beta >= 0 and a product grid of consecutive "
                                   "integer levels (first dimension 4 or 8 levels, <= 4096 tuples)");
+  if (algo == MIOC_ALGO_SEPARABLE && !sdt_ok)
+    return fail(ctx, MIOC_EINVAL, "the separable L1 transform needs p = 1, beta > 0 and an 8^3 or 8^4 product grid "
+                                  "of consecutive integer levels");
   if (!ctx->d_counters) {
     size_t cc = 0;
     int rc0 = grow(ctx, &ctx->d_counters, &cc, 8 * sizeof(int32_t), "counters");
@@ -232,7 +239,7 @@ int run_bellman(mioc_ctx *ctx) {
   ctx->algo = algo;
   const size_t K = (size_t)ctx->K, nt = (size_t)ctx->nt, L = (size_t)ctx->L, RP = (size_t)ctx->RP;
 
-  if (algo == MIOC_ALGO_PYRAMID) {
+  if (algo == MIOC_ALGO_PYRAMID || algo == MIOC_ALGO_SEPARABLE) {
     const size_t s_stride = (size_t)(ctx->B + 1) * L;
     int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, 2 * K * s_stride * sizeof(double), "staging fronts");
     if (rc) return rc;
@@ -244,10 +251,17 @@ int run_bellman(mioc_ctx *ctx) {
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
     HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm));
     HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, st[(nt - 1) & 1], s_stride));
-    ev_begin(ctx, 0, "k_pyr_step");
-    for (int i = ctx->nt - 2; i >= 0; --i)
-      HIP_TRY(ctx, launch_pyr_step(ctx->stream, P, Lv, ctx->pyr, i, ctx->d_perm, st[(i + 1) & 1], st[i & 1],
-                                   (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters));
+    if (algo == MIOC_ALGO_SEPARABLE) {
+      ev_begin(ctx, 0, "k_sdt_step");
+      for (int i = ctx->nt - 2; i >= 0; --i)
+        HIP_TRY(ctx, launch_sdt_step(ctx->stream, P, Lv, ctx->pyr, i, ctx->d_perm, st[(i + 1) & 1], st[i & 1],
+                                     (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters));
+    } else {
+      ev_begin(ctx, 0, "k_pyr_step");
+      for (int i = ctx->nt - 2; i >= 0; --i)
+        HIP_TRY(ctx, launch_pyr_step(ctx->stream, P, Lv, ctx->pyr, i, ctx->d_perm, st[(i + 1) & 1], st[i & 1],
+                                     (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters));
+    }
     ev_end(ctx, 0, ctx->nt - 1);
   } else if (algo == MIOC_ALGO_GENERIC) {
     ctx->ubytes = L <= 256 ? 1 : 2;
@@ -307,7 +321,7 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
   int32_t *d_urank = ctx->d_ranks + K * nt;
   if (ctx->algo != MIOC_ALGO_PINF) HIP_TRY(ctx, launch_uold_rank(ctx->stream, P, Lv, d_urank));
   HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags + 2, 0, 2 * sizeof(int32_t), ctx->stream));
-  if (ctx->algo == MIOC_ALGO_PYRAMID) {
+  if (ctx->algo == MIOC_ALGO_PYRAMID || ctx->algo == MIOC_ALGO_SEPARABLE) {
     const size_t s_stride = (size_t)(ctx->B + 1) * ctx->L;
     const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
     HIP_TRY(ctx, launch_stage_argmin0(ctx->stream, P, Lv, ctx->d_perm, ctx->d_stage, s_stride, (int)B_use, ctx->d_start));
@@ -406,7 +420,7 @@ const char *mioc_last_error(const mioc_ctx *ctx) { return ctx ? ctx->err.c_str()
 int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   if (!ctx) return MIOC_EINVAL;
   if (option == MIOC_OPT_ALGO) {
-    if (value < MIOC_ALGO_AUTO || value > MIOC_ALGO_PYRAMID) return fail(ctx, MIOC_EINVAL, "unknown algorithm");
+    if (value < MIOC_ALGO_AUTO || value > MIOC_ALGO_SEPARABLE) return fail(ctx, MIOC_EINVAL, "unknown algorithm");
     ctx->opt_algo = value;
     return MIOC_OK;
   }
@@ -667,7 +681,7 @@ int32_t mioc_get_argmin_table(mioc_ctx *ctx, int64_t k, int64_t step, int32_t *U
   if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "no bellman result to read");
   if (k < 0 || k >= ctx->K || step < 0 || step + 1 >= ctx->nt)
     return fail(ctx, MIOC_EINVAL, "subproblem or step out of range (0 <= step < nt-1)");
-  if (ctx->algo != MIOC_ALGO_GENERIC && ctx->algo != MIOC_ALGO_PYRAMID)
+  if (ctx->algo == MIOC_ALGO_PINF)
     return fail(ctx, MIOC_EINVAL, "the p=Inf collapse keeps per-budget class tables, not U");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -682,7 +696,7 @@ int32_t mioc_get_argmin_table(mioc_ctx *ctx, int64_t k, int64_t step, int32_t *U
     return b;
   };
   const size_t step_cells = (size_t)R * L;
-  if (ctx->algo == MIOC_ALGO_PYRAMID) {  // staged: UU_i[c'][l] = U_i[l, c' + b̃_l(i)]
+  if (ctx->algo == MIOC_ALGO_PYRAMID || ctx->algo == MIOC_ALGO_SEPARABLE) {  // staged: UU_i[c'][l] = U_i[l, c' + b̃_l(i)]
     std::vector<uint16_t> uu(step_cells);
     const uint16_t *src = (const uint16_t *)ctx->d_U + ((size_t)k * (nt - 1) + step) * step_cells;
     HIP_TRY(ctx, hipMemcpy(uu.data(), src, step_cells * sizeof(uint16_t), hipMemcpyDeviceToHost));

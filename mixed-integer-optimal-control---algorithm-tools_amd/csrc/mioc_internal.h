@@ -87,6 +87,12 @@ hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
                            const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
                            size_t uu_stride_k, int32_t *counters);
 size_t pyr_lds_bytes(const PyrGeom &G);
+// separable L1 transform (mioc_sdt.hip): same staging layout, 8^M grids (M = 3, 4), beta > 0
+bool sdt_supported(const PyrGeom &G);
+size_t sdt_lds_bytes(const PyrGeom &G);
+hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
+                           const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
+                           size_t uu_stride_k, int32_t *counters);
 hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
                                 const double *S0, size_t s_stride, int Bu, Start *start);
 hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,

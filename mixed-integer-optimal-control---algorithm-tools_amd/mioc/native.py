@@ -27,7 +27,7 @@ MIOC_ENONFINITE = -7
 
 MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
 MIOC_OPT_ALGO, MIOC_OPT_TIMING = 1, 2
-MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID = 0, 1, 2, 3
+MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID, MIOC_ALGO_SEPARABLE = 0, 1, 2, 3, 4
 
 EXPORTED = [
     "mioc_version", "mioc_create", "mioc_destroy", "mioc_last_error", "mioc_set_option", "mioc_set_levels",
@@ -281,3 +281,9 @@ def pyramid_eligible(levels: LevelTable):
     if not np.array_equal(((levels.tuples - 1) * strides).sum(axis=1), np.arange(levels.L)):
         return False
     return all(list(v) == list(range(v[0], v[0] + len(v))) for v in levels.nu)
+
+
+def separable_eligible(levels: LevelTable):
+    """Mirror of the library's separable-transform domain (p = 1 and beta > 0 are checked by the library):
+    the pyramid domain restricted to 8^3 and 8^4 grids."""
+    return pyramid_eligible(levels) and levels.M in (3, 4) and all(int(c) == 8 for c in levels.counts)

@@ -37,6 +37,8 @@ def _oracle_levels(lt):
 def _algos(p_kind, lt=None):
     if p_kind == P_INF:
         return ALGOS_PINF
+    if p_kind == P_ONE and lt is not None and native.separable_eligible(lt):
+        return (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID, native.MIOC_ALGO_SEPARABLE)
     if p_kind == P_ONE and lt is not None and native.pyramid_eligible(lt):
         return (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID)
     return (native.MIOC_ALGO_GENERIC,)
@@ -365,10 +367,14 @@ def test_trm_on_gpu_matches_trm_on_oracle():
         assert np.array_equal(objs[0].x, objs[1].x)
 
 
-@pytest.mark.parametrize("mode", ["gauss", "integer", "zero", "dyadic"])
-def test_pyramid_vs_oracle_512_levels(oracle_c, mode):
-    """8x8x8 product grid, p=1: clean rows (pyramid + value lookup) and dirty rows (exact scan)."""
-    rng = np.random.default_rng({"gauss": 1, "integer": 2, "zero": 3, "dyadic": 4}[mode])
+@pytest.mark.parametrize("algo", ["pyramid", "separable"])
+@pytest.mark.parametrize("mode", ["gauss", "integer", "zero", "dyadic", "steep"])
+def test_pyramid_vs_oracle_512_levels(oracle_c, mode, algo):
+    """8x8x8 product grid, p=1: clean rows (pyramid + value lookup / certified transform argmin) and
+    dirty rows (exact scan).  "steep": value spread ~1e14 times beta, outside the separable
+    transform's binade, so its rows go to the exact scan."""
+    algo = {"pyramid": native.MIOC_ALGO_PYRAMID, "separable": native.MIOC_ALGO_SEPARABLE}[algo]
+    rng = np.random.default_rng({"gauss": 1, "integer": 2, "zero": 3, "dyadic": 4, "steep": 5}[mode])
     lv = Levels.product([list(range(8))] * 3)
     lt = LevelTable(lv.nu, [tuple(t) for t in lv.tuples])
     n, B = 12, 20
@@ -378,12 +384,14 @@ def test_pyramid_vs_oracle_512_levels(oracle_c, mode):
         df = rng.integers(-3, 4, size=(3, n)).astype(float)
     elif mode == "zero":
         df = np.zeros((3, n))
+    elif mode == "steep":
+        df = rng.standard_normal((3, n)) * 1e3
     else:
         df = rng.integers(-64, 65, size=(3, n)) / 64.0
     uo = np.array([lv.nuval[rng.integers(lv.L)] for _ in range(n)], dtype=np.float64).T
-    beta, dt = (0.125, 0.25) if mode != "gauss" else (1e-3, 2.0 ** -10)
+    beta, dt = {"gauss": (1e-3, 2.0 ** -10), "steep": (1e-12, 2.0 ** -10)}.get(mode, (0.125, 0.25))
     phi, U = oracle_c.bellman(lv, df, uo, B, P_ONE, beta, dt)
-    ctx = _ctx(lt, P_ONE, beta, native.MIOC_ALGO_PYRAMID)
+    ctx = _ctx(lt, P_ONE, beta, algo)
     ctx.bellman(df, uo, B, dt)
     diag = ctx.diagnostics()
     _assert_U(ctx, U, n, mode)
@@ -392,8 +400,13 @@ def test_pyramid_vs_oracle_512_levels(oracle_c, mode):
         u, ps, _ = ctx.backtrack(Bp)
         assert np.array_equal(u, ou), f"{mode} Bp={Bp} diag={diag}"
         assert ps == ops
+    assert ctx.last_algo() == algo
     if mode in ("integer", "zero"):
         assert diag[0] > 0  # the exact scan for targets whose winning value is tied was exercised
+    if algo == native.MIOC_ALGO_SEPARABLE:
+        assert diag[1] > 0  # rows near B (few targets) went straight to the exact scan
+        if mode == "steep":
+            assert diag[0] == 0 and diag[1] > 1000  # every row out of the binade: all exact scans
     ctx.close()
 
 
@@ -438,14 +451,24 @@ def test_run_ahead_walk_vs_oracle(oracle_c, uo_mode, pk):
 
 
 def test_pyramid_equals_generic_at_c4_scale():
-    """4096 levels, B=256, p=1: the pyramid and the generic sweep are independent algorithms."""
+    """4096 levels, B=256, p=1: the pyramid, the separable transform and the generic sweep are independent
+    algorithms.  Also every U cell of a late step (where most cells are finite) agrees."""
     cfg = CONFIGS["C4"]
     lt, df, uo = make_inputs(cfg, nt=48)
-    out = {}
-    for algo in (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID):
+    out, tabs = {}, {}
+    algos = (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID, native.MIOC_ALGO_SEPARABLE)
+    for algo in algos:
         ctx = _ctx(lt, P_ONE, cfg.beta, algo)
         ctx.bellman(df, uo, cfg.B, cfg.dt)
+        assert ctx.last_algo() == algo
+        tabs[algo] = [ctx.argmin_table(i) for i in (0, 20)]
         out[algo] = [ctx.backtrack(Bp)[:2] for Bp in (cfg.B, 100, 7)]
         ctx.close()
-    for (ug, pg), (up, pp) in zip(out[native.MIOC_ALGO_GENERIC], out[native.MIOC_ALGO_PYRAMID]):
-        assert np.array_equal(ug, up) and pg == pp
+    for algo in algos[1:]:
+        for (ug, pg), (up, pp) in zip(out[native.MIOC_ALGO_GENERIC], out[algo]):
+            assert np.array_equal(ug, up) and pg == pp, f"algo={algo}"
+    # cells with c >= b̃ that generic and the staged algorithms both wrote agree wherever both are >= 0
+    for a_, b_ in zip(tabs[native.MIOC_ALGO_PYRAMID], tabs[native.MIOC_ALGO_SEPARABLE]):
+        m = (a_ >= 0) & (b_ >= 0)
+        assert m.sum() > 0.5 * m.size
+        assert np.array_equal(a_[m], b_[m])
