@@ -168,6 +168,7 @@ def roofline_of(res, args):
     lv, B, K, nt = res["levels"], res["B"], res["K"], res["nt"]
     L = lv.L
     avg_s = (res["dom_ms"] / 1e3) / max(1, res["dom_n"])
+    steps = 1  # DP recursion steps per launch
     if res["dom_name"] == "k_generic_step":
         # front in + front out (fp64) + compact U (uint16/uint8) per step, per subproblem
         ub = 1 if L <= 256 else 2
@@ -177,13 +178,15 @@ def roofline_of(res, args):
         roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
                      "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
                      "candidates_per_launch": ncand}
-    elif res["dom_name"] == "k_sdt_step":
-        # the same algorithmic traffic as the reference DP step: front in + front out + compact U
-        bytes_per_launch = K * (B + 1) * L * (8 + 8 + 2)
+    elif res["dom_name"] in ("k_sdt_step", "k_sdt_run"):
+        # the same algorithmic traffic as the reference DP step: front in + front out + compact U, per step;
+        # k_sdt_run is one persistent launch over all nt - 1 steps
+        steps = (nt - 1) if res["dom_name"] == "k_sdt_run" else 1
+        bytes_per_launch = steps * K * (B + 1) * L * (8 + 8 + 2)
         M = lv.M
         # per pass and 8-point line: 20 merges (7 forward, 6 backward, 7 combine), each add + min + sub + cmp
-        ops = 1.0 * K * (B + 1) * L * M * (20 / 8) * 4
-        ncand = K * candidates_per_step(lv, res["uo"], B)
+        ops = 1.0 * steps * K * (B + 1) * L * M * (20 / 8) * 4
+        ncand = steps * K * candidates_per_step(lv, res["uo"], B)
         roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
                      "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
                      "note": "separable transform FP64 ops (4 per merge); brute-force-equivalent candidates/s "
@@ -211,7 +214,8 @@ def roofline_of(res, args):
     roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None if traffic is None else round(traffic),
             "traffic_source": tsrc, "kernel": res["dom_name"],
-            "avg_launch_us": round(avg_s * 1e6, 3), "bytes_per_launch": bytes_per_launch}
+            "avg_launch_us": round(avg_s * 1e6, 3), "bytes_per_launch": bytes_per_launch,
+            "us_per_dp_step": round(avg_s * 1e6 / steps, 3)}
     roof_valu = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in roof_valu.items()}
     return roof, roof_valu
 

@@ -57,6 +57,8 @@ extern "C" {
 #define MIOC_ALGO_SEPARABLE 4 /* p=1, beta>0, 8^3 / 8^4 product grid of consecutive levels: separable L1
                                  distance transform in exact fixed point with a certified argmin */
 #define MIOC_OPT_TIMING 2   /* 1: record HIP events around the dominant kernel (mioc_kernel_stats) */
+#define MIOC_OPT_PERSIST 3  /* separable transform: 1 (default) runs the whole DP as one persistent launch
+                               whose workgroups hand rows to each other; 0: one launch per step */
 
 typedef struct mioc_ctx mioc_ctx;
 

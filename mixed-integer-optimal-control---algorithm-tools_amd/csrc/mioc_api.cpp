@@ -67,6 +67,7 @@ LevelsDev levels_dev(const mioc_ctx *ctx) {
   Lv.p_kind = ctx->p_kind;
   Lv.p_int = (int)ctx->p_int;
   Lv.beta = ctx->beta;
+  Lv.inv_beta = ctx->beta > 0.0 ? 1.0 / ctx->beta : 0.0;
   Lv.costlut = ctx->d_costlut;
   Lv.costtab = ctx->d_costtab;
   return Lv;
@@ -88,6 +89,8 @@ ProblemDev problem_dev(const mioc_ctx *ctx) {
 void ev_collect(mioc_ctx *ctx);
 
 void free_all(mioc_ctx *ctx) {
+  if (ctx->d_runflags) hipFree(ctx->d_runflags);
+  if (ctx->h_run_err) hipHostFree(ctx->h_run_err);
   void *ptrs[] = {ctx->d_nuval, ctx->d_nuint,  ctx->d_gidx,      ctx->d_numin,       ctx->d_numax,
                   ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
@@ -241,7 +244,33 @@ int run_bellman(mioc_ctx *ctx) {
 
   if (algo == MIOC_ALGO_PYRAMID || algo == MIOC_ALGO_SEPARABLE) {
     const size_t s_stride = (size_t)(ctx->B + 1) * L;
-    int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, 2 * K * s_stride * sizeof(double), "staging fronts");
+    // persistent separable transform: every workgroup resident (rows dealt round-robin over at most
+    // blocks-per-CU x CUs workgroups), three staging buffers
+    // one workgroup per CU (its register file allows no second one); the row left over by B+1 > CUs is the
+    // cheapest pair (c' = 0: one finite source; c' = B: one target)
+    const size_t run_lds = std::max<size_t>(sdt_lds_bytes(ctx->pyr), 96 * 1024);
+    int nwg = 0;
+    bool persist = false;
+    // (B + 1)·L·8 < 2^31: the persistent kernel addresses a staging block with 32-bit buffer offsets
+    if (algo == MIOC_ALGO_SEPARABLE && ctx->opt_persist && nt >= 2 && s_stride * sizeof(double) < (1ull << 31)) {
+      int ncu = 0;
+      HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+      const int bpc = sdt_run_blocks_per_cu(ctx->pyr, run_lds);
+      // contiguous row chunks, nwg / K workgroups per subproblem
+      const size_t slots = (size_t)ncu * (size_t)std::max(bpc, 0);
+      const size_t per_k = std::min<size_t>((size_t)std::max<int64_t>(ctx->B, 1), K ? slots / K : 0);  // B: rows 0, B share one
+      nwg = (int)(per_k * K);
+      persist = per_k > 0;
+    }
+    const size_t runflag_bytes = ((2 * K * (size_t)(ctx->B + 1) + 1) * sizeof(int32_t) + 15) / 16 * 16;
+    if (persist) {
+      int rcf = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, runflag_bytes, "persistent row flags");
+      if (rcf) return rcf;
+      if (!ctx->h_run_err) HIP_TRY(ctx, hipHostMalloc(&ctx->h_run_err, 16, 0));
+      *ctx->h_run_err = 0;
+    }
+    const int nbuf = persist ? 3 : 2;
+    int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, nbuf * K * s_stride * sizeof(double), "staging fronts");
     if (rc) return rc;
     const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
     rc = grow(ctx, &ctx->d_U, &ctx->U_cap, K * uu_stride_k * sizeof(uint16_t), "argmin table U");
@@ -249,20 +278,33 @@ int run_bellman(mioc_ctx *ctx) {
     rc = grow(ctx, &ctx->d_perm, &ctx->perm_cap, K * nt * L * sizeof(uint32_t), "sphere orders");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
+    double *term = persist ? ctx->d_stage + ((nt - 1) % 3) * K * s_stride : st[(nt - 1) & 1];
     HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm));
-    HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, st[(nt - 1) & 1], s_stride));
-    if (algo == MIOC_ALGO_SEPARABLE) {
+    HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, term, s_stride));
+    if (algo == MIOC_ALGO_SEPARABLE && persist) {
+      // the whole DP as one persistent launch: rows handed between resident workgroups by flags
+      HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, runflag_bytes, ctx->stream));
+      ev_begin(ctx, 0, "k_sdt_run");
+      HIP_TRY(ctx, launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_stage, K * s_stride,
+                                  (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters, ctx->d_runflags,
+                                  nwg, run_lds));
+      ev_end(ctx, 0, 1);
+      HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + 2 * K * (size_t)(ctx->B + 1), sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, ctx->stream));
+      ctx->run_pending = true;
+    } else if (algo == MIOC_ALGO_SEPARABLE) {
       ev_begin(ctx, 0, "k_sdt_step");
       for (int i = ctx->nt - 2; i >= 0; --i)
         HIP_TRY(ctx, launch_sdt_step(ctx->stream, P, Lv, ctx->pyr, i, ctx->d_perm, st[(i + 1) & 1], st[i & 1],
                                      (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters));
+      ev_end(ctx, 0, ctx->nt - 1);
     } else {
       ev_begin(ctx, 0, "k_pyr_step");
       for (int i = ctx->nt - 2; i >= 0; --i)
         HIP_TRY(ctx, launch_pyr_step(ctx->stream, P, Lv, ctx->pyr, i, ctx->d_perm, st[(i + 1) & 1], st[i & 1],
                                      (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters));
+      ev_end(ctx, 0, ctx->nt - 1);
     }
-    ev_end(ctx, 0, ctx->nt - 1);
   } else if (algo == MIOC_ALGO_GENERIC) {
     ctx->ubytes = L <= 256 ? 1 : 2;
     const size_t front_stride = L * RP;
@@ -347,6 +389,17 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
   return MIOC_OK;
 }
 
+// after a synchronisation: did the persistent DP's dependency waits time out?
+int check_run(mioc_ctx *ctx) {
+  if (!ctx->run_pending) return MIOC_OK;
+  ctx->run_pending = false;
+  if (ctx->h_run_err && *ctx->h_run_err) {
+    ctx->have_dp = false;
+    return fail(ctx, MIOC_EHIP, "persistent DP: a workgroup's dependency wait timed out (workgroups not co-resident?)");
+  }
+  return MIOC_OK;
+}
+
 int check_ready(mioc_ctx *ctx) {
   if (!ctx) return MIOC_EINVAL;
   if (!ctx->have_levels) return fail(ctx, MIOC_ESTATE, "mioc_set_levels has not been called");
@@ -426,6 +479,10 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   }
   if (option == MIOC_OPT_TIMING) {
     ctx->timing = value != 0;
+    return MIOC_OK;
+  }
+  if (option == MIOC_OPT_PERSIST) {
+    ctx->opt_persist = value != 0;
     return MIOC_OK;
   }
   return fail(ctx, MIOC_EINVAL, "unknown option");
@@ -589,6 +646,8 @@ int32_t mioc_bellman(mioc_ctx *ctx, const double *df, const double *u_old, int64
   rc = run_bellman(ctx);
   if (rc) return rc;
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  rc = check_run(ctx);
+  if (rc) return rc;
   ev_collect(ctx);
   return MIOC_OK;
 }
@@ -641,7 +700,7 @@ int32_t mioc_synchronize(mioc_ctx *ctx) {
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   ev_collect(ctx);
-  return MIOC_OK;
+  return check_run(ctx);
 }
 
 void *mioc_stream(mioc_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
@@ -702,7 +761,10 @@ int32_t mioc_get_argmin_table(mioc_ctx *ctx, int64_t k, int64_t step, int32_t *U
     HIP_TRY(ctx, hipMemcpy(uu.data(), src, step_cells * sizeof(uint16_t), hipMemcpyDeviceToHost));
     for (int64_t r = 0; r < L; ++r) {
       const int64_t b = bt(r);
-      for (int64_t c = b; c < R; ++c) out[c + R * ctx->gidx_h[r]] = uu[(c - b) * L + r];
+      for (int64_t c = b; c < R; ++c) {  // 0xFFFF: a cell the separable transform left unwritten (Φ = +Inf)
+        const uint16_t x = uu[(c - b) * L + r];
+        out[c + R * ctx->gidx_h[r]] = x == 0xFFFF ? -1 : (int32_t)x;
+      }
     }
   } else {  // generic: U_i[l][c]
     std::vector<unsigned char> raw(step_cells * ctx->ubytes);

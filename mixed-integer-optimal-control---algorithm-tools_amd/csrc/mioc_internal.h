@@ -28,6 +28,7 @@ struct LevelsDev {
   int p_kind = MIOC_P_INF;
   int p_int = 1;
   double beta = 0.0;
+  double inv_beta = 0.0;           // fl(1/beta) for beta > 0 (separable transform scale)
   const double *costlut = nullptr; // beta*weight by integer key (P_INF: [beta], P_ONE/P_INTLUT)
   const double *costtab = nullptr; // [L][L] beta*weight (P_TABLE only)
 };
@@ -93,6 +94,10 @@ size_t sdt_lds_bytes(const PyrGeom &G);
 hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
                            const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
                            size_t uu_stride_k, int32_t *counters);
+hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
+                          const uint32_t *perm, double *S, size_t buf_stride, uint16_t *UU, size_t s_stride,
+                          size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, size_t lds);
+int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds);
 hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
                                 const double *S0, size_t s_stride, int Bu, Start *start);
 hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,
@@ -166,6 +171,11 @@ struct mioc_ctx {
   size_t stage_cap = 0;
   uint32_t *d_perm = nullptr;      // [K][nt][L] sphere order of u_old(i): rank | (L1 distance << 16)
   size_t perm_cap = 0;
+  bool opt_persist = true;         // separable transform: one persistent launch (MIOC_OPT_PERSIST)
+  int32_t *d_runflags = nullptr;   // persistent DP: [K][B+1] done, [K][B+1] loaded, err
+  size_t runflag_cap = 0;
+  int32_t *h_run_err = nullptr;    // pinned copy of err
+  bool run_pending = false;
   int32_t *d_counters = nullptr;   // [8] diagnostics: value-collision targets, multi-level targets, ...
 
   // generic buffers

@@ -22,6 +22,9 @@
 // rows with very few targets and rows whose scale does not fit the binade are resolved by an exact scan
 // of the reference loop.  Results are bit-identical to the reference in every case.
 //
+// Two drivers: one launch per step (k_sdt_step), or the whole DP as one persistent launch (k_sdt_run) whose
+// workgroups hand rows to each other through per-row flags.
+//
 // Layout: the staging layout of the pyramid (mioc_pyramid.hip): S_i[c'][pos_i(l)] = Φ_i[l, c' + b̃_l(i)]
 // (+Inf where c' + b̃_l > B) in the sphere order of u_old(i), UU_i[c'][l] = U_i[l, c' + b̃_l(i)] (uint16
 // rank, natural order).  One workgroup of L/8 threads per source row; every pass gives each thread one
@@ -39,6 +42,61 @@ constexpr int SD_FLAG = 1 << SD_RB;      // near-tie flag (payload bit 12)
 constexpr int SD_PAY = 2 * SD_FLAG - 1;  // payload mask: 13 low mantissa bits
 constexpr int SD_COOP = 8;               // listed targets up to this many: whole-workgroup scans, else one wave each
 constexpr int SD_FEW = 4;                // rows with at most this many targets go straight to the exact scan
+constexpr int SD_SPARSE = 4;             // rows with at most this many finite sources: direct minimum over them
+constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, the scan sweeps every rank
+
+// Diagnostic build only (make stamps -> libmioc_stamps.so): per-workgroup phase clocks of the last launch.
+#if defined(MIOC_STAMPS) && !defined(MIOC_STAMPS_TL)
+// phase clocks are kept in LDS (a global store would join the vmcnt queue and delay the row's own
+// loads) and copied out once per row: g_sdt_stamps[workgroup] = the last row it processed
+__device__ unsigned long long g_sdt_stamps[4096][16];
+#define SD_STAMP(k)                                                                          \
+  do {                                                                                       \
+    if (threadIdx.x == 0) sh.stamp[k] = __builtin_amdgcn_s_memtime();                         \
+  } while (0)
+#define SD_RSTAMP(k)                                                                         \
+  do {                                                                                       \
+    if (threadIdx.x == 0) sh.stamp[k] = __builtin_amdgcn_s_memrealtime();                     \
+  } while (0)
+#define SD_FLUSH()                                                                           \
+  do {                                                                                       \
+    if (threadIdx.x == 0)                                                                    \
+      for (int _q = 0; _q < 16; ++_q) g_sdt_stamps[blockIdx.x][_q] = sh.stamp[_q];           \
+  } while (0)
+#define SD_TL(k) \
+  do {           \
+  } while (0)
+#elif defined(MIOC_STAMPS)
+// persistent-kernel timeline (diagnostic build, make stamps_tl): per row, for steps i < 64: wait begin, wait
+// end (after the barrier), row body end, done published -- s_memrealtime (100 MHz); no in-row stamps
+__device__ unsigned long long g_sdt_tl[4096][64][4];
+#define SD_TL(k)                                                                                          \
+  do {                                                                                                    \
+    if (threadIdx.x == 0 && g < 4096 && i < 64) g_sdt_tl[g][i][k] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+#define SD_STAMP(k) \
+  do {              \
+  } while (0)
+#define SD_RSTAMP(k) \
+  do {               \
+  } while (0)
+#define SD_FLUSH() \
+  do {             \
+  } while (0)
+#else
+#define SD_TL(k) \
+  do {           \
+  } while (0)
+#define SD_STAMP(k) \
+  do {              \
+  } while (0)
+#define SD_RSTAMP(k) \
+  do {               \
+  } while (0)
+#define SD_FLUSH() \
+  do {             \
+  } while (0)
+#endif
 
 // v_min_f64 without llvm.minnum's canonicalising v_max_f64 x,x on every operand (inputs are finite or +Inf)
 __device__ __forceinline__ double sd_min(double a, double b) {
@@ -69,7 +127,8 @@ __device__ __forceinline__ int sd_rank(int q, int m, int x) {
 // Exact scan of the listed targets: the reference loop (HelpFunctions.jl:60-77) for one cell each.
 // COOP: the whole workgroup scans one target at a time (thread t: sources t + T·s, ascending), then a
 // (value, rank) minimum, ties to the lower rank.  Otherwise one wave per target (lane: sources
-// lane + 64·t).  Writes U (finite minimum) and the value (+Inf if none) into outnat.
+// lane + 64·t); list == nullptr scans every rank whose outnat slot is NaN.  Writes U (finite minimum, into the
+// LDS U row) and the value (+Inf if none) into outnat.
 template <int M, bool COOP>
 __device__ __forceinline__ void sd_scan(const uint16_t *list, int nl, const double *psi, const double *a,
                                         const int *base, double beta, uint16_t *UU, double *outnat, double *redv,
@@ -139,7 +198,8 @@ __device__ __forceinline__ void sd_scan(const uint16_t *list, int nl, const doub
     }
   } else {
     for (int e = w; e < nl; e += NW) {
-      const int r = list[e];
+      const int r = list ? (int)list[e] : e;
+      if (!list && !__builtin_isnan(outnat[r])) continue;  // overflowed list: every NaN-marked rank
       int xl[M];
       const double t1 = target(r, xl);
       double bv = INFINITY;
@@ -164,86 +224,133 @@ __device__ __forceinline__ void sd_scan(const uint16_t *list, int nl, const doub
   }
 }
 
+// Global traffic of a row.  The per-step kernel uses plain loads and stores (kernel boundaries order the
+// steps).  The persistent kernel hands rows between workgroups inside one launch (MI355X_MICROARCH.md,
+// visibility: payload stored write-through `sc1` and drained, flag stored `sc1`, every load of handed-off
+// bytes an `sc1` load), so there its staging loads and stores are `sc1` buffer loads / stores (aux 16),
+// 16 bytes per lane where the layout allows (narrow `sc1` stores cost 2-3x per byte and write partial lines).
+// `base` is wave-uniform (a subproblem's staging block or one row of it), `bytes` its extent (< 2^31).
+typedef unsigned int sd_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int sd_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sd_rsrc(const double *base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base), 0, bytes, 0x00020000);
+}
+template <bool SC1>
+__device__ __forceinline__ double sd_load8(const double *base, int bytes, int e) {
+  if constexpr (SC1) {
+    const sd_u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(sd_rsrc(base, bytes), e * 8, 0, 16);
+    return __hiloint2double((int)w.y, (int)w.x);
+  } else {
+    return base[e];
+  }
+}
+// Ψ at elements ea (even) and eb of a staging block: eb = ea + 1 (one 16-byte load) unless the pair straddles
+// a sphere boundary, i.e. its two positions come from different rows (then a second, 8-byte load)
+template <bool SC1>
+__device__ __forceinline__ void sd_load_pair(const double *base, int bytes, int ea, int eb, double &va, double &vb) {
+  if constexpr (SC1) {
+    const sd_u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(sd_rsrc(base, bytes), ea * 8, 0, 16);
+    va = __hiloint2double((int)t.y, (int)t.x);
+    vb = __hiloint2double((int)t.w, (int)t.z);
+  } else {
+    const double2 t = *reinterpret_cast<const double2 *>(base + ea);
+    va = t.x;
+    vb = t.y;
+  }
+  if (eb != ea + 1) vb = sd_load8<SC1>(base, bytes, eb);
+}
+template <bool SC1>
+__device__ __forceinline__ void sd_store16(double *base, int bytes, int e, unsigned long long lo,
+                                           unsigned long long hi) {
+  if constexpr (SC1) {
+    const sd_u32x4 d = {(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(d, sd_rsrc(base, bytes), e * 8, 0, 16);
+  } else {
+    *reinterpret_cast<ulonglong2 *>(base + e) = make_ulonglong2(lo, hi);
+  }
+}
+
+template <int NW>
+struct SdtShared {
+  double redv[SD_COOP * NW];
+  int redj[SD_COOP * NW];
+  double rmn[NW], rmx[NW];
+  int rnv[NW];
+  int nlist;
+  int stop;  // persistent kernel: a dependency wait timed out
+  unsigned long long stamp[16];  // diagnostic build: phase clocks of the current row
+  int nsp;   // sparse rows: the finite sources (rank, Ψ)
+  int spj[SD_SPARSE];
+  double spv[SD_SPARSE];
+};
+
+// The sphere orders a step reads (step i+1, for the sources) and writes (step i, for the output row), as the
+// position pairs 2(tid + T·q) + {0, 1} of this thread, plus both heads (position 0).  Loaded at the start of
+// a row (per-step kernel) or ahead of the dependency wait (persistent kernel): they are static, so their
+// latency never sits behind a barrier.
+struct SdPerm {
+  uint2 in[4], out[4];
+  uint32_t hin, hout;
+};
 template <int M>
-__global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i,
-                                                           const uint32_t *__restrict__ perm_all,
-                                                           const double *__restrict__ Sin_all,
-                                                           double *__restrict__ Sout_all,
-                                                           uint16_t *__restrict__ UU_all, size_t s_stride,
-                                                           size_t uu_stride_k, int32_t *__restrict__ counters) {
+__device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restrict__ perm_all, int nt, int k,
+                                             int i) {
+  constexpr int T = 1 << (3 * M - 3);
+  const uint32_t *pin = perm_all + ((size_t)k * nt + i + 1) * ((size_t)T * 8);
+  const uint32_t *pout = perm_all + ((size_t)k * nt + i) * ((size_t)T * 8);
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    pm.in[q] = *reinterpret_cast<const uint2 *>(pin + 2 * (tid + T * q));
+    pm.out[q] = *reinterpret_cast<const uint2 *>(pout + 2 * (tid + T * q));
+  }
+  pm.hin = pin[0];
+  pm.hout = pout[0];
+}
+
+// One source row c' of step i for subproblem k: reads S_{i+1} (Sin), writes row c' of S_i (Sout) and of
+// UU_i.  `loaded` (persistent kernel): flag stored once this row's reads of S_{i+1} are complete.
+template <int M, bool PERSIST>
+__device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int k, int cp,
+                                        int i, const SdPerm &pm, const double *Sin_all,
+                                        double *Sout_all, uint16_t *__restrict__ UU_all, size_t s_stride,
+                                        size_t uu_stride_k, int32_t *__restrict__ counters,
+                                        SdtShared<(1 << (3 * M - 3)) / 64> &sh, unsigned char *sds, int32_t *loaded,
+                                        int token) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
-  extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
-  double *psi = reinterpret_cast<double *>(sds);      // [L] Ψ_j by rank
-  double *dtv = psi + L;                              // [L] transform values (swizzled), then outputs (natural)
-  uint16_t *list = reinterpret_cast<uint16_t *>(dtv + L);  // [L] targets for the exact scan
-  __shared__ double redv[SD_COOP * NW];
-  __shared__ int redj[SD_COOP * NW];
-  __shared__ double rmn[NW], rmx[NW];
-  __shared__ int rnv[NW];
-  __shared__ int nlist;
+  double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
+  double *dtv = psi + L;                                // [L] transform values (swizzled), then outputs (natural)
+  uint16_t *uu = reinterpret_cast<uint16_t *>(dtv + L);  // [L] the U row (natural order)
+  uint16_t *list = uu + L;                              // [SD_LCAP] targets for the exact scan
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int k = blockIdx.y, cp = (int)blockIdx.x, B = P.B;
+  const int B = P.B;
   const double beta = Lv.beta;
   const double *Sin = Sin_all + (size_t)k * s_stride;
   double *Sout = Sout_all + (size_t)k * s_stride + (size_t)cp * L;
   uint16_t *UU = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L) + (size_t)cp * L;
   const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
   const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
-  const uint32_t *pin = perm_all + ((size_t)k * P.nt + i + 1) * L;
-  const uint32_t *pout = perm_all + ((size_t)k * P.nt + i) * L;
+  const uint2 *ein = pm.in, *eout = pm.out;
+  SD_RSTAMP(13);
+  SD_STAMP(0);
 
-  // ---- sources: Ψ_j = Φ_{i+1}[j, c'] = S_{i+1}[c' - b̃_j(i+1)][pos_{i+1}(j)], read position-coalesced ----
-  uint32_t ein[8], eout[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    ein[q] = pin[tid + T * q];
-    eout[q] = pout[tid + T * q];
-  }
+  // ---- sources: Ψ_j = Φ_{i+1}[j, c'] = S_{i+1}[c' - b̃_j(i+1)][pos_{i+1}(j)]; thread: position pairs
+  // 2(tid + T·q) + {0, 1}, so each wave instruction covers 512 contiguous bytes ----------------------
+  // all loads issue back to back: a row below 0 (no such budget) reads row 0 and is masked after
+  const int sbytes = (B + 1) * L * (int)sizeof(double);
   double v[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int row = cp - (int)(ein[q] >> 16);
-    v[q] = row >= 0 ? Sin[(size_t)row * L + tid + T * q] : INFINITY;
-  }
-  if (tid == 0) nlist = 0;
-  double pmn = INFINITY, pmx = -INFINITY;
-  int nv = 0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    psi[ein[q] & 0xFFFFu] = v[q];
-    if (v[q] < INFINITY) {
-      pmn = fmin(pmn, v[q]);
-      pmx = fmax(pmx, v[q]);
-    }
-    nv += (int)(eout[q] >> 16) <= B - cp;  // target inside the trust region: c' + b̃_l(i) <= B
+  for (int q = 0; q < 4; ++q) {
+    const int p2 = 2 * (tid + T * q);
+    const int ra = max(cp - (int)(ein[q].x >> 16), 0), rb = max(cp - (int)(ein[q].y >> 16), 0);
+    sd_load_pair<PERSIST>(Sin, sbytes, ra * L + p2, rb * L + p2 + 1, v[2 * q], v[2 * q + 1]);
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    pmn = fmin(pmn, __shfl_xor(pmn, off));
-    pmx = fmax(pmx, __shfl_xor(pmx, off));
-    nv += __shfl_xor(nv, off);
-  }
-  if (lane == 0) {
-    rmn[w] = pmn;
-    rmx[w] = pmx;
-    rnv[w] = nv;
-  }
-  __syncthreads();
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-  for (int q = 0; q < NW; ++q) {
-    pmn = fmin(pmn, rmn[q]);
-    pmx = fmax(pmx, rmx[q]);
-  }
-  nv = 0;
-#pragma unroll
-  for (int q = 0; q < NW; ++q) nv += rnv[q];
-  if (nv == 0 || !(pmn < INFINITY)) {  // no target in the trust region, or nothing reachable
-#pragma unroll
-    for (int q = 0; q < 8; ++q) Sout[tid + T * q] = INFINITY;
-    return;
-  }
-
-  // ---- the binade: values base + (Ψ - Ψmin)/β + d lie in [base, 2·base), grid g = 2^13 ulp ----------
+    for (int h = 0; h < 2; ++h)
+      if ((int)((h ? ein[q].y : ein[q].x) >> 16) > cp) v[2 * q + h] = INFINITY;
+  // ---- this thread's targets: ranks tid | x << 3(M-1) (the lines of the last pass) -----------------
   double a[M];
   int lb[M], uo[M];
 #pragma unroll
@@ -252,7 +359,69 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
     lb[m] = G.base[m];
     uo[m] = (int)uoi[m];
   }
-  const double inv = 1.0 / beta;
+  double pre = 0.0;
+  int bpre = 0;
+  int xt[M];
+#pragma unroll
+  for (int m = 0; m < M - 1; ++m) {
+    xt[m] = (tid >> (3 * m)) & 7;
+    const int nu = lb[m] + xt[m];
+    pre = pre + a[m] * (double)nu;  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
+    bpre += abs(nu - uo[m]);
+  }
+  unsigned valid = 0;  // target inside the trust region: c' + b̃_l(i) <= B
+#pragma unroll
+  for (int x = 0; x < 8; ++x) valid |= (unsigned)(bpre + abs(lb[M - 1] + x - uo[M - 1]) <= B - cp) << x;
+
+  if (tid == 0) sh.nlist = 0;
+  double pmn = INFINITY, pmx = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const double x = v[2 * q + h];
+      psi[(h ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
+      if (x < INFINITY) {
+        pmn = fmin(pmn, x);
+        pmx = fmax(pmx, x);
+      }
+    }
+  int nv = __popc(valid);  // targets in the trust region (low 16 bits) + finite sources (high 16 bits)
+#pragma unroll
+  for (int q = 0; q < 8; ++q) nv += (v[q] < INFINITY) << 16;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    pmn = fmin(pmn, __shfl_xor(pmn, off));
+    pmx = fmax(pmx, __shfl_xor(pmx, off));
+    nv += __shfl_xor(nv, off);
+  }
+  if (lane == 0) {
+    sh.rmn[w] = pmn;
+    sh.rmx[w] = pmx;
+    sh.rnv[w] = nv;
+  }
+  __syncthreads();  // every load of S_{i+1} has returned (its value is in LDS)
+  if (PERSIST && tid == 0) __hip_atomic_store(loaded, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    pmn = fmin(pmn, sh.rmn[q]);
+    pmx = fmax(pmx, sh.rmx[q]);
+  }
+  nv = 0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) nv += sh.rnv[q];
+  const int nf = nv >> 16;
+  nv &= 0xFFFF;
+  SD_STAMP(1);
+  if (nv == 0 || !(pmn < INFINITY)) {  // no target in the trust region, or nothing reachable
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      sd_store16<PERSIST>(Sout, L * 8, 2 * (tid + T * q), 0x7FF0000000000000ull, 0x7FF0000000000000ull);
+    return;
+  }
+
+  // ---- the binade: values base + (Ψ - Ψmin)/β + d lie in [base, 2·base), grid g = 2^13 ulp ----------
+  const double inv = Lv.inv_beta;                      // fl(1/β), host-computed
   const double rs = (pmx - pmn) * inv + (double)Smax;  // scaled range of every transform value
   const bool scale_ok = rs < 0x1p36;                   // else unit steps are not on the grid: exact scans
   const int E = ilogb(fmin(rs, 0x1p36) * (1.0 + 0x1p-20) + 1.0) + 2;  // 2^E >= 2·rs
@@ -262,26 +431,49 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
   for (int m = 0; m < M; ++m) qmax += fabs(a[m]) * (double)max(abs(lb[m]), abs(lb[m] + 7));
   // 2 × stamping error (< g) + 2 × the reference's rounding (<= 4u·qmax per candidate), in units of β
   const double tol = 3.0 * g + 0x1p-49 * qmax * inv;
-  const bool direct = nv <= SD_FEW || !scale_ok || !(tol < base * 0x1p-20);
+  // few finite sources (rows near c' = 0): every target's minimum over them, directly
+  const bool sparse = nf <= SD_SPARSE;
+  const bool direct = !sparse && (nv <= SD_FEW || !scale_ok || !(tol < base * 0x1p-20));
 
-  if (!direct) {
+  double o[8];
+  int spj[SD_SPARSE];
+  double spv[SD_SPARSE];
+  if (sparse) {
+    if (tid == 0) sh.nsp = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (v[2 * q + h] < INFINITY) {
+          const int e = atomicAdd(&sh.nsp, 1);
+          sh.spj[e] = (int)((h ? ein[q].y : ein[q].x) & 0xFFFFu);
+          sh.spv[e] = v[2 * q + h];
+        }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < SD_SPARSE; ++e) {  // uniform: broadcast reads into registers
+      spj[e] = sh.spj[e];
+      spv[e] = sh.spv[e];
+    }
+  } else if (!direct) {
     // ---- stamp: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) | j --------------------------------------------
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int j = (int)(ein[q] & 0xFFFFu);
-      double V = INFINITY;
-      if (v[q] < INFINITY) {
-        const double y = (v[q] - pmn) * inv + base;
-        V = __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | j);
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = (int)((h ? ein[q].y : ein[q].x) & 0xFFFFu);
+        const double x = v[2 * q + h];
+        double V = INFINITY;
+        if (x < INFINITY) {
+          const double y = (x - pmn) * inv + base;
+          V = __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | j);
+        }
+        dtv[sd_swz(j)] = V;
       }
-      dtv[sd_swz(j)] = V;
-    }
     __syncthreads();
-  }
-
-  // ---- M passes: forward and backward sweep along the 8 levels of one dimension, unit step 1.0 -------
-  double o[8];
-  if (!direct) {
+    SD_STAMP(2);
+    // ---- M passes: forward and backward sweep along the 8 levels of one dimension, unit step 1.0 -----
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       int pos[8];
@@ -305,70 +497,386 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
         for (int x = 0; x < 8; ++x) dtv[pos[x]] = o[x];
       }
       __syncthreads();  // last pass: every read of dtv is done before it becomes the output buffer
+      SD_STAMP(3 + m);
     }
   }
 
-  // ---- targets of this thread: ranks tid | x << 3(M-1) ----------------------------------------------
-  double pre = 0.0;
-  int bpre = 0;
-  int xt[M];
-#pragma unroll
-  for (int m = 0; m < M - 1; ++m) {
-    xt[m] = (tid >> (3 * m)) & 7;
-    const int nu = lb[m] + xt[m];
-    pre = pre + a[m] * (double)nu;
-    bpre += abs(nu - uo[m]);
-  }
+  // ---- targets: R(l, j*) for a certified winner; the others are listed for the exact scan (their
+  // output slot holds NaN until the scan fills it) ----------------------------------------------------
   unsigned listed = 0;
+  if (!direct && !sparse) {  // branch-free: the eight winners' Ψ reads issue together
+    int jx[8];
+    double pv[8];
 #pragma unroll
-  for (int x = 0; x < 8; ++x) {
-    const int r = tid | (x << (3 * (M - 1)));
-    const int nu = lb[M - 1] + x;
-    const bool valid = bpre + abs(nu - uo[M - 1]) <= B - cp;
-    double ov = INFINITY;
-    if (direct) {
-      listed |= (unsigned)valid << x;
-    } else if (valid && o[x] < INFINITY) {
-      const int pl = __double2loint(o[x]);
-      if (pl & SD_FLAG) {
-        listed |= 1u << x;
-      } else {
-        const int j = pl & (SD_FLAG - 1);
-        unsigned d = __sad(x, (j >> (3 * (M - 1))) & 7, 0u);
+    for (int x = 0; x < 8; ++x) jx[x] = __double2loint(o[x]) & (SD_FLAG - 1);  // +Inf carries payload 0
 #pragma unroll
-        for (int m = 0; m < M - 1; ++m) d = __sad((j >> (3 * m)) & 7, xt[m], d);
-        const double t1 = pre + a[M - 1] * (double)nu;
-        ov = (t1 + beta * (double)d) + psi[j];  // R(l, j*), HelpFunctions.jl:63-71
-        UU[r] = (uint16_t)j;
-      }
+    for (int x = 0; x < 8; ++x) pv[x] = psi[jx[x]];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const int r = tid | (x << (3 * (M - 1))), j = jx[x];
+      const bool fin = (valid >> x & 1) && o[x] < INFINITY;
+      const bool flg = (__double2loint(o[x]) & SD_FLAG) != 0;
+      unsigned d = __sad(x, (j >> (3 * (M - 1))) & 7, 0u);
+#pragma unroll
+      for (int m = 0; m < M - 1; ++m) d = __sad((j >> (3 * m)) & 7, xt[m], d);
+      const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
+      const double val = (t1 + beta * (double)d) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
+      listed |= (unsigned)(fin && flg) << x;
+      uu[r] = (uint16_t)(fin && !flg ? j : 0xFFFF);  // 0xFFFF: unwritten (Φ = +Inf) or not yet known (listed)
+      dtv[r] = fin ? (flg ? __longlong_as_double(0x7FF8000000000000ll) : val) : INFINITY;
     }
-    dtv[r] = ov;
+  } else {
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const int r = tid | (x << (3 * (M - 1)));
+      double ov = INFINITY;
+      int uj = 0xFFFF;  // U cell not written by the reference (Φ = +Inf) or not yet known (listed)
+      if (direct) {
+        listed |= valid & (1u << x);
+      } else if (sparse) {
+        if (valid >> x & 1) {  // the reference loop over the finite sources, ties to the lower rank
+          const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
+          double bv = INFINITY;
+          int bj = 0xFFFF;
+#pragma unroll
+          for (int e = 0; e < SD_SPARSE; ++e) {
+            if (e < nf) {
+              const int j = spj[e];
+              unsigned d = __sad(x, (j >> (3 * (M - 1))) & 7, 0u);
+#pragma unroll
+              for (int m = 0; m < M - 1; ++m) d = __sad((j >> (3 * m)) & 7, xt[m], d);
+              const double val = (t1 + beta * (double)d) + spv[e];
+              if (val < bv || (val == bv && j < bj)) {
+                bv = val;
+                bj = j;
+              }
+            }
+          }
+          ov = bv;
+          uj = bj;
+        }
+      }
+      uu[r] = (uint16_t)uj;
+      dtv[r] = (listed >> x & 1) ? __longlong_as_double(0x7FF8000000000000ll) : ov;
+    }
   }
   if (listed) {
-    const int at = atomicAdd(&nlist, __popc(listed));
-    int e = at;
+    int e = atomicAdd(&sh.nlist, __popc(listed));
 #pragma unroll
     for (int x = 0; x < 8; ++x)
-      if (listed >> x & 1) list[e++] = (uint16_t)(tid | (x << (3 * (M - 1))));
+      if (listed >> x & 1) {
+        if (e < SD_LCAP) list[e] = (uint16_t)(tid | (x << (3 * (M - 1))));
+        ++e;
+      }
   }
   __syncthreads();
-  const int nl = nlist;
+  SD_STAMP(7);
+  const int nl = sh.nlist;
   if (nl) {
     if (nl <= SD_COOP)
-      sd_scan<M, true>(list, nl, psi, a, lb, beta, UU, dtv, redv, redj);
+      sd_scan<M, true>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
+    else if (nl <= SD_LCAP)
+      sd_scan<M, false>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
     else
-      sd_scan<M, false>(list, nl, psi, a, lb, beta, UU, dtv, redv, redj);
+      sd_scan<M, false>(nullptr, L, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);  // every NaN-marked rank
     __syncthreads();
     if (tid == 0) atomicAdd(&counters[direct ? 1 : 0], nl);
   }
-  // ---- Φ_i row c' in the sphere order of u_old(i), position-coalesced -----------------------------
+  SD_STAMP(8);
+  // ---- Φ_i row c' in the sphere order of u_old(i), and the U row, both 16 bytes per lane ------------
 #pragma unroll
-  for (int q = 0; q < 8; ++q) Sout[tid + T * q] = dtv[eout[q] & 0xFFFFu];
+  for (int q = 0; q < 4; ++q)
+    sd_store16<PERSIST>(Sout, L * 8, 2 * (tid + T * q), __double_as_longlong(dtv[eout[q].x & 0xFFFFu]),
+                        __double_as_longlong(dtv[eout[q].y & 0xFFFFu]));
+  {
+    const ulonglong2 t = reinterpret_cast<const ulonglong2 *>(uu)[tid];
+    *reinterpret_cast<ulonglong2 *>(UU + 8 * tid) = t;  // read by later launches only (backtrack)
+  }
+  SD_STAMP(9);
+  SD_RSTAMP(14);
+}
+
+// Rows c' = 0 and c' = B of one step, together (B >= 1; block 0 of the per-step kernel, workgroup 0 of the
+// persistent one).  Neither needs the transform:
+//  * row 0 has at most one finite source, j0 = the level at L1 distance 0 from u_old(i+1) (sphere position 0
+//    of step i+1): Φ_i[l, b̃_l] = fl(fl(T1(l) + β·d(l, j0)) + Φ_{i+1}[j0, 0]) and U = j0 for every target;
+//  * row B has at most one target, l0 = the level at distance 0 from u_old(i) (sphere position 0 of step i):
+//    Φ_i[l0, B] = min_j fl(fl(T1(l0) + β·d(l0, j)) + Φ_{i+1}[j, B]), the first minimum in rank order
+//    (HelpFunctions.jl:60-77); every other cell of row B is +Inf and unwritten.
+// `loaded` (persistent kernel): flags of rows 0 and B, stored once every read of S_{i+1} has returned.
+template <int M, bool PERSIST>
+__device__ __forceinline__ void sdt_edges(const ProblemDev &P, const LevelsDev &Lv, int k, int i, const SdPerm &pm,
+                                          const double *Sin_all,
+                                          double *Sout_all, uint16_t *__restrict__ UU_all, size_t s_stride,
+                                          size_t uu_stride_k, const int *lb_g, int32_t *__restrict__ counters,
+                                          SdtShared<(1 << (3 * M - 3)) / 64> &sh, int32_t *loaded0,
+                                          int32_t *loadedB, int token) {
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int B = P.B;
+  const double beta = Lv.beta;
+  const double *Sin = Sin_all + (size_t)k * s_stride;
+  double *S0 = Sout_all + (size_t)k * s_stride, *SB = S0 + (size_t)B * L;
+  uint16_t *U0 = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L), *UB = U0 + (size_t)B * L;
+  const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
+  const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
+  const uint2 *ein = pm.in, *eout = pm.out;
+  const uint32_t hin = pm.hin, hout = pm.hout;
+
+  // ---- loads: row B's sources (position pairs as in sdt_row) and row 0's one source ----------------------
+  const int sbytes = (B + 1) * L * (int)sizeof(double);
+  double v[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p2 = 2 * (tid + T * q);
+    const int ra = max(B - (int)(ein[q].x >> 16), 0), rb = max(B - (int)(ein[q].y >> 16), 0);
+    sd_load_pair<PERSIST>(Sin, sbytes, ra * L + p2, rb * L + p2 + 1, v[2 * q], v[2 * q + 1]);
+  }
+  const double psi0 = sd_load8<PERSIST>(Sin, sbytes, 0);  // Φ_{i+1}[j0, 0]: row 0, sphere position 0
+  double a[M];
+  int lb[M], uo[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    a[m] = P.dt * dfi[m];
+    lb[m] = lb_g[m];
+    uo[m] = (int)uoi[m];
+  }
+  auto t1_of = [&](int r) {  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
+    double t1 = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) t1 = t1 + a[m] * (double)(lb[m] + ((r >> (3 * m)) & 7));
+    return t1;
+  };
+  auto dist = [&](int r, int j) {
+    unsigned d = 0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) d = __sad((r >> (3 * m)) & 7, (j >> (3 * m)) & 7, d);
+    return d;
+  };
+
+  // ---- row B: the one target's minimum over every source ------------------------------------------
+  const int r0 = (int)(hout & 0xFFFFu);
+  const bool has0 = (hout >> 16) == 0;  // u_old(i) is a level of the table
+  const double t1b = t1_of(r0);
+  double bv = INFINITY;
+  int bj = -1;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t e = h ? ein[q].y : ein[q].x;
+      const int j = (int)(e & 0xFFFFu);
+      const double x = (int)(e >> 16) > B ? INFINITY : v[2 * q + h];
+      const double val = (t1b + beta * (double)dist(r0, j)) + x;
+      if (val < bv || (val == bv && bj >= 0 && j < bj)) {
+        bv = val;
+        bj = j;
+      }
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ov = __shfl_xor(bv, off);
+    const int oj = __shfl_xor(bj, off);
+    if (oj >= 0 && (bj < 0 || ov < bv || (ov == bv && oj < bj))) {
+      bv = ov;
+      bj = oj;
+    }
+  }
+  if (lane == 0) {
+    sh.redv[w] = bv;
+    sh.redj[w] = bj;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // psi0 too: every read of S_{i+1} has returned
+  __syncthreads();
+  if (PERSIST && tid == 0) {
+    __hip_atomic_store(loaded0, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(loadedB, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  bv = INFINITY;
+  bj = -1;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const double ov = sh.redv[q];
+    const int oj = sh.redj[q];
+    if (oj >= 0 && (bj < 0 || ov < bv || (ov == bv && oj < bj))) {
+      bv = ov;
+      bj = oj;
+    }
+  }
+  const bool wb = has0 && bj >= 0;  // the reference writes U[l0, B] (finite minimum)
+  if (has0 && tid == 0) atomicAdd(&counters[1], 1);
+
+  // ---- row 0: every target from the one source --------------------------------------------------------
+  const int j0 = (int)(hin & 0xFFFFu);
+  const bool src0 = (hin >> 16) == 0 && psi0 < INFINITY;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    double o[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t e = h ? eout[q].y : eout[q].x;
+      const int r = (int)(e & 0xFFFFu);
+      const double val = (t1_of(r) + beta * (double)dist(r, j0)) + psi0;
+      o[h] = src0 && (int)(e >> 16) <= B && val < INFINITY ? val : INFINITY;
+    }
+    sd_store16<PERSIST>(S0, L * 8, 2 * (tid + T * q), __double_as_longlong(o[0]), __double_as_longlong(o[1]));
+    const bool p0 = wb && tid == 0 && q == 0;  // row B: only sphere position 0 (= l0) can be finite
+    sd_store16<PERSIST>(SB, L * 8, 2 * (tid + T * q), p0 ? __double_as_longlong(bv) : 0x7FF0000000000000ull,
+                        0x7FF0000000000000ull);
+  }
+  // U rows in natural order: ranks 8·tid .. 8·tid + 7, one 16-byte store per row
+  unsigned short u0[8], ub[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    const int r = 8 * tid + x;
+    int bt = 0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) bt += abs(lb[m] + ((r >> (3 * m)) & 7) - uo[m]);
+    const double val = (t1_of(r) + beta * (double)dist(r, j0)) + psi0;
+    u0[x] = src0 && bt <= B && val < INFINITY ? (unsigned short)j0 : (unsigned short)0xFFFF;
+    ub[x] = wb && r == r0 ? (unsigned short)bj : (unsigned short)0xFFFF;
+  }
+  auto pack = [](const unsigned short *u, int o) {
+    return (unsigned long long)u[o] | (unsigned long long)u[o + 1] << 16 | (unsigned long long)u[o + 2] << 32 |
+           (unsigned long long)u[o + 3] << 48;
+  };
+  *reinterpret_cast<ulonglong2 *>(U0 + 8 * tid) = make_ulonglong2(pack(u0, 0), pack(u0, 4));
+  *reinterpret_cast<ulonglong2 *>(UB + 8 * tid) = make_ulonglong2(pack(ub, 0), pack(ub, 4));
+}
+
+// One launch per step: one workgroup per (source row c', subproblem k).
+template <int M>
+__global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i,
+                                                           const uint32_t *__restrict__ perm_all,
+                                                           const double *__restrict__ Sin_all,
+                                                           double *__restrict__ Sout_all,
+                                                           uint16_t *__restrict__ UU_all, size_t s_stride,
+                                                           size_t uu_stride_k, int32_t *__restrict__ counters) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
+  __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
+  SdPerm pm;
+  sd_perm_load<M>(pm, perm_all, P.nt, (int)blockIdx.y, i);
+  // B >= 1: block 0 takes rows 0 and B together, block x the row x (B workgroups, one per CU at B = 256)
+  if (blockIdx.x == 0 && P.B >= 1)
+    sdt_edges<M, false>(P, Lv, (int)blockIdx.y, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k,
+                        G.base, counters, sh, nullptr, nullptr, 0);
+  else
+    sdt_row<M, false>(P, Lv, G, (int)blockIdx.y, (int)blockIdx.x, i, pm, Sin_all, Sout_all, UU_all,
+                      s_stride, uu_stride_k, counters, sh, sds, nullptr, 0);
+  SD_FLUSH();
+}
+
+// Persistent: the whole DP in one launch.  Each subproblem's rows 0..B are split into chunks, one per resident
+// workgroup (nwg / K workgroups per subproblem, one per CU; chunks differ by at most one row; with B
+// workgroups, workgroup 0 takes rows 0 and B together).  Each
+// workgroup runs the steps i = nt-2 .. 0 and, per step, its chunk's rows in increasing c'.  Row c' of step
+// i reads rows c' - s (s <= Smax) of S_{i+1} and overwrites row c' of the staging buffer i % 3, which held
+// S_{i+3}, read by rows c' .. c' + Smax at step i+2.  So before a chunk [lo, hi) starts a step, one wave
+// polls (relaxed agent loads, s_sleep)
+//   done[k][lo - s]        >= token(i+1)   for 1 <= s <= min(lo, Smax)            (its inputs are published)
+//   loaded[k][hi - 1 + s]  >= token(i+2)   for 1 <= s <= min(B + 1 - hi, Smax)    (nobody still reads S_{i+3})
+// with token(i) = nt - 1 - i (0 = nothing yet; the terminal row comes from the previous launch); rows
+// inside the chunk are the workgroup's own, already done in order.  The least advanced workgroup can always
+// proceed (every other one has finished the steps it waits on), so with every workgroup resident there is
+// no deadlock; a wait that exceeds its spin bound sets *err and every workgroup leaves.
+template <int M>
+__global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_run(ProblemDev P, LevelsDev Lv, PyrGeom G,
+                                                          const uint32_t *__restrict__ perm_all, double *S_all,
+                                                          size_t buf_stride, uint16_t *__restrict__ UU_all,
+                                                          size_t s_stride, size_t uu_stride_k,
+                                                          int32_t *__restrict__ counters, int32_t *flags, int nwg) {
+  constexpr int Smax = 7 * M;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
+  __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
+  const int R = P.B + 1, nrows = P.K * R, tid = threadIdx.x;
+  int32_t *done = flags, *loaded = flags + nrows, *err = flags + 2 * nrows;
+  // this workgroup's chunk
+  const int W = nwg / P.K;  // workgroups per subproblem (>= 1: the host guarantees nwg >= K)
+  const int k = (int)blockIdx.x / W, wl = (int)blockIdx.x - k * W;
+  if (k >= P.K) return;
+  const int base = R / W, extra = R - base * W;
+  // the chunk: rows [lo, hi), contiguous, the longer chunks highest; with W = R - 1 (257 rows on 256 CUs)
+  // workgroup 0 takes the two rows that need no transform, 0 and B (sdt_edges), and workgroup w the row w
+  const bool edges = W == R - 1 && R >= 2 && wl == 0;
+  int lo, hi;
+  if (W == R - 1 && R >= 2) {
+    lo = edges ? 0 : wl;
+    hi = lo + 1;
+  } else {
+    lo = wl * base + max(0, wl - (W - extra));
+    hi = lo + base + (wl >= W - extra ? 1 : 0);
+  }
+  // rows whose `done` (RAW: below rlo) and `loaded` (WAR: from whi up) flags gate each step
+  const int rlo = edges ? R - 1 : lo, whi = edges ? 1 : hi;
+  if (tid == 0) sh.stop = 0;
+#pragma nounroll
+  for (int i = P.nt - 2; i >= 0; --i) {
+    const int tok = P.nt - 1 - i;
+    double *Sout = S_all + (size_t)(i % 3) * buf_stride;
+    const double *Sin = S_all + (size_t)((i + 1) % 3) * buf_stride;
+    const int g = k * R + lo;  // timeline stamps: the chunk's first row
+    (void)g;
+    SdPerm pm;  // static: in flight during the wait
+    sd_perm_load<M>(pm, perm_all, P.nt, k, i);
+    SD_TL(0);
+    if (tid < 64) {  // wave 0: dependency wait for the chunk
+      const int lane = tid;
+      const int s = lane < 32 ? lane + 1 : lane - 31;
+      int32_t *fp = nullptr;
+      int need = 0;
+      if (lane < 32 && s <= Smax && s <= rlo) {
+        fp = done + k * R + rlo - s;
+        need = tok - 1;
+      } else if (lane >= 32 && s <= Smax && whi - 1 + s < R) {
+        fp = loaded + k * R + whi - 1 + s;
+        need = tok - 2;
+      }
+      unsigned spins = 0;
+      for (;;) {
+        const bool ok = !fp || need <= 0 || __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
+        if (__all(ok)) break;
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > (1u << 24)) {
+          if (lane == 0) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh.stop = 1;
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    SD_TL(1);
+    if (sh.stop) return;
+    if (edges) {
+      sdt_edges<M, true>(P, Lv, k, i, pm, Sin, Sout, UU_all, s_stride, uu_stride_k, G.base, counters, sh,
+                         loaded + k * R, loaded + k * R + R - 1, tok);
+      SD_TL(2);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
+      __syncthreads();
+      if (tid == 0) {
+        __hip_atomic_store(done + k * R, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(done + k * R + R - 1, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      SD_TL(3);
+    }
+#pragma nounroll
+    for (int cp = lo; cp < hi && !edges; ++cp) {
+      sdt_row<M, true>(P, Lv, G, k, cp, i, pm, Sin, Sout, UU_all, s_stride, uu_stride_k, counters, sh, sds,
+                       loaded + k * R + cp, tok);
+      SD_TL(2);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(done + k * R + cp, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      SD_TL(3);
+    }
+    if (i == 0) SD_FLUSH();
+  }
 }
 
 size_t sdt_lds_bytes(const PyrGeom &G) {
   const size_t L = (size_t)1 << (3 * G.M);
-  return L * (2 * sizeof(double) + sizeof(uint16_t));
+  return L * (2 * sizeof(double) + sizeof(uint16_t)) + SD_LCAP * sizeof(uint16_t);
 }
 
 bool sdt_supported(const PyrGeom &G) {
@@ -378,11 +886,31 @@ bool sdt_supported(const PyrGeom &G) {
   return true;
 }
 
+hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
+                          const uint32_t *perm, double *S, size_t buf_stride, uint16_t *UU, size_t s_stride,
+                          size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, size_t lds) {
+  if (!sdt_supported(G)) return hipErrorInvalidValue;
+  if (G.M == 4)
+    hipLaunchKernelGGL(k_sdt_run<4>, dim3(nwg), dim3(512), lds, s, P, Lv, G, perm, S, buf_stride, UU, s_stride,
+                       uu_stride_k, counters, flags, nwg);
+  else
+    hipLaunchKernelGGL(k_sdt_run<3>, dim3(nwg), dim3(64), lds, s, P, Lv, G, perm, S, buf_stride, UU, s_stride,
+                       uu_stride_k, counters, flags, nwg);
+  return hipGetLastError();
+}
+
+int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds) {
+  int n = 0;
+  hipError_t e = G.M == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_sdt_run<4>, 512, lds)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_sdt_run<3>, 64, lds);
+  return e == hipSuccess ? n : 0;
+}
+
 hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
                            const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
                            size_t uu_stride_k, int32_t *counters) {
   if (!sdt_supported(G)) return hipErrorInvalidValue;
-  const dim3 grid(P.B + 1, P.K);
+  const dim3 grid(P.B >= 1 ? P.B : 1, P.K);  // rows 0 and B share block 0
   const size_t lds = sdt_lds_bytes(G);
   if (G.M == 4)
     hipLaunchKernelGGL(k_sdt_step<4>, grid, dim3(512), lds, s, P, Lv, G, i, perm, Sin, Sout, UU, s_stride,
@@ -392,5 +920,21 @@ hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
                        uu_stride_k, counters);
   return hipGetLastError();
 }
+
+#if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
+extern "C" int32_t mioc_debug_sdt_timeline(unsigned long long *out, int64_t nrows) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sdt_tl), (size_t)nrows * 64 * 4 * sizeof(unsigned long long)) ==
+                 hipSuccess
+             ? 0
+             : -4;
+}
+#elif defined(MIOC_STAMPS)
+extern "C" int32_t mioc_debug_sdt_stamps(unsigned long long *out, int64_t nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sdt_stamps), (size_t)nblocks * 16 * sizeof(unsigned long long)) ==
+                 hipSuccess
+             ? 0
+             : -4;
+}
+#endif
 
 }  // namespace mioc

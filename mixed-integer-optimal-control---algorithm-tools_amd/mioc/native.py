@@ -26,7 +26,7 @@ MIOC_ESTATE = -6
 MIOC_ENONFINITE = -7
 
 MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
-MIOC_OPT_ALGO, MIOC_OPT_TIMING = 1, 2
+MIOC_OPT_ALGO, MIOC_OPT_TIMING, MIOC_OPT_PERSIST = 1, 2, 3
 MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID, MIOC_ALGO_SEPARABLE = 0, 1, 2, 3, 4
 
 EXPORTED = [
