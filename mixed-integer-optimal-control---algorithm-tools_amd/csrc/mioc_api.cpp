@@ -244,10 +244,9 @@ int run_bellman(mioc_ctx *ctx) {
 
   if (algo == MIOC_ALGO_PYRAMID || algo == MIOC_ALGO_SEPARABLE) {
     const size_t s_stride = (size_t)(ctx->B + 1) * L;
-    // persistent separable transform: every workgroup resident (rows dealt round-robin over at most
-    // blocks-per-CU x CUs workgroups), three staging buffers
-    // one workgroup per CU (its register file allows no second one); the row left over by B+1 > CUs is the
-    // cheapest pair (c' = 0: one finite source; c' = B: one target)
+    // persistent separable transform: every workgroup resident, one per CU (96 KB of LDS keeps a second one
+    // off the CU: its register file would not hold it), kSdtBuffers staging buffers; B + 1 rows on B
+    // workgroups, workgroup 0 taking rows 0 and B (k_sdt_run)
     const size_t run_lds = std::max<size_t>(sdt_lds_bytes(ctx->pyr), 96 * 1024);
     int nwg = 0;
     bool persist = false;
@@ -269,7 +268,7 @@ int run_bellman(mioc_ctx *ctx) {
       if (!ctx->h_run_err) HIP_TRY(ctx, hipHostMalloc(&ctx->h_run_err, 16, 0));
       *ctx->h_run_err = 0;
     }
-    const int nbuf = persist ? 3 : 2;
+    const int nbuf = persist ? kSdtBuffers : 2;
     int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, nbuf * K * s_stride * sizeof(double), "staging fronts");
     if (rc) return rc;
     const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
@@ -278,7 +277,7 @@ int run_bellman(mioc_ctx *ctx) {
     rc = grow(ctx, &ctx->d_perm, &ctx->perm_cap, K * nt * L * sizeof(uint32_t), "sphere orders");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
-    double *term = persist ? ctx->d_stage + ((nt - 1) % 3) * K * s_stride : st[(nt - 1) & 1];
+    double *term = persist ? ctx->d_stage + ((nt - 1) % kSdtBuffers) * K * s_stride : st[(nt - 1) & 1];
     HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm));
     HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, term, s_stride));
     if (algo == MIOC_ALGO_SEPARABLE && persist) {

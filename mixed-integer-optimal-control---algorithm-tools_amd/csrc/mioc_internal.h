@@ -91,6 +91,7 @@ size_t pyr_lds_bytes(const PyrGeom &G);
 // separable L1 transform (mioc_sdt.hip): same staging layout, 8^M grids (M = 3, 4), beta > 0
 bool sdt_supported(const PyrGeom &G);
 size_t sdt_lds_bytes(const PyrGeom &G);
+constexpr int kSdtBuffers = 4;  // persistent separable transform: staging buffers S_i, step i in buffer i % 4
 hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
                            const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
                            size_t uu_stride_k, int32_t *counters);

@@ -44,6 +44,7 @@ constexpr int SD_COOP = 8;               // listed targets up to this many: whol
 constexpr int SD_FEW = 4;                // rows with at most this many targets go straight to the exact scan
 constexpr int SD_SPARSE = 4;             // rows with at most this many finite sources: direct minimum over them
 constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, the scan sweeps every rank
+constexpr int SD_BLAG = 2;               // persistent kernel: row B runs this many steps behind row 0
 
 // Diagnostic build only (make stamps -> libmioc_stamps.so): per-workgroup phase clocks of the last launch.
 #if defined(MIOC_STAMPS) && !defined(MIOC_STAMPS_TL)
@@ -72,7 +73,7 @@ __device__ unsigned long long g_sdt_stamps[4096][16];
 __device__ unsigned long long g_sdt_tl[4096][64][4];
 #define SD_TL(k)                                                                                          \
   do {                                                                                                    \
-    if (threadIdx.x == 0 && g < 4096 && i < 64) g_sdt_tl[g][i][k] = __builtin_amdgcn_s_memrealtime();    \
+    if (threadIdx.x == 0 && g < 4096 && (unsigned)i < 64u) g_sdt_tl[g][i][k] = __builtin_amdgcn_s_memrealtime();    \
   } while (0)
 #define SD_STAMP(k) \
   do {              \
@@ -482,16 +483,13 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
         pos[x] = sd_swz(sd_rank(tid, m, x));
         o[x] = dtv[pos[x]];
       }
-      double lf[8], rb[8];
-      lf[0] = o[0];
+      // in place: after the forward sweep o[x] covers the sources at <= x; a backward merge of o[x] with
+      // o[x+1] + 1 compares a source at <= x with itself shifted by >= 2, never within tol, so every
+      // flagged tie is between two distinct sources (as in a merge of disjoint sets)
 #pragma unroll
-      for (int x = 1; x < 8; ++x) lf[x] = sd_merge(o[x], lf[x - 1] + 1.0, tol);
-      rb[7] = o[7];
+      for (int x = 1; x < 8; ++x) o[x] = sd_merge(o[x], o[x - 1] + 1.0, tol);
 #pragma unroll
-      for (int x = 6; x >= 1; --x) rb[x] = sd_merge(o[x], rb[x + 1] + 1.0, tol);
-      o[7] = lf[7];
-#pragma unroll
-      for (int x = 0; x < 7; ++x) o[x] = sd_merge(lf[x], rb[x + 1] + 1.0, tol);
+      for (int x = 6; x >= 0; --x) o[x] = sd_merge(o[x], o[x + 1] + 1.0, tol);
       if (m + 1 < M) {
 #pragma unroll
         for (int x = 0; x < 8; ++x) dtv[pos[x]] = o[x];
@@ -596,78 +594,130 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
   SD_RSTAMP(14);
 }
 
-// Rows c' = 0 and c' = B of one step, together (B >= 1; block 0 of the per-step kernel, workgroup 0 of the
-// persistent one).  Neither needs the transform:
+// The two rows that need no transform (B >= 1):
 //  * row 0 has at most one finite source, j0 = the level at L1 distance 0 from u_old(i+1) (sphere position 0
 //    of step i+1): Φ_i[l, b̃_l] = fl(fl(T1(l) + β·d(l, j0)) + Φ_{i+1}[j0, 0]) and U = j0 for every target;
 //  * row B has at most one target, l0 = the level at distance 0 from u_old(i) (sphere position 0 of step i):
 //    Φ_i[l0, B] = min_j fl(fl(T1(l0) + β·d(l0, j)) + Φ_{i+1}[j, B]), the first minimum in rank order
 //    (HelpFunctions.jl:60-77); every other cell of row B is +Inf and unwritten.
-// `loaded` (persistent kernel): flags of rows 0 and B, stored once every read of S_{i+1} has returned.
+// Both run in one workgroup (block 0 of the per-step kernel, workgroup 0 of the persistent one, which runs
+// row B a few steps behind row 0).  `loaded` (persistent kernel): the row's flag, stored once every read of
+// S_{i+1} has returned.
+template <int M>
+struct SdEdge {
+  double a[M];
+  int lb[M], uo[M];
+  __device__ __forceinline__ SdEdge(const ProblemDev &P, const int *lb_g, int k, int i) {
+    const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
+    const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      a[m] = P.dt * dfi[m];
+      lb[m] = lb_g[m];
+      uo[m] = (int)uoi[m];
+    }
+  }
+  __device__ __forceinline__ double t1(int r) const {  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
+    double t = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) t = t + a[m] * (double)(lb[m] + ((r >> (3 * m)) & 7));
+    return t;
+  }
+  __device__ __forceinline__ int bt(int r) const {  // b̃_r(i) = Σ_m |ν_rm - u_old[m, i]|
+    int b = 0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) b += abs(lb[m] + ((r >> (3 * m)) & 7) - uo[m]);
+    return b;
+  }
+  static __device__ __forceinline__ unsigned dist(int r, int j) {
+    unsigned d = 0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) d = __sad((r >> (3 * m)) & 7, (j >> (3 * m)) & 7, d);
+    return d;
+  }
+};
+__device__ __forceinline__ unsigned long long sd_pack4(const unsigned short *u) {
+  return (unsigned long long)u[0] | (unsigned long long)u[1] << 16 | (unsigned long long)u[2] << 32 |
+         (unsigned long long)u[3] << 48;
+}
+
 template <int M, bool PERSIST>
-__device__ __forceinline__ void sdt_edges(const ProblemDev &P, const LevelsDev &Lv, int k, int i, const SdPerm &pm,
-                                          const double *Sin_all,
-                                          double *Sout_all, uint16_t *__restrict__ UU_all, size_t s_stride,
-                                          size_t uu_stride_k, const int *lb_g, int32_t *__restrict__ counters,
-                                          SdtShared<(1 << (3 * M - 3)) / 64> &sh, int32_t *loaded0,
-                                          int32_t *loadedB, int token) {
-  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int B = P.B;
+__device__ __forceinline__ void sdt_row0(const ProblemDev &P, const LevelsDev &Lv, int k, int i, const SdPerm &pm,
+                                         const double *Sin_all, double *Sout_all, uint16_t *__restrict__ UU_all,
+                                         size_t s_stride, size_t uu_stride_k, const int *lb_g, int32_t *loaded,
+                                         int token) {
+  constexpr int L = 1 << (3 * M), T = L / 8;
+  const int tid = threadIdx.x, B = P.B;
   const double beta = Lv.beta;
   const double *Sin = Sin_all + (size_t)k * s_stride;
-  double *S0 = Sout_all + (size_t)k * s_stride, *SB = S0 + (size_t)B * L;
-  uint16_t *U0 = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L), *UB = U0 + (size_t)B * L;
-  const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
-  const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
-  const uint2 *ein = pm.in, *eout = pm.out;
-  const uint32_t hin = pm.hin, hout = pm.hout;
+  double *S0 = Sout_all + (size_t)k * s_stride;
+  uint16_t *U0 = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L);
+  const double psi0 = sd_load8<PERSIST>(Sin, (B + 1) * L * (int)sizeof(double), 0);  // Φ_{i+1}[j0, 0]
+  const SdEdge<M> E(P, lb_g, k, i);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's read of S_{i+1} has returned
+  if (PERSIST && tid == 0) __hip_atomic_store(loaded, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int j0 = (int)(pm.hin & 0xFFFFu);
+  const bool src0 = (pm.hin >> 16) == 0 && psi0 < INFINITY;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    double o[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t e = h ? pm.out[q].y : pm.out[q].x;
+      const int r = (int)(e & 0xFFFFu);
+      const double val = (E.t1(r) + beta * (double)SdEdge<M>::dist(r, j0)) + psi0;
+      o[h] = src0 && (int)(e >> 16) <= B && val < INFINITY ? val : INFINITY;
+    }
+    sd_store16<PERSIST>(S0, L * 8, 2 * (tid + T * q), __double_as_longlong(o[0]), __double_as_longlong(o[1]));
+  }
+  // U row in natural order: ranks 8·tid .. 8·tid + 7, one 16-byte store
+  unsigned short u0[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    const int r = 8 * tid + x;
+    const double val = (E.t1(r) + beta * (double)SdEdge<M>::dist(r, j0)) + psi0;
+    u0[x] = src0 && E.bt(r) <= B && val < INFINITY ? (unsigned short)j0 : (unsigned short)0xFFFF;
+  }
+  *reinterpret_cast<ulonglong2 *>(U0 + 8 * tid) = make_ulonglong2(sd_pack4(u0), sd_pack4(u0 + 4));
+}
 
-  // ---- loads: row B's sources (position pairs as in sdt_row) and row 0's one source ----------------------
+template <int M, bool PERSIST>
+__device__ __forceinline__ void sdt_rowB(const ProblemDev &P, const LevelsDev &Lv, int k, int i, const SdPerm &pm,
+                                         const double *Sin_all, double *Sout_all, uint16_t *__restrict__ UU_all,
+                                         size_t s_stride, size_t uu_stride_k, const int *lb_g,
+                                         int32_t *__restrict__ counters, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
+                                         int32_t *loaded, int token) {
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, B = P.B;
+  const double beta = Lv.beta;
+  const double *Sin = Sin_all + (size_t)k * s_stride;
+  double *SB = Sout_all + (size_t)k * s_stride + (size_t)B * L;
+  uint16_t *UB = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L) + (size_t)B * L;
+  // ---- every source: Ψ_j = S_{i+1}[B - b̃_j(i+1)][pos(j)] (position pairs as in sdt_row) ------------------
   const int sbytes = (B + 1) * L * (int)sizeof(double);
   double v[8];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int p2 = 2 * (tid + T * q);
-    const int ra = max(B - (int)(ein[q].x >> 16), 0), rb = max(B - (int)(ein[q].y >> 16), 0);
+    const int ra = max(B - (int)(pm.in[q].x >> 16), 0), rb = max(B - (int)(pm.in[q].y >> 16), 0);
     sd_load_pair<PERSIST>(Sin, sbytes, ra * L + p2, rb * L + p2 + 1, v[2 * q], v[2 * q + 1]);
   }
-  const double psi0 = sd_load8<PERSIST>(Sin, sbytes, 0);  // Φ_{i+1}[j0, 0]: row 0, sphere position 0
-  double a[M];
-  int lb[M], uo[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    a[m] = P.dt * dfi[m];
-    lb[m] = lb_g[m];
-    uo[m] = (int)uoi[m];
-  }
-  auto t1_of = [&](int r) {  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
-    double t1 = 0.0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) t1 = t1 + a[m] * (double)(lb[m] + ((r >> (3 * m)) & 7));
-    return t1;
-  };
-  auto dist = [&](int r, int j) {
-    unsigned d = 0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) d = __sad((r >> (3 * m)) & 7, (j >> (3 * m)) & 7, d);
-    return d;
-  };
-
-  // ---- row B: the one target's minimum over every source ------------------------------------------
-  const int r0 = (int)(hout & 0xFFFFu);
-  const bool has0 = (hout >> 16) == 0;  // u_old(i) is a level of the table
-  const double t1b = t1_of(r0);
+  const SdEdge<M> E(P, lb_g, k, i);
+  // ---- the one target's minimum over every source ------------------------------------------------------
+  const int r0 = (int)(pm.hout & 0xFFFFu);
+  const bool has0 = (pm.hout >> 16) == 0;  // u_old(i) is a level of the table
+  const double t1b = E.t1(r0);
   double bv = INFINITY;
   int bj = -1;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const uint32_t e = h ? ein[q].y : ein[q].x;
+      const uint32_t e = h ? pm.in[q].y : pm.in[q].x;
       const int j = (int)(e & 0xFFFFu);
       const double x = (int)(e >> 16) > B ? INFINITY : v[2 * q + h];
-      const double val = (t1b + beta * (double)dist(r0, j)) + x;
+      const double val = (t1b + beta * (double)SdEdge<M>::dist(r0, j)) + x;
       if (val < bv || (val == bv && bj >= 0 && j < bj)) {
         bv = val;
         bj = j;
@@ -686,12 +736,8 @@ __device__ __forceinline__ void sdt_edges(const ProblemDev &P, const LevelsDev &
     sh.redv[w] = bv;
     sh.redj[w] = bj;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // psi0 too: every read of S_{i+1} has returned
-  __syncthreads();
-  if (PERSIST && tid == 0) {
-    __hip_atomic_store(loaded0, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(loadedB, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  __syncthreads();  // every read of S_{i+1} has returned (its values are consumed above)
+  if (PERSIST && tid == 0) __hip_atomic_store(loaded, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   bv = INFINITY;
   bj = -1;
 #pragma unroll
@@ -703,45 +749,19 @@ __device__ __forceinline__ void sdt_edges(const ProblemDev &P, const LevelsDev &
       bj = oj;
     }
   }
+  __syncthreads();  // sh.redv / redj are free again
   const bool wb = has0 && bj >= 0;  // the reference writes U[l0, B] (finite minimum)
   if (has0 && tid == 0) atomicAdd(&counters[1], 1);
-
-  // ---- row 0: every target from the one source --------------------------------------------------------
-  const int j0 = (int)(hin & 0xFFFFu);
-  const bool src0 = (hin >> 16) == 0 && psi0 < INFINITY;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    double o[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t e = h ? eout[q].y : eout[q].x;
-      const int r = (int)(e & 0xFFFFu);
-      const double val = (t1_of(r) + beta * (double)dist(r, j0)) + psi0;
-      o[h] = src0 && (int)(e >> 16) <= B && val < INFINITY ? val : INFINITY;
-    }
-    sd_store16<PERSIST>(S0, L * 8, 2 * (tid + T * q), __double_as_longlong(o[0]), __double_as_longlong(o[1]));
-    const bool p0 = wb && tid == 0 && q == 0;  // row B: only sphere position 0 (= l0) can be finite
+    const bool p0 = wb && tid == 0 && q == 0;  // only sphere position 0 (= l0) can be finite
     sd_store16<PERSIST>(SB, L * 8, 2 * (tid + T * q), p0 ? __double_as_longlong(bv) : 0x7FF0000000000000ull,
                         0x7FF0000000000000ull);
   }
-  // U rows in natural order: ranks 8·tid .. 8·tid + 7, one 16-byte store per row
-  unsigned short u0[8], ub[8];
+  unsigned short ub[8];
 #pragma unroll
-  for (int x = 0; x < 8; ++x) {
-    const int r = 8 * tid + x;
-    int bt = 0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) bt += abs(lb[m] + ((r >> (3 * m)) & 7) - uo[m]);
-    const double val = (t1_of(r) + beta * (double)dist(r, j0)) + psi0;
-    u0[x] = src0 && bt <= B && val < INFINITY ? (unsigned short)j0 : (unsigned short)0xFFFF;
-    ub[x] = wb && r == r0 ? (unsigned short)bj : (unsigned short)0xFFFF;
-  }
-  auto pack = [](const unsigned short *u, int o) {
-    return (unsigned long long)u[o] | (unsigned long long)u[o + 1] << 16 | (unsigned long long)u[o + 2] << 32 |
-           (unsigned long long)u[o + 3] << 48;
-  };
-  *reinterpret_cast<ulonglong2 *>(U0 + 8 * tid) = make_ulonglong2(pack(u0, 0), pack(u0, 4));
-  *reinterpret_cast<ulonglong2 *>(UB + 8 * tid) = make_ulonglong2(pack(ub, 0), pack(ub, 4));
+  for (int x = 0; x < 8; ++x) ub[x] = wb && 8 * tid + x == r0 ? (unsigned short)bj : (unsigned short)0xFFFF;
+  *reinterpret_cast<ulonglong2 *>(UB + 8 * tid) = make_ulonglong2(sd_pack4(ub), sd_pack4(ub + 4));
 }
 
 // One launch per step: one workgroup per (source row c', subproblem k).
@@ -757,35 +777,42 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
   SdPerm pm;
   sd_perm_load<M>(pm, perm_all, P.nt, (int)blockIdx.y, i);
   // B >= 1: block 0 takes rows 0 and B together, block x the row x (B workgroups, one per CU at B = 256)
-  if (blockIdx.x == 0 && P.B >= 1)
-    sdt_edges<M, false>(P, Lv, (int)blockIdx.y, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k,
-                        G.base, counters, sh, nullptr, nullptr, 0);
-  else
+  if (blockIdx.x == 0 && P.B >= 1) {
+    sdt_row0<M, false>(P, Lv, (int)blockIdx.y, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k, G.base,
+                       nullptr, 0);
+    sdt_rowB<M, false>(P, Lv, (int)blockIdx.y, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k, G.base,
+                       counters, sh, nullptr, 0);
+  } else
     sdt_row<M, false>(P, Lv, G, (int)blockIdx.y, (int)blockIdx.x, i, pm, Sin_all, Sout_all, UU_all,
                       s_stride, uu_stride_k, counters, sh, sds, nullptr, 0);
   SD_FLUSH();
 }
 
 // Persistent: the whole DP in one launch.  Each subproblem's rows 0..B are split into chunks, one per resident
-// workgroup (nwg / K workgroups per subproblem, one per CU; chunks differ by at most one row; with B
-// workgroups, workgroup 0 takes rows 0 and B together).  Each
-// workgroup runs the steps i = nt-2 .. 0 and, per step, its chunk's rows in increasing c'.  Row c' of step
-// i reads rows c' - s (s <= Smax) of S_{i+1} and overwrites row c' of the staging buffer i % 3, which held
-// S_{i+3}, read by rows c' .. c' + Smax at step i+2.  So before a chunk [lo, hi) starts a step, one wave
-// polls (relaxed agent loads, s_sleep)
-//   done[k][lo - s]        >= token(i+1)   for 1 <= s <= min(lo, Smax)            (its inputs are published)
-//   loaded[k][hi - 1 + s]  >= token(i+2)   for 1 <= s <= min(B + 1 - hi, Smax)    (nobody still reads S_{i+3})
-// with token(i) = nt - 1 - i (0 = nothing yet; the terminal row comes from the previous launch); rows
-// inside the chunk are the workgroup's own, already done in order.  The least advanced workgroup can always
-// proceed (every other one has finished the steps it waits on), so with every workgroup resident there is
-// no deadlock; a wait that exceeds its spin bound sets *err and every workgroup leaves.
+// workgroup (nwg / K workgroups per subproblem, one per CU; chunks differ by at most one row).  With W = B
+// workgroups (257 rows on 256 CUs), workgroup w >= 1 takes row w and workgroup 0 the two rows that need no
+// transform: row 0 of step i and row B of step i + SD_BLAG.  Row B lags because it reads rows B - Smax .. B
+// of the step before: run in lockstep with row 0 it would close a dependency cycle through every row
+// (row 0 -> row 1 -> ... -> row B -> row 0 of the next step) and hold the whole DP to the hand-off latency
+// of every step; a lag of SD_BLAG steps leaves each row bound by its own body.
+//
+// Row c' of step i reads rows c' - s (s <= Smax) of S_{i+1} and overwrites row c' of the staging buffer
+// i % NB, which held S_{i+NB}, read by rows c' .. c' + Smax at step i+NB-1.  So before a chunk [lo, hi)
+// starts a step, one wave polls (relaxed agent loads, s_sleep)
+//   done[k][lo - s]        >= token(i+1)      for 1 <= s <= min(lo, Smax)           (its inputs are published)
+//   loaded[k][hi - 1 + s]  >= token(i+NB-1)   for 1 <= s <= min(B + 1 - hi, Smax)   (nobody still reads S_{i+NB})
+// with token(i) = nt - 1 - i (0 = nothing yet; the terminal row comes from the previous launch); rows inside
+// the chunk are the workgroup's own, already done in order.  Every wait points at a strictly earlier item in
+// the order (step descending, row ascending; workgroup 0's iteration i between steps i + 1 and i), so with
+// every workgroup resident there is no deadlock; a wait that exceeds its spin bound sets *err and every
+// workgroup leaves.
 template <int M>
 __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_run(ProblemDev P, LevelsDev Lv, PyrGeom G,
                                                           const uint32_t *__restrict__ perm_all, double *S_all,
                                                           size_t buf_stride, uint16_t *__restrict__ UU_all,
                                                           size_t s_stride, size_t uu_stride_k,
                                                           int32_t *__restrict__ counters, int32_t *flags, int nwg) {
-  constexpr int Smax = 7 * M;
+  constexpr int Smax = 7 * M, NB = kSdtBuffers;
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
   const int R = P.B + 1, nrows = P.K * R, tid = threadIdx.x;
@@ -795,41 +822,43 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_run(ProblemDev P, Leve
   const int k = (int)blockIdx.x / W, wl = (int)blockIdx.x - k * W;
   if (k >= P.K) return;
   const int base = R / W, extra = R - base * W;
-  // the chunk: rows [lo, hi), contiguous, the longer chunks highest; with W = R - 1 (257 rows on 256 CUs)
-  // workgroup 0 takes the two rows that need no transform, 0 and B (sdt_edges), and workgroup w the row w
-  const bool edges = W == R - 1 && R >= 2 && wl == 0;
-  int lo, hi;
-  if (W == R - 1 && R >= 2) {
-    lo = edges ? 0 : wl;
+  const bool split = W == R - 1 && R >= 2, edges = split && wl == 0;
+  int lo, hi;  // rows [lo, hi), contiguous, the longer chunks highest
+  if (split) {
+    lo = wl;
     hi = lo + 1;
   } else {
     lo = wl * base + max(0, wl - (W - extra));
     hi = lo + base + (wl >= W - extra ? 1 : 0);
   }
-  // rows whose `done` (RAW: below rlo) and `loaded` (WAR: from whi up) flags gate each step
-  const int rlo = edges ? R - 1 : lo, whi = edges ? 1 : hi;
   if (tid == 0) sh.stop = 0;
+  auto tok_of = [&](int step) { return P.nt - 1 - step; };
+  auto buf = [&](int step) { return S_all + (size_t)(step % NB) * buf_stride; };
 #pragma nounroll
-  for (int i = P.nt - 2; i >= 0; --i) {
-    const int tok = P.nt - 1 - i;
-    double *Sout = S_all + (size_t)(i % 3) * buf_stride;
-    const double *Sin = S_all + (size_t)((i + 1) % 3) * buf_stride;
+  for (int i = P.nt - 2; i >= (edges ? -SD_BLAG : 0); --i) {
+    const int iB = i + SD_BLAG;                   // workgroup 0: the step of its row B
+    const bool do0 = i >= 0, doB = edges && iB <= P.nt - 2;
     const int g = k * R + lo;  // timeline stamps: the chunk's first row
     (void)g;
-    SdPerm pm;  // static: in flight during the wait
-    sd_perm_load<M>(pm, perm_all, P.nt, k, i);
+    SdPerm pm, pmB;  // static: in flight during the wait
+    if (do0) sd_perm_load<M>(pm, perm_all, P.nt, k, i);
+    if (doB) sd_perm_load<M>(pmB, perm_all, P.nt, k, iB);
     SD_TL(0);
-    if (tid < 64) {  // wave 0: dependency wait for the chunk
+    if (tid < 64) {  // wave 0: dependency wait
       const int lane = tid;
       const int s = lane < 32 ? lane + 1 : lane - 31;
       int32_t *fp = nullptr;
       int need = 0;
-      if (lane < 32 && s <= Smax && s <= rlo) {
+      // RAW: inputs of row lo at step i (workgroup 0: of row B at step iB)
+      const int rlo = edges ? R - 1 : lo, sraw = edges ? iB : i;
+      // WAR: readers of the buffer row lo .. hi-1 overwrites at step i (workgroup 0: row 0 at step i)
+      const int whi = edges ? 1 : hi;
+      if (lane < 32 && s <= Smax && s <= rlo && (!edges || doB)) {
         fp = done + k * R + rlo - s;
-        need = tok - 1;
-      } else if (lane >= 32 && s <= Smax && whi - 1 + s < R) {
+        need = tok_of(sraw + 1);
+      } else if (lane >= 32 && s <= Smax && whi - 1 + s < R && do0) {
         fp = loaded + k * R + whi - 1 + s;
-        need = tok - 2;
+        need = tok_of(i + NB - 1);
       }
       unsigned spins = 0;
       for (;;) {
@@ -849,25 +878,29 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_run(ProblemDev P, Leve
     SD_TL(1);
     if (sh.stop) return;
     if (edges) {
-      sdt_edges<M, true>(P, Lv, k, i, pm, Sin, Sout, UU_all, s_stride, uu_stride_k, G.base, counters, sh,
-                         loaded + k * R, loaded + k * R + R - 1, tok);
+      if (do0)
+        sdt_row0<M, true>(P, Lv, k, i, pm, buf(i + 1), buf(i), UU_all, s_stride, uu_stride_k, G.base,
+                          loaded + k * R, tok_of(i));
+      if (doB)
+        sdt_rowB<M, true>(P, Lv, k, iB, pmB, buf(iB + 1), buf(iB), UU_all, s_stride, uu_stride_k, G.base,
+                          counters, sh, loaded + k * R + R - 1, tok_of(iB));
       SD_TL(2);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
       __syncthreads();
       if (tid == 0) {
-        __hip_atomic_store(done + k * R, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(done + k * R + R - 1, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (do0) __hip_atomic_store(done + k * R, tok_of(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (doB) __hip_atomic_store(done + k * R + R - 1, tok_of(iB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       SD_TL(3);
     }
 #pragma nounroll
     for (int cp = lo; cp < hi && !edges; ++cp) {
-      sdt_row<M, true>(P, Lv, G, k, cp, i, pm, Sin, Sout, UU_all, s_stride, uu_stride_k, counters, sh, sds,
-                       loaded + k * R + cp, tok);
+      sdt_row<M, true>(P, Lv, G, k, cp, i, pm, buf(i + 1), buf(i), UU_all, s_stride, uu_stride_k, counters, sh,
+                       sds, loaded + k * R + cp, tok_of(i));
       SD_TL(2);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(done + k * R + cp, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_store(done + k * R + cp, tok_of(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       SD_TL(3);
     }
     if (i == 0) SD_FLUSH();
