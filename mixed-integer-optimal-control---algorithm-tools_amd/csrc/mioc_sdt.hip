@@ -125,6 +125,12 @@ __device__ __forceinline__ int sd_rank(int q, int m, int x) {
   return lo | (x << (3 * m)) | ((q >> (3 * m)) << (3 * (m + 1)));
 }
 
+// L1 distance between two ranks of the 8^M grid with one v_sad_u8: a rank spread to one byte per dimension
+__device__ __forceinline__ unsigned sd_bytes(unsigned r) {
+  return (r & 7u) | ((r & 0x38u) << 5) | ((r & 0x1C0u) << 10) | ((r & 0xE00u) << 15);
+}
+__device__ __forceinline__ unsigned sd_l1(unsigned pa, unsigned pb) { return __builtin_amdgcn_sad_u8(pa, pb, 0u); }
+
 // Exact scan of the listed targets: the reference loop (HelpFunctions.jl:60-77) for one cell each.
 // COOP: the whole workgroup scans one target at a time (thread t: sources t + T·s, ascending), then a
 // (value, rank) minimum, ties to the lower rank.  Otherwise one wave per target (lane: sources
@@ -161,15 +167,13 @@ __device__ __forceinline__ void sd_scan(const uint16_t *list, int nl, const doub
       const int r = list[e];
       int xl[M];
       const double t1 = target(r, xl);
-      unsigned dpre = 0;
-#pragma unroll
-      for (int m = 0; m < M - 1; ++m) dpre = __sad((tid >> (3 * m)) & 7, xl[m], dpre);
+      const unsigned dpre = sd_l1(sd_bytes(tid), sd_bytes(r & ((1 << (3 * (M - 1))) - 1)));
       double bv = INFINITY;
       int bj = -1;
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const int j = tid + T * s;
-        const double val = (t1 + beta * (double)__sad(s, xl[M - 1], dpre)) + psi[j];
+        const double val = (t1 + beta * (double)(dpre + (unsigned)abs(s - xl[M - 1]))) + psi[j];
         if (val < bv) {
           bv = val;
           bj = j;
@@ -203,13 +207,12 @@ __device__ __forceinline__ void sd_scan(const uint16_t *list, int nl, const doub
       if (!list && !__builtin_isnan(outnat[r])) continue;  // overflowed list: every NaN-marked rank
       int xl[M];
       const double t1 = target(r, xl);
+      const unsigned pr = sd_bytes(r);
       double bv = INFINITY;
       int bj = -1;
       for (int t = 0; t < L / 64; ++t) {
         const int j = lane + 64 * t;
-        unsigned d = 0;
-#pragma unroll
-        for (int m = 0; m < M; ++m) d = __sad((j >> (3 * m)) & 7, xl[m], d);
+        const unsigned d = sd_l1(sd_bytes(j), pr);
         const double val = (t1 + beta * (double)d) + psi[j];
         if (val < bv) {
           bv = val;
@@ -370,6 +373,7 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
     pre = pre + a[m] * (double)nu;  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
     bpre += abs(nu - uo[m]);
   }
+  const unsigned ptid = sd_bytes((unsigned)tid);  // the thread's first M-1 coordinates, one byte each
   unsigned valid = 0;  // target inside the trust region: c' + b̃_l(i) <= B
 #pragma unroll
   for (int x = 0; x < 8; ++x) valid |= (unsigned)(bpre + abs(lb[M - 1] + x - uo[M - 1]) <= B - cp) << x;
@@ -514,9 +518,7 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
       const int r = tid | (x << (3 * (M - 1))), j = jx[x];
       const bool fin = (valid >> x & 1) && o[x] < INFINITY;
       const bool flg = (__double2loint(o[x]) & SD_FLAG) != 0;
-      unsigned d = __sad(x, (j >> (3 * (M - 1))) & 7, 0u);
-#pragma unroll
-      for (int m = 0; m < M - 1; ++m) d = __sad((j >> (3 * m)) & 7, xt[m], d);
+      const unsigned d = sd_l1(sd_bytes(j), ptid | (unsigned)x << (8 * (M - 1)));
       const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
       const double val = (t1 + beta * (double)d) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
       listed |= (unsigned)(fin && flg) << x;
@@ -540,9 +542,7 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
           for (int e = 0; e < SD_SPARSE; ++e) {
             if (e < nf) {
               const int j = spj[e];
-              unsigned d = __sad(x, (j >> (3 * (M - 1))) & 7, 0u);
-#pragma unroll
-              for (int m = 0; m < M - 1; ++m) d = __sad((j >> (3 * m)) & 7, xt[m], d);
+              const unsigned d = sd_l1(sd_bytes(j), ptid | (unsigned)x << (8 * (M - 1)));
               const double val = (t1 + beta * (double)d) + spv[e];
               if (val < bv || (val == bv && j < bj)) {
                 bv = val;
@@ -629,12 +629,7 @@ struct SdEdge {
     for (int m = 0; m < M; ++m) b += abs(lb[m] + ((r >> (3 * m)) & 7) - uo[m]);
     return b;
   }
-  static __device__ __forceinline__ unsigned dist(int r, int j) {
-    unsigned d = 0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) d = __sad((r >> (3 * m)) & 7, (j >> (3 * m)) & 7, d);
-    return d;
-  }
+  static __device__ __forceinline__ unsigned dist(int r, int j) { return sd_l1(sd_bytes(r), sd_bytes(j)); }
 };
 __device__ __forceinline__ unsigned long long sd_pack4(const unsigned short *u) {
   return (unsigned long long)u[0] | (unsigned long long)u[1] << 16 | (unsigned long long)u[2] << 32 |
