@@ -20,5 +20,5 @@ for nt in [int(x) for x in sys.argv[1:]]:
         wall = time.perf_counter() - t0
         ms, n, name = ctx.kernel_stats(0)
         u, phi, _ = ctx.backtrack(cfg.B)
-        print(f"nt={nt} {name}: events {ms:.3f} ms ({1e3 * ms / (nt - 1):.2f} us/step), wall {1e3 * wall:.3f} ms, phi={phi!r}", flush=True)
+        print(f"nt={nt} {name}: events {ms:.3f} ms ({1e3 * ms / (nt - 1):.2f} us/step), wall {1e3 * wall:.3f} ms, phi={phi!r} diag={ctx.diagnostics()}", flush=True)
         ctx.close()
