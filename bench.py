@@ -15,6 +15,7 @@ import argparse
 import json
 import math
 import os
+import platform
 import sys
 import time
 
@@ -226,17 +227,26 @@ def cpu_baseline(args):
     from mioc.synth import CONFIGS, make_inputs
     cfg = CONFIGS[args.config]
     p = cfg.p if args.p is None else (math.inf if args.p == "inf" else float(args.p))
-    lt, df, uo = make_inputs(cfg, nt=args.cpu_steps + 1)
-    lv = Levels(lt.nu, [tuple(t) for t in lt.tuples])
+    # single-thread (the reference is single-threaded Julia) and OpenMP over the target levels
+    # on the host cores this job may use (OMP_NUM_THREADS on the GPU box; os.cpu_count() there is the machine's)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+    kind = P_INF if p == math.inf else P_ONE
     oc = OracleC()
-    t0 = time.perf_counter()
-    oc.bellman_steps(lv, df, uo, cfg.B, P_INF if p == math.inf else P_ONE, cfg.beta, cfg.dt, args.cpu_steps)
-    dt = time.perf_counter() - t0
-    per_step = dt / args.cpu_steps
-    per_sub = per_step * (cfg.nt - 1)
-    return {"value": 1.0 / per_sub, "unit": "subproblems/s", "cores": 1, "kind": "port",
-            "sample": f"{args.cpu_steps} of {cfg.nt - 1} recursion steps of the reference loop (C restatement, "
-                      f"1 thread) at L={lt.L}, B={cfg.B}; {per_step:.3f} s/step, extrapolated x{cfg.nt - 1}"}
+    per_step = {}
+    for nthr, steps in ((1, args.cpu_steps), (threads, args.cpu_steps * max(1, min(threads, 8)))):
+        lt, df, uo = make_inputs(cfg, nt=steps + 1)
+        lv = Levels(lt.nu, [tuple(t) for t in lt.tuples])
+        t0 = time.perf_counter()
+        oc.bellman_steps(lv, df, uo, cfg.B, kind, cfg.beta, cfg.dt, steps, threads=nthr)
+        per_step[nthr] = (time.perf_counter() - t0) / steps
+    per_sub = {k: v * (cfg.nt - 1) for k, v in per_step.items()}
+    return {"value": 1.0 / per_sub[threads], "unit": "subproblems/s", "cores": threads, "kind": "port",
+            "value_1thread": 1.0 / per_sub[1],
+            "sample": f"recursion steps of the reference loop (C restatement) at L={lt.L}, B={cfg.B}: "
+                      f"{args.cpu_steps} steps on 1 thread ({per_step[1]:.3f} s/step) and "
+                      f"{args.cpu_steps * max(1, min(threads, 8))} steps on {threads} OpenMP threads "
+                      f"({per_step[threads]:.3f} s/step), extrapolated x{cfg.nt - 1}; host {platform.processor() or platform.machine()}, "
+                      f"{os.cpu_count()} CPUs visible"}
 
 
 def main():

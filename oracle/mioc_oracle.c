@@ -270,9 +270,31 @@ double oracle_tv_p(const double *u, int64_t M, int64_t n, int p_kind, double p) 
  * the bench config would be 2.21 TB.  Runs `steps` recursion steps after the terminal step
  * (steps < n-1 gives the truncated timing sample of BASELINE.md §2).  Returns a checksum.
  */
+static double bellman_steps_impl(const or_levels *lv, const double *df, const double *u_old, int64_t n,
+                                 int64_t B, int p_kind, double beta, double dt, int64_t steps,
+                                 double *front_a, double *front_b, uint16_t *Ustep, int threads);
+
 double oracle_bellman_steps(const or_levels *lv, const double *df, const double *u_old, int64_t n,
                             int64_t B, int p_kind, double beta, double dt, int64_t steps,
                             double *front_a, double *front_b, uint16_t *Ustep) {
+    return bellman_steps_impl(lv, df, u_old, n, B, p_kind, beta, dt, steps, front_a, front_b, Ustep, 1);
+}
+
+/*
+ * The same loop with the target levels rl of each step split over `threads` OpenMP threads (BASELINE.md §2:
+ * "OpenMP over the level index l"): every rl writes only its own front column and U cells, so the result is
+ * identical to the single-threaded loop.
+ */
+double oracle_bellman_steps_mt(const or_levels *lv, const double *df, const double *u_old, int64_t n,
+                               int64_t B, int p_kind, double beta, double dt, int64_t steps,
+                               double *front_a, double *front_b, uint16_t *Ustep, int threads) {
+    return bellman_steps_impl(lv, df, u_old, n, B, p_kind, beta, dt, steps, front_a, front_b, Ustep,
+                              threads < 1 ? 1 : threads);
+}
+
+static double bellman_steps_impl(const or_levels *lv, const double *df, const double *u_old, int64_t n,
+                                 int64_t B, int p_kind, double beta, double dt, int64_t steps,
+                                 double *front_a, double *front_b, uint16_t *Ustep, int threads) {
     const int64_t M = lv->M, L = lv->L, R = B + 1;
     int64_t off[16];
     for (int64_t m = 0; m < M; ++m) off[m] = level_off(lv, m);
@@ -291,6 +313,7 @@ double oracle_bellman_steps(const or_levels *lv, const double *df, const double 
     }
     for (int64_t i = n - 1; i >= 1 && steps > 0; --i, --steps) {
         for (int64_t k = 0; k < R * L; ++k) w[k] = INFINITY;
+#pragma omp parallel for num_threads(threads) schedule(static)
         for (int64_t rl = 0; rl < L; ++rl) {
             const int32_t *l = lv->tuples + rl * M;
             double t1 = 0.0;

@@ -123,6 +123,8 @@ class OracleC:
                                            ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
                                            ctypes.c_double, ctypes.c_int64, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_bellman_steps_mt.restype = ctypes.c_double
+        L.oracle_bellman_steps_mt.argtypes = L.oracle_bellman_steps.argtypes + [ctypes.c_int]
 
     @staticmethod
     def _lv(lv):
@@ -164,8 +166,9 @@ class OracleC:
         kind = P_INF if p == math.inf else P_ONE
         return self.lib.oracle_tv_p(_ptr(u), u.shape[0], u.shape[1], kind, float(p))
 
-    def bellman_steps(self, lv, df, u_old, B, p_kind, beta, dt, steps):
-        """Timing leg for bench.py's cpu_baseline (p in {1, Inf}); returns (checksum, fronts)."""
+    def bellman_steps(self, lv, df, u_old, B, p_kind, beta, dt, steps, threads=1):
+        """Timing leg for bench.py's cpu_baseline (p in {1, Inf}); returns the checksum of the last front.
+        threads > 1: OpenMP over the target levels of each step (same result)."""
         df = np.asfortranarray(df, dtype=np.float64)
         u_old = np.asfortranarray(u_old, dtype=np.float64)
         M, n = df.shape
@@ -173,9 +176,11 @@ class OracleC:
         fa = np.empty(R * lv.L, dtype=np.float64)
         fb = np.empty(R * lv.L, dtype=np.float64)
         Us = np.zeros(R * lv.L, dtype=np.uint16)
-        cs = self.lib.oracle_bellman_steps(ctypes.byref(self._lv(lv)), _ptr(df), _ptr(u_old), n, B, p_kind,
-                                           beta, dt, steps, _ptr(fa), _ptr(fb), _ptr(Us))
-        return cs
+        args = (ctypes.byref(self._lv(lv)), _ptr(df), _ptr(u_old), n, B, p_kind, beta, dt, steps, _ptr(fa),
+                _ptr(fb), _ptr(Us))
+        if threads > 1:
+            return self.lib.oracle_bellman_steps_mt(*args, int(threads))
+        return self.lib.oracle_bellman_steps(*args)
 
 
 class OracleError(RuntimeError):
