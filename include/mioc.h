@@ -49,13 +49,16 @@ extern "C" {
 /* ---- algorithm selection (mioc_set_option(MIOC_OPT_ALGO, ...)) ----------------------------- */
 #define MIOC_OPT_ALGO 1
 #define MIOC_ALGO_AUTO 0    /* p=Inf -> class collapse; p=1, beta>0 on an 8^3 or 8^4 product grid ->
-                               separable transform; other large product grids at p=1 -> pyramid;
-                               otherwise the generic min-plus sweep */
+                               separable transform; small state (front fits one CU's LDS) -> fused;
+                               other large product grids at p=1 -> pyramid; otherwise the generic
+                               min-plus sweep */
 #define MIOC_ALGO_GENERIC 1 /* per-step min-plus sweep over every (c, l, j): any p */
 #define MIOC_ALGO_PINF 2    /* exact p=Inf collapse onto per-budget row minima */
 #define MIOC_ALGO_PYRAMID 3 /* p=1 on product grids of consecutive levels: exact L1-ball pyramid */
 #define MIOC_ALGO_SEPARABLE 4 /* p=1, beta>0, 8^3 / 8^4 product grid of consecutive levels: separable L1
                                  distance transform in exact fixed point with a certified argmin */
+#define MIOC_ALGO_FUSED 5   /* whole DP of each subproblem in ONE workgroup with the value front in LDS
+                               (any p; L <= 64, small B): the batch path for small-state problems */
 #define MIOC_OPT_TIMING 2   /* 1: record HIP events around the dominant kernel (mioc_kernel_stats) */
 #define MIOC_OPT_PERSIST 3  /* separable transform: 1 (default) runs the whole DP as one persistent launch
                                whose workgroups hand rows to each other; 0: one launch per step */

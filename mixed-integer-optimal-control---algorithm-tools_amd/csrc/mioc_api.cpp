@@ -221,10 +221,15 @@ int run_bellman(mioc_ctx *ctx) {
   const bool pyr_ok = ctx->p_kind == MIOC_P_ONE && ctx->pyr_ok && ctx->beta >= 0.0;
   // the separable transform works in units of beta (exact unit steps): beta > 0, 8^3 / 8^4 grids
   const bool sdt_ok = pyr_ok && ctx->beta > 0.0 && sdt_supported(ctx->pyr);
+  // the fused small-state DP keeps a subproblem's whole front (and the per-step K table) in one CU's LDS
+  const bool fused_ok = fused_supported((int)ctx->L, ctx->B, nullptr) && ctx->nt >= 1;
   if (algo == MIOC_ALGO_AUTO)
-    algo = pinf_ok  ? MIOC_ALGO_PINF
-           : sdt_ok ? MIOC_ALGO_SEPARABLE
-                    : (pyr_ok && ctx->L >= 256 ? MIOC_ALGO_PYRAMID : MIOC_ALGO_GENERIC);
+    algo = pinf_ok    ? MIOC_ALGO_PINF
+           : sdt_ok   ? MIOC_ALGO_SEPARABLE
+           : fused_ok ? MIOC_ALGO_FUSED
+                      : (pyr_ok && ctx->L >= 256 ? MIOC_ALGO_PYRAMID : MIOC_ALGO_GENERIC);
+  if (algo == MIOC_ALGO_FUSED && !fused_ok)
+    return fail(ctx, MIOC_EINVAL, "the fused small-state DP needs L <= 64 and a front that fits one CU's LDS");
   if (algo == MIOC_ALGO_PINF && !pinf_ok)
     return fail(ctx, MIOC_EINVAL, "p=Inf collapse needs p_kind MIOC_P_INF, <= 64 budget classes and B < 7936");
   if (algo == MIOC_ALGO_PYRAMID && !pyr_ok)
@@ -304,6 +309,17 @@ int run_bellman(mioc_ctx *ctx) {
                                      (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters));
       ev_end(ctx, 0, ctx->nt - 1);
     }
+  } else if (algo == MIOC_ALGO_FUSED) {
+    ctx->ubytes = 1;
+    const size_t front_stride = L * RP;
+    int rc = grow(ctx, &ctx->d_front, &ctx->front_cap, K * front_stride * sizeof(double), "value fronts");
+    if (rc) return rc;
+    const size_t u_stride_k = (nt > 1 ? nt - 1 : 1) * L * (size_t)(ctx->B + 1);
+    rc = grow(ctx, &ctx->d_U, &ctx->U_cap, K * u_stride_k, "argmin table U");
+    if (rc) return rc;
+    ev_begin(ctx, 0, "k_fused_run");
+    HIP_TRY(ctx, launch_fused_run(ctx->stream, P, Lv, ctx->d_front, front_stride, (uint8_t *)ctx->d_U, u_stride_k));
+    ev_end(ctx, 0, 1);
   } else if (algo == MIOC_ALGO_GENERIC) {
     ctx->ubytes = L <= 256 ? 1 : 2;
     const size_t front_stride = L * RP;
@@ -370,7 +386,7 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
     HIP_TRY(ctx, launch_stage_walk(ctx->stream, P, Lv, (const uint16_t *)ctx->d_U, uu_stride_k, ctx->d_start,
                                    d_urank, ctx->d_ranks, ctx->d_flags + 2));
     ev_end(ctx, 1, 1);
-  } else if (ctx->algo == MIOC_ALGO_GENERIC) {
+  } else if (ctx->algo == MIOC_ALGO_GENERIC || ctx->algo == MIOC_ALGO_FUSED) {
     const size_t front_stride = (size_t)ctx->L * ctx->RP;
     const size_t u_stride_k = (nt > 1 ? nt - 1 : 1) * (size_t)ctx->L * (size_t)(ctx->B + 1);
     HIP_TRY(ctx, launch_generic_argmin0(ctx->stream, P, Lv, ctx->d_front, front_stride, (int)B_use, ctx->d_start));
@@ -472,7 +488,7 @@ const char *mioc_last_error(const mioc_ctx *ctx) { return ctx ? ctx->err.c_str()
 int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   if (!ctx) return MIOC_EINVAL;
   if (option == MIOC_OPT_ALGO) {
-    if (value < MIOC_ALGO_AUTO || value > MIOC_ALGO_SEPARABLE) return fail(ctx, MIOC_EINVAL, "unknown algorithm");
+    if (value < MIOC_ALGO_AUTO || value > MIOC_ALGO_FUSED) return fail(ctx, MIOC_EINVAL, "unknown algorithm");
     ctx->opt_algo = value;
     return MIOC_OK;
   }

@@ -105,6 +105,11 @@ hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev
                              size_t uu_stride_k, const Start *start, const int32_t *urank, int32_t *ranks,
                              int32_t *counters);
 
+// ---- fused small-state DP (mioc_fused.hip): one workgroup per subproblem, front in LDS -------------
+bool fused_supported(int L, int B, size_t *lds_out);
+hipError_t launch_fused_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, double *front0,
+                            size_t front_stride, uint8_t *U, size_t u_stride_k);
+
 // ---- p = Inf collapse (mioc_pinf.hip) -----------------------------------------------------------
 struct PinfDev {
   int BW = 0;                      // budget classes tracked: bmax+1 <= B+1

@@ -28,6 +28,7 @@ MIOC_ENONFINITE = -7
 MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
 MIOC_OPT_ALGO, MIOC_OPT_TIMING, MIOC_OPT_PERSIST = 1, 2, 3
 MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID, MIOC_ALGO_SEPARABLE = 0, 1, 2, 3, 4
+MIOC_ALGO_FUSED = 5
 
 EXPORTED = [
     "mioc_version", "mioc_create", "mioc_destroy", "mioc_last_error", "mioc_set_option", "mioc_set_levels",
@@ -281,6 +282,20 @@ def pyramid_eligible(levels: LevelTable):
     if not np.array_equal(((levels.tuples - 1) * strides).sum(axis=1), np.arange(levels.L)):
         return False
     return all(list(v) == list(range(v[0], v[0] + len(v))) for v in levels.nu)
+
+
+def fused_eligible(L, B):
+    """Mirror of the library's fused small-state domain (mioc_fused.hip fused_supported): L <= 64 levels, at
+    most 192 (64-row block, target) tasks per step, and front + per-step tables within one CU's 160 KiB LDS."""
+    if not (1 <= L <= 64) or B < 0:
+        return False
+    LP = next(x for x in (4, 8, 16, 24, 32, 36, 48, 64) if L <= x)
+    R = B + 1
+    nrb = (R + 63) // 64
+    if nrb * L > 8 * 24:
+        return False
+    o = (R * (LP + 2) * 8 + 15) // 16 * 16 + 2 * L * LP * 8 + 2 * LP * 4 + 2 * 8 * 24 * 2
+    return (o + 15) // 16 * 16 + 16 <= 160 * 1024
 
 
 def separable_eligible(levels: LevelTable):

@@ -34,14 +34,15 @@ def _oracle_levels(lt):
     return Levels(lt.nu, [tuple(int(x) for x in t) for t in lt.tuples])
 
 
-def _algos(p_kind, lt=None):
+def _algos(p_kind, lt=None, B=None):
+    fused = (native.MIOC_ALGO_FUSED,) if lt is not None and B is not None and native.fused_eligible(lt.L, B) else ()
     if p_kind == P_INF:
-        return ALGOS_PINF
+        return ALGOS_PINF + fused
     if p_kind == P_ONE and lt is not None and native.separable_eligible(lt):
-        return (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID, native.MIOC_ALGO_SEPARABLE)
+        return (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID, native.MIOC_ALGO_SEPARABLE) + fused
     if p_kind == P_ONE and lt is not None and native.pyramid_eligible(lt):
-        return (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID)
-    return (native.MIOC_ALGO_GENERIC,)
+        return (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_PYRAMID) + fused
+    return (native.MIOC_ALGO_GENERIC,) + fused
 
 
 def _assert_U(ctx, U, n, tag):
@@ -60,7 +61,7 @@ def test_golden_fixtures(path):
     g = load_golden(path)
     lt = LevelTable(g["nu"], g["tuple_list"])
     table = g["wtab"] if g["wtab"].size else None
-    for algo in _algos(g["p_kind"], lt):
+    for algo in _algos(g["p_kind"], lt, g["B"]):
         ctx = _ctx(lt, g["p_kind"], g["beta"], algo, p_int=g["p_int"], table=table)
         ctx.bellman(g["df"], g["u_old"], g["B"], g["dt"])
         assert ctx.last_algo() == algo
@@ -101,7 +102,7 @@ def test_random_vs_oracle(oracle_c, seed):
     phi, U = oracle_c.bellman(lv, df, uo, B, pk, beta, dt)
     lt = LevelTable(lv.nu, [tuple(t) for t in lv.tuples])
     budgets = sorted({B, B // 2, 0, int(rng.integers(0, B + 1))})
-    for algo in _algos(pk, lt):
+    for algo in _algos(pk, lt, B):
         ctx = _ctx(lt, pk, beta, algo)
         ctx.bellman(df, uo, B, dt)
         if algo != native.MIOC_ALGO_PINF:
@@ -127,17 +128,19 @@ def test_p2_lut_and_table_kinds_vs_oracle(oracle_c):
     k, pint, tab = native.cost_spec(2, levels=lt)
     phi, U = oracle_c.bellman(lv, df, uo, B, P_INTLUT, 1e-3, cfg.dt, p_int=2, wtab=tab)
     ou, ops = oracle_c.backtrack(lv, uo, phi, U, B, B)
-    ctx = _ctx(lt, k, 1e-3, native.MIOC_ALGO_GENERIC, p_int=pint, table=tab)
-    ctx.bellman(df, uo, B, cfg.dt)
-    u, ps, _ = ctx.backtrack(B)
-    assert np.array_equal(u, ou) and ps == ops
-    # the same weights as a full pair table (MIOC_P_TABLE) must give the same answer
     nv = lt.nuval
     S = (np.abs(nv[:, None, :] - nv[None, :, :]) ** 2).sum(axis=2).astype(int)
-    ctx2 = _ctx(lt, native.MIOC_P_TABLE, 1e-3, native.MIOC_ALGO_GENERIC, table=tab[S].reshape(-1))
-    ctx2.bellman(df, uo, B, cfg.dt)
-    u2, ps2, _ = ctx2.backtrack(B)
-    assert np.array_equal(u2, ou) and ps2 == ops
+    for algo in (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_FUSED):
+        ctx = _ctx(lt, k, 1e-3, algo, p_int=pint, table=tab)
+        ctx.bellman(df, uo, B, cfg.dt)
+        u, ps, _ = ctx.backtrack(B)
+        assert np.array_equal(u, ou) and ps == ops, f"algo={algo}"
+        _assert_U(ctx, U, df.shape[1], f"p2 lut algo={algo}")
+        # the same weights as a full pair table (MIOC_P_TABLE) must give the same answer
+        ctx2 = _ctx(lt, native.MIOC_P_TABLE, 1e-3, algo, table=tab[S].reshape(-1))
+        ctx2.bellman(df, uo, B, cfg.dt)
+        u2, ps2, _ = ctx2.backtrack(B)
+        assert np.array_equal(u2, ou) and ps2 == ops, f"algo={algo}"
 
 
 @pytest.mark.parametrize("key", ["C1", "C2", "C3"])
@@ -149,7 +152,7 @@ def test_full_size_sos1_configs_vs_oracle(oracle_c, key):
     phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_INF, cfg.beta, cfg.dt)
     for Bp in (cfg.B, cfg.B // 2, cfg.B // 8):
         ou, ops = oracle_c.backtrack(lv, uo, phi, U, cfg.B, Bp)
-        for algo in ALGOS_PINF:
+        for algo in ALGOS_PINF + (native.MIOC_ALGO_FUSED,):
             ctx = _ctx(lt, P_INF, cfg.beta, algo)
             ctx.bellman(df, uo, cfg.B, cfg.dt)
             u, ps, _ = ctx.backtrack(Bp)
@@ -164,10 +167,11 @@ def test_full_size_c5_restart_vs_oracle(oracle_c):
     lv = _oracle_levels(lt)
     phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_ONE, cfg.beta, cfg.dt)
     ou, ops = oracle_c.backtrack(lv, uo, phi, U, cfg.B, cfg.B)
-    ctx = _ctx(lt, P_ONE, cfg.beta, native.MIOC_ALGO_GENERIC)
-    ctx.bellman(df, uo, cfg.B, cfg.dt)
-    u, ps, _ = ctx.backtrack(cfg.B)
-    assert np.array_equal(u, ou) and ps == ops
+    for algo in (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_FUSED):
+        ctx = _ctx(lt, P_ONE, cfg.beta, algo)
+        ctx.bellman(df, uo, cfg.B, cfg.dt)
+        u, ps, _ = ctx.backtrack(cfg.B)
+        assert np.array_equal(u, ou) and ps == ops, f"algo={algo}"
 
 
 def _path_objective(lt, df, u, dt, beta, p_kind):
@@ -285,7 +289,8 @@ def test_batch_device_api_equals_single():
         _, df, uo = make_inputs(cfg, k=k, nt=nt, levels=lt)
         dfs.append(df)
         uos.append(uo)
-    for pk, algos in ((P_ONE, (native.MIOC_ALGO_GENERIC,)), (P_INF, ALGOS_PINF)):
+    for pk, algos in ((P_ONE, (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_FUSED)),
+                      (P_INF, ALGOS_PINF + (native.MIOC_ALGO_FUSED,))):
         for algo in algos:
             ctx = _ctx(lt, pk, cfg.beta, algo)
             ddf = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in dfs])), dtype=torch.float64, device="cuda")
@@ -433,7 +438,7 @@ def test_run_ahead_walk_vs_oracle(oracle_c, uo_mode, pk):
         for i in rng.choice(n, size=12, replace=False):
             uo[rng.integers(3), i] = float(rng.choice([-1, 4]))
     phi, U = oracle_c.bellman(lv, df, uo, B, pk, beta, dt)
-    for algo in _algos(pk, lt):
+    for algo in _algos(pk, lt, B):
         ctx = _ctx(lt, pk, beta, algo)
         ctx.bellman(df, uo, B, dt)
         for Bp in (B, B // 3, 0):
