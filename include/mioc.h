@@ -59,6 +59,9 @@ extern "C" {
                                  distance transform in exact fixed point with a certified argmin */
 #define MIOC_ALGO_FUSED 5   /* whole DP of each subproblem in ONE workgroup with the value front in LDS
                                (any p; L <= 64, small B): the batch path for small-state problems */
+#define MIOC_ALGO_FUSED_SEPARABLE 6 /* the fused DP with the separable L1 transform of MIOC_ALGO_SEPARABLE:
+                                       p=1, beta>0, 2-D product grid of consecutive integer levels
+                                       (6x6, 4x4, 8x8, 8x4), B < 512 */
 #define MIOC_OPT_TIMING 2   /* 1: record HIP events around the dominant kernel (mioc_kernel_stats) */
 #define MIOC_OPT_PERSIST 3  /* separable transform: 1 (default) runs the whole DP as one persistent launch
                                whose workgroups hand rows to each other; 0: one launch per step */
@@ -146,7 +149,8 @@ int32_t mioc_last_algo(mioc_ctx *ctx);
  * targets of rows sent straight to the exact scan: few targets, or a value scale outside its binade), [2] backtrack: p=Inf walk steps resolved
  * by the exact scan, or for the U-table walks (generic, pyramid) the run-ahead rounds taken (each round
  * settles up to 64 steps), [3] internal consistency failures (must be 0); [4..7] pyramid internals: rows whose
- * value hash overflowed, targets whose value was not found, values flagged as colliding, reserved.
+ * value hash overflowed, targets whose value was not found, values flagged as colliding; [7] fused DP: resident
+ * workgroups per CU (occupancy query).
  */
 int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n);
 

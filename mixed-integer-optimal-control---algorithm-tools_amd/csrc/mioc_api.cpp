@@ -223,11 +223,18 @@ int run_bellman(mioc_ctx *ctx) {
   const bool sdt_ok = pyr_ok && ctx->beta > 0.0 && sdt_supported(ctx->pyr);
   // the fused small-state DP keeps a subproblem's whole front (and the per-step K table) in one CU's LDS
   const bool fused_ok = fused_supported((int)ctx->L, ctx->B, nullptr) && ctx->nt >= 1;
+  // ... and with the separable L1 transform (p = 1, β > 0, 2-D product grid of consecutive levels)
+  const bool fsep_ok = ctx->p_kind == MIOC_P_ONE && ctx->grid_ok && ctx->beta > 0.0 &&
+                       fsep_supported(ctx->pyr, ctx->B, nullptr, nullptr);
   if (algo == MIOC_ALGO_AUTO)
     algo = pinf_ok    ? MIOC_ALGO_PINF
            : sdt_ok   ? MIOC_ALGO_SEPARABLE
+           : fsep_ok  ? MIOC_ALGO_FUSED_SEPARABLE
            : fused_ok ? MIOC_ALGO_FUSED
                       : (pyr_ok && ctx->L >= 256 ? MIOC_ALGO_PYRAMID : MIOC_ALGO_GENERIC);
+  if (algo == MIOC_ALGO_FUSED_SEPARABLE && !fsep_ok)
+    return fail(ctx, MIOC_EINVAL, "the fused separable DP needs p = 1, beta > 0, a 2-D product grid of consecutive "
+                                  "integer levels (6x6, 4x4, 8x8 or 8x4) and B < 512");
   if (algo == MIOC_ALGO_FUSED && !fused_ok)
     return fail(ctx, MIOC_EINVAL, "the fused small-state DP needs L <= 64 and a front that fits one CU's LDS");
   if (algo == MIOC_ALGO_PINF && !pinf_ok)
@@ -309,7 +316,7 @@ int run_bellman(mioc_ctx *ctx) {
                                      (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters));
       ev_end(ctx, 0, ctx->nt - 1);
     }
-  } else if (algo == MIOC_ALGO_FUSED) {
+  } else if (algo == MIOC_ALGO_FUSED || algo == MIOC_ALGO_FUSED_SEPARABLE) {
     ctx->ubytes = 1;
     const size_t front_stride = L * RP;
     int rc = grow(ctx, &ctx->d_front, &ctx->front_cap, K * front_stride * sizeof(double), "value fronts");
@@ -317,8 +324,15 @@ int run_bellman(mioc_ctx *ctx) {
     const size_t u_stride_k = (nt > 1 ? nt - 1 : 1) * L * (size_t)(ctx->B + 1);
     rc = grow(ctx, &ctx->d_U, &ctx->U_cap, K * u_stride_k, "argmin table U");
     if (rc) return rc;
-    ev_begin(ctx, 0, "k_fused_run");
-    HIP_TRY(ctx, launch_fused_run(ctx->stream, P, Lv, ctx->d_front, front_stride, (uint8_t *)ctx->d_U, u_stride_k));
+    ctx->occupancy = fused_blocks_per_cu(algo == MIOC_ALGO_FUSED_SEPARABLE, ctx->pyr, (int)ctx->L, ctx->B);
+    if (algo == MIOC_ALGO_FUSED) {
+      ev_begin(ctx, 0, "k_fused_run");
+      HIP_TRY(ctx, launch_fused_run(ctx->stream, P, Lv, ctx->d_front, front_stride, (uint8_t *)ctx->d_U, u_stride_k));
+    } else {
+      ev_begin(ctx, 0, "k_fsep_run");
+      HIP_TRY(ctx, launch_fsep_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_front, front_stride, (uint8_t *)ctx->d_U,
+                                   u_stride_k, ctx->d_counters));
+    }
     ev_end(ctx, 0, 1);
   } else if (algo == MIOC_ALGO_GENERIC) {
     ctx->ubytes = L <= 256 ? 1 : 2;
@@ -386,7 +400,8 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
     HIP_TRY(ctx, launch_stage_walk(ctx->stream, P, Lv, (const uint16_t *)ctx->d_U, uu_stride_k, ctx->d_start,
                                    d_urank, ctx->d_ranks, ctx->d_flags + 2));
     ev_end(ctx, 1, 1);
-  } else if (ctx->algo == MIOC_ALGO_GENERIC || ctx->algo == MIOC_ALGO_FUSED) {
+  } else if (ctx->algo == MIOC_ALGO_GENERIC || ctx->algo == MIOC_ALGO_FUSED ||
+             ctx->algo == MIOC_ALGO_FUSED_SEPARABLE) {
     const size_t front_stride = (size_t)ctx->L * ctx->RP;
     const size_t u_stride_k = (nt > 1 ? nt - 1 : 1) * (size_t)ctx->L * (size_t)(ctx->B + 1);
     HIP_TRY(ctx, launch_generic_argmin0(ctx->stream, P, Lv, ctx->d_front, front_stride, (int)B_use, ctx->d_start));
@@ -488,7 +503,7 @@ const char *mioc_last_error(const mioc_ctx *ctx) { return ctx ? ctx->err.c_str()
 int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   if (!ctx) return MIOC_EINVAL;
   if (option == MIOC_OPT_ALGO) {
-    if (value < MIOC_ALGO_AUTO || value > MIOC_ALGO_FUSED) return fail(ctx, MIOC_EINVAL, "unknown algorithm");
+    if (value < MIOC_ALGO_AUTO || value > MIOC_ALGO_FUSED_SEPARABLE) return fail(ctx, MIOC_EINVAL, "unknown algorithm");
     ctx->opt_algo = value;
     return MIOC_OK;
   }
@@ -587,12 +602,13 @@ int32_t mioc_set_levels(mioc_ctx *ctx, int64_t M, const int64_t *counts, const i
   HIP_TRY(ctx, hipMemcpy(ctx->d_numax, ctx->numax_h.data(), M * sizeof(double), hipMemcpyHostToDevice));
   // pyramid domain: product iterator in grid order, consecutive integer levels, dim 0 <= 8 levels
   {
-    bool ok = L == Lgrid && L <= 4096 && M >= 2 && M <= 6 && (counts[0] == 8 || counts[0] == 4) &&
-              Lgrid / counts[0] <= 512;
-    for (int64_t r = 0; ok && r < L; ++r) ok = gidx[r] == r;
-    for (int64_t m = 0; ok && m < M; ++m)
-      for (int64_t q = 0; ok && q < counts[m]; ++q) ok = values[off[m] + q] == values[off[m]] + q;
-    ctx->pyr_ok = ok;
+    // a product grid of consecutive integer levels in iterator (grid) order
+    bool grid = L == Lgrid && L <= 4096 && M >= 2 && M <= 6;
+    for (int64_t r = 0; grid && r < L; ++r) grid = gidx[r] == r;
+    for (int64_t m = 0; grid && m < M; ++m)
+      for (int64_t q = 0; grid && q < counts[m]; ++q) grid = values[off[m] + q] == values[off[m]] + q;
+    ctx->grid_ok = grid;
+    ctx->pyr_ok = grid && (counts[0] == 8 || counts[0] == 4) && Lgrid / counts[0] <= 512;
     mioc::PyrGeom G;
     G.M = (int)M;
     G.ncol = (int)(Lgrid / counts[0]);
@@ -745,7 +761,7 @@ int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->d_counters) HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
   HIP_TRY(ctx, hipMemcpy(f, ctx->d_flags, sizeof f, hipMemcpyDeviceToHost));
-  const int64_t all[8] = {c[0], c[1], f[2], f[3], c[4], c[5], c[6], c[7]};
+  const int64_t all[8] = {c[0], c[1], f[2], f[3], c[4], c[5], c[6], ctx->occupancy};
   for (int32_t q = 0; q < n && q < 8; ++q) counters[q] = all[q];
   return MIOC_OK;
 }

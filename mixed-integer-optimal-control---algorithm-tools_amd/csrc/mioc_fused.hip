@@ -36,6 +36,12 @@ constexpr int FU_W = 8;      // waves per workgroup (two per SIMD)
 constexpr int FU_MAXT = 24;  // tasks per wave per step (host checks ceil(R/64)·L <= FU_W·FU_MAXT)
 constexpr int FU_G = 4;      // argmin group
 
+// Workgroup barrier for LDS hand-offs only: every wave drains its own LDS operations, then s_barrier.  A
+// __syncthreads() would also wait for the wave's outstanding global stores (the U bytes, which nothing in the
+// launch reads back), i.e. pay their full latency at every step.  The "memory" clobber keeps the compiler from
+// moving LDS accesses across it.
+__device__ __forceinline__ void fu_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // v_min_f64 without llvm.minnum's canonicalising v_max_f64 x,x on every operand (operands are finite or +Inf)
 __device__ __forceinline__ double fu_min(double a, double b) {
   double r;
@@ -45,7 +51,7 @@ __device__ __forceinline__ double fu_min(double a, double b) {
 
 struct FuLayout {
   int FS, R, nrb;
-  size_t off_K, off_bt, off_task, off_cnt, bytes;
+  size_t off_K, off_bt, off_task, off_cnt, off_nu, bytes;
 };
 
 __host__ __device__ inline FuLayout fu_layout(int LP, int L, int B) {
@@ -64,6 +70,8 @@ __host__ __device__ inline FuLayout fu_layout(int LP, int L, int B) {
   o = (o + 15) / 16 * 16;
   f.off_cnt = o;
   o += 16;
+  f.off_nu = o;
+  o += (size_t)L * kMaxM * sizeof(double);
   f.bytes = o;
   return f;
 }
@@ -99,20 +107,19 @@ __device__ __forceinline__ double fu_cost(const LevelsDev &Lv, int l, int j) {
   return Lv.costlut[key];
 }
 
-// Per-step tables for step s (K, b̃, task list) into buffer `buf`.  Every thread recomputes the T1 / b̃ it needs
-// from the step's df / u_old (broadcast loads), so no barrier separates the pieces.  cst: this thread's cached
-// β·w(l, j) for the pairs e = tid + 512·q.
+// Per-step tables for step s (K, b̃, task list) into buffer `buf`, from the step's Δt·df and u_old, which lane
+// m of every wave holds (dfv, uov: loaded a step ahead).  Every thread recomputes the T1 / b̃ it needs, so no
+// barrier separates the pieces.  cst: this thread's cached β·w(l, j) for the pairs e = tid + 512·q; nul: the
+// level values [L][M] in LDS.
 template <int LP, int NQ>
-__device__ __forceinline__ void fu_prepare(const ProblemDev &P, const LevelsDev &Lv, int k, int s, int buf,
-                                           const double (&cst)[NQ], double *Kb, int *btb, uint16_t *taskb,
-                                           int *cnt, const FuLayout &F) {
+__device__ __forceinline__ void fu_prepare(const ProblemDev &P, const LevelsDev &Lv, double dfv, double uov,
+                                           int buf, const double (&cst)[NQ], const double *nul, double *Kb,
+                                           int *btb, uint16_t *taskb, int *cnt, const FuLayout &F) {
   const int tid = threadIdx.x, L = Lv.L, M = P.M;
-  const double *dfs = P.df + ((size_t)k * P.nt + s) * M;
-  const double *uos = P.uold + ((size_t)k * P.nt + s) * M;
   double a[kMaxM], uo[kMaxM];
   for (int m = 0; m < M; ++m) {
-    a[m] = P.dt * dfs[m];
-    uo[m] = uos[m];
+    a[m] = __shfl(dfv, m);
+    uo[m] = __shfl(uov, m);
   }
   double *K = Kb + (size_t)buf * L * LP;
 #pragma unroll
@@ -120,13 +127,18 @@ __device__ __forceinline__ void fu_prepare(const ProblemDev &P, const LevelsDev 
     const int e = tid + 512 * q;
     if (e < L * LP) {
       const int l = e / LP, j = e - l * LP;
-      K[e] = j < L ? fu_t1(Lv, l, a) + cst[q] : INFINITY;
+      double t = 0.0;  // T1(l) = ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
+      for (int m = 0; m < M; ++m) t = t + a[m] * nul[l * M + m];
+      K[e] = j < L ? t + cst[q] : INFINITY;
     }
   }
   if (tid < 64) {  // wave 0: b̃ and the compacted task list (row block major, target ascending)
     const int lane = tid;
     int b = 1 << 29;
-    if (lane < L) b = fu_bt(Lv, lane, uo);
+    if (lane < L) {
+      b = 0;  // saturated: far off-grid u_old entries only ever mean "beyond every budget"
+      for (int m = 0; m < M; ++m) b += (int)fmin(fabs(nul[lane * M + m] - uo[m]), 1.0e8);
+    }
     if (lane < LP) btb[buf * LP + lane] = b;
     int n = 0;
     uint16_t *tl = taskb + buf * (FU_W * FU_MAXT);
@@ -139,6 +151,32 @@ __device__ __forceinline__ void fu_prepare(const ProblemDev &P, const LevelsDev 
     if (lane == 0) cnt[buf] = n;
   }
 }
+
+// lane m < M: Δt·df[m, s] and u_old[m, s] (one load each, in flight until fu_prepare)
+__device__ __forceinline__ void fu_fetch(const ProblemDev &P, int k, int s, double &dfv, double &uov) {
+  const int lane = threadIdx.x & 63;
+  dfv = 0.0;
+  uov = 0.0;
+  if (lane < P.M) {
+    dfv = P.dt * P.df[((size_t)k * P.nt + s) * P.M + lane];
+    uov = P.uold[((size_t)k * P.nt + s) * P.M + lane];
+  }
+}
+
+#if defined(MIOC_STAMPS)
+// diagnostic build: cycles per phase summed over the steps, per workgroup (wave 0's view)
+__device__ unsigned long long g_fu_stamps[4096][8];
+#define FU_T(v) unsigned long long v = ((threadIdx.x & 63) == 0) ? __builtin_amdgcn_s_memtime() : 0ull
+#define FU_ACC(q, a, b) \
+  if ((threadIdx.x & 63) == 0) acc[q] += (b) - (a)
+#else
+#define FU_T(v) \
+  do {          \
+  } while (0)
+#define FU_ACC(q, a, b) \
+  do {                  \
+  } while (0)
+#endif
 
 template <int LP>
 __global__ __launch_bounds__(512) void k_fused_run(ProblemDev P, LevelsDev Lv, double *__restrict__ front0_all,
@@ -156,6 +194,11 @@ __global__ __launch_bounds__(512) void k_fused_run(ProblemDev P, LevelsDev Lv, d
   int *btb = reinterpret_cast<int *>(fsm + F.off_bt);
   uint16_t *taskb = reinterpret_cast<uint16_t *>(fsm + F.off_task);
   int *cnt = reinterpret_cast<int *>(fsm + F.off_cnt);
+  double *nul = reinterpret_cast<double *>(fsm + F.off_nu);
+  for (int e = tid; e < L * P.M; e += 512) nul[e] = Lv.nuval[e];
+#if defined(MIOC_STAMPS)
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
   double cst[NQ];
 #pragma unroll
@@ -179,7 +222,12 @@ __global__ __launch_bounds__(512) void k_fused_run(ProblemDev P, LevelsDev Lv, d
       front[c * FS + l] = v;
     }
   }
-  if (nt >= 2) fu_prepare<LP, NQ>(P, Lv, k, nt - 2, (nt - 2) & 1, cst, Kb, btb, taskb, cnt, F);
+  double dfv, uov;
+  __syncthreads();  // nul
+  if (nt >= 2) {
+    fu_fetch(P, k, nt - 2, dfv, uov);
+    fu_prepare<LP, NQ>(P, Lv, dfv, uov, (nt - 2) & 1, cst, nul, Kb, btb, taskb, cnt, F);
+  }
   __syncthreads();
 
   uint8_t *Uk = U_all + (size_t)k * u_stride_k;
@@ -190,15 +238,17 @@ __global__ __launch_bounds__(512) void k_fused_run(ProblemDev P, LevelsDev Lv, d
     const uint16_t *tl = taskb + cur * (FU_W * FU_MAXT);
     const int V = __builtin_amdgcn_readfirstlane(cnt[cur]);
     const int t0 = (w * V) / FU_W, t1 = ((w + 1) * V) / FU_W;
+    const int *bt = btb + cur * LP;
+    uint8_t *Ui = Uk + (size_t)i * ((size_t)L * R);
+    if (i >= 1) fu_fetch(P, k, i - 1, dfv, uov);  // the next step's inputs, consumed after this step's tasks
+    FU_T(s0);
     double ov[FU_MAXT];
-    int oa[FU_MAXT];
     double psi[LP];
     int cur_rb = -1;
     // ---- compute: every task of this wave, outputs kept in registers -----------------------------------
 #pragma unroll
     for (int t = 0; t < FU_MAXT; ++t) {
       ov[t] = INFINITY;
-      oa[t] = 0xFF;
       if (t0 + t < t1) {
         const int task = __builtin_amdgcn_readfirstlane((int)tl[t0 + t]);
         const int rb = task >> 8, l = task & 255;
@@ -240,24 +290,25 @@ __global__ __launch_bounds__(512) void k_fused_run(ProblemDev P, LevelsDev Lv, d
           arg = q0.x + p0.x == best ? j0 : arg;
         }
         ov[t] = best;
-        oa[t] = arg;
+        const int c = cp + bt[l];  // U goes to HBM at once; the value waits for the barrier
+#ifndef FU_NOU
+        if (c <= B && best < INFINITY) Ui[(size_t)l * R + c] = (uint8_t)arg;
+#endif
       }
     }
-    // prefetch-free: the next step's tables come from df / u_old, read after the barrier
-    __syncthreads();  // every wave has read its rows of Φ_{i+1}: the front may be overwritten
-    // ---- write Φ_i in place and the U bytes ---------------------------------------------------------------
-    const int *bt = btb + cur * LP;
-    uint8_t *Ui = Uk + (size_t)i * ((size_t)L * R);
+    FU_T(s1);
+    if (i >= 1) fu_prepare<LP, NQ>(P, Lv, dfv, uov, (i - 1) & 1, cst, nul, Kb, btb, taskb, cnt, F);
+    FU_T(s2);
+    fu_lds_barrier();  // every wave has read its rows of Φ_{i+1}: the front may be overwritten
+    FU_T(s3);
+    // ---- write Φ_i in place --------------------------------------------------------------------------------
 #pragma unroll
     for (int t = 0; t < FU_MAXT; ++t) {
       if (t0 + t < t1) {
         const int task = __builtin_amdgcn_readfirstlane((int)tl[t0 + t]);
         const int rb = task >> 8, l = task & 255;
         const int c = 64 * rb + lane + bt[l];
-        if (c <= B) {
-          front[c * FS + l] = ov[t];
-          if (ov[t] < INFINITY) Ui[(size_t)l * R + c] = (uint8_t)oa[t];
-        }
+        if (c <= B) front[c * FS + l] = ov[t];
       }
     }
     // cells below the target's own budget class are unreachable: Φ_i[c, l] = +Inf for c < b̃(l, i)
@@ -265,15 +316,413 @@ __global__ __launch_bounds__(512) void k_fused_run(ProblemDev P, LevelsDev Lv, d
       const int b = min(bt[l], R);
       for (int c = lane; c < b; c += 64) front[c * FS + l] = INFINITY;
     }
-    if (i >= 1) fu_prepare<LP, NQ>(P, Lv, k, i - 1, (i - 1) & 1, cst, Kb, btb, taskb, cnt, F);
-    __syncthreads();
+    FU_T(s4);
+    fu_lds_barrier();
+    FU_T(s5);
+    FU_ACC(0, s0, s1);
+    FU_ACC(1, s1, s2);
+    FU_ACC(2, s2, s3);
+    FU_ACC(3, s3, s4);
+    FU_ACC(4, s4, s5);
   }
+#if defined(MIOC_STAMPS)
+  if (tid == 0)
+    for (int q = 0; q < 8; ++q) g_fu_stamps[k & 4095][q] = acc[q];
+#endif
   // ---- Φ_0 to HBM in the generic layout [L][RP] (the backtrack's argmin reads it) ------------------------
   double *f0 = front0_all + (size_t)k * front_stride;
   for (int e = tid; e < L * P.RP; e += 512) {
     const int l = e / P.RP, c = e - l * P.RP;
     f0[e] = c < R ? front[c * FS + l] : INFINITY;
   }
+}
+
+// ==============================================================================================================
+// p = 1 on a 2-D product grid of consecutive integer levels (N0 x N1 <= 8 x 8): the same fused DP with the
+// separable L1 transform of mioc_sdt.hip in place of the min-plus sweep, entirely in registers.
+//
+// Lane = source row c' (one wave per 64 rows, the whole workgroup one subproblem).  The lane's row Ψ_j =
+// Φ_{i+1}[c', j] (all L sources) sits in VGPRs, so the two passes of the transform (forward and backward along
+// x0, then along x1) are register-to-register: 2·(N1·2(N0-1) + N0·2(N1-1)) merges per row.  Exact fixed point as
+// in mioc_sdt.hip: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) with the source coordinates x0 | x1 << 3 in the 6 low
+// mantissa bits and bit 6 as the near-tie flag (g = 2^7 ulp(base)); a unit step costs exactly 1.0; a merge of two
+// candidate sets whose values differ by <= tol sets the flag.  An unflagged winner j* beats every other source by
+// more than tol, so it is the reference's unique argmin and the output is R(l, j*) = fl(fl(T1_l + fl(β·d)) + Ψ_j*)
+// evaluated with the reference's expression (K_l[d] = fl(T1_l + fl(β·d)) is a per-step table).  Flagged targets,
+// rows whose value range leaves the binade, and waves whose rows have at most FSP_FEW targets each run the
+// reference loop (HelpFunctions.jl:60-77) exactly.  Results are bit-identical to the reference in every case.
+// ==============================================================================================================
+constexpr int FSP_FLAG = 64;       // near-tie flag (payload bit 6)
+constexpr int FSP_FEW_PAIRS = 8;   // a wave with at most this many (row, target) pairs scans them exactly
+
+
+
+__device__ __forceinline__ double fsp_merge(double a, double t, double tol) {
+  const double m = fu_min(a, t);
+  const bool close = fabs(a - t) <= tol;
+  return __hiloint2double(__double2hiint(m), __double2loint(m) | (close ? FSP_FLAG : 0));
+}
+
+struct FspLayout {
+  int FS, ND;
+  size_t off_f1, off_K, bytes;
+};
+__host__ __device__ inline FspLayout fsp_layout(int N0, int N1, int B) {
+  FspLayout f;
+  const int L = N0 * N1;
+  f.FS = (L + 1) | 1;  // odd row stride (8-byte words, a pad column at index L): a wave's ds_read_b64 /
+                       // ds_write_b64 of 64 rows is conflict-free
+  f.ND = N0 + N1 - 1;
+  size_t o = (size_t)(B + 1) * f.FS * sizeof(double);
+  o = (o + 15) / 16 * 16;
+  f.off_f1 = o;  // the second front buffer
+  o += (size_t)(B + 1) * f.FS * sizeof(double);
+  o = (o + 15) / 16 * 16;
+  f.off_K = o;  // K_l[d], double-buffered by step parity
+  o += 2 * (size_t)L * f.ND * sizeof(double);
+  f.bytes = (o + 15) / 16 * 16;
+  return f;
+}
+
+// b̃(l) = |ν0(l) - u0| + |ν1(l) - u1| for the integer u_old coordinates of the step (clamped: a far off-grid
+// entry only ever means "beyond every budget"); wave-uniform, so it lives in SGPRs
+__device__ __forceinline__ int fsp_uint(double u) { return (int)fmin(fmax(u, -1.0e8), 1.0e8); }
+
+// Double-buffered front (Φ_{i+1} read, Φ_i written), so every output goes to LDS the moment it is known and
+// a step needs one barrier; one workgroup per CU (the two fronts fill its LDS).
+template <int N0, int N1>
+__global__ __launch_bounds__(512, 2) void k_fsep_run(ProblemDev P, LevelsDev Lv, int base0, int base1,
+                                                     double *__restrict__ front0_all, size_t front_stride,
+                                                     uint8_t *__restrict__ U_all, size_t u_stride_k,
+                                                     int32_t *__restrict__ counters) {
+  constexpr int L = N0 * N1, SMAX = N0 + N1 - 2;
+  constexpr int FS = (L + 1) | 1, ND = SMAX + 1;  // odd row stride with a pad column (index L)
+  extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+  const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nthr = blockDim.x;
+  const int nw = nthr >> 6;
+  const int B = P.B, R = B + 1, nt = P.nt;
+  const FspLayout F = fsp_layout(N0, N1, B);
+  // (pointer arithmetic on the LDS array itself -- a pointer picked from a private array would lose the LDS
+  // address space and turn every front access into a flat load / store)
+  double *const fbase = reinterpret_cast<double *>(fsm);
+  const int f1off = (int)(F.off_f1 / sizeof(double));
+  double *Ktb = reinterpret_cast<double *>(fsm + F.off_K);
+  const int cp = 64 * w + lane;
+  const bool act = cp < R;
+  const int room = act ? B - cp : -1;   // target l is inside the trust region iff b̃_l <= room
+  const int cps = act ? cp : 0;         // rows past B read row 0: they have no targets
+  const int padw = (act ? cp : cp % R) * FS + L;  // this lane's pad slot: the target of a masked-off write
+  const double beta = Lv.beta, inv = Lv.inv_beta;
+  // |T1| bound over the step's targets is folded into qmax per step: Σ_m |a_m|·max|ν_m|
+  const double numx0 = (double)max(abs(base0), abs(base0 + N0 - 1)),
+               numx1 = (double)max(abs(base1), abs(base1 + N1 - 1));
+  const bool prep_wave = w == nw - 1;  // the last wave (the fewest rows) builds the per-step table
+
+  // per-step table, HelpFunctions.jl:52-67: K_l[d] = fl(T1(l) + fl(β·d)), double-buffered by step parity
+  auto prepare = [&](double a0, double a1, int buf) {
+    double *K = Ktb + buf * (L * ND);
+    for (int e = lane; e < L * ND; e += 64) {
+      const int l = e / ND, d = e - l * ND;
+      const double t1 = (0.0 + a0 * (double)(base0 + l % N0)) + a1 * (double)(base1 + l / N0);
+      K[e] = t1 + beta * (double)d;
+    }
+  };
+  auto inputs = [&](int s, double &a0, double &a1, double &u0, double &u1) {
+    const double *dfs = P.df + ((size_t)k * nt + s) * 2;
+    const double *uos = P.uold + ((size_t)k * nt + s) * 2;
+    a0 = P.dt * dfs[0];
+    a1 = P.dt * dfs[1];
+    u0 = uos[0];
+    u1 = uos[1];
+  };
+  // ---- terminal step (HelpFunctions.jl:27-43) into the buffer step nt-2 reads ------------------------------
+  double ca0 = 0.0, ca1 = 0.0;  // Δt·df of the current step (the tolerance's |T1| bound)
+  int cu0 = 0, cu1 = 0;         // u_old of the current step (integer coordinates, b̃)
+  {
+    double a0, a1, u0, u1;
+    inputs(nt - 1, a0, a1, u0, u1);
+    const int iu0 = fsp_uint(u0), iu1 = fsp_uint(u1);
+    double *ft = fbase + ((nt - 1) & 1) * f1off;
+    for (int e = tid; e < R * FS; e += nthr) {
+      const int c = e / FS, l = e - c * FS;
+      double v = INFINITY;
+      if (l < L && abs(base0 + l % N0 - iu0) + abs(base1 + l / N0 - iu1) == c)
+        v = (0.0 + a0 * (double)(base0 + l % N0)) + a1 * (double)(base1 + l / N0);
+      ft[e] = v;
+    }
+    if (nt >= 2) {
+      inputs(nt - 2, a0, a1, u0, u1);
+      if (prep_wave) prepare(a0, a1, (nt - 2) & 1);
+      ca0 = a0;
+      ca1 = a1;
+      cu0 = fsp_uint(u0);
+      cu1 = fsp_uint(u1);
+    }
+  }
+  __syncthreads();
+  uint8_t *Uk = U_all + (size_t)k * u_stride_k;
+  int nflag = 0, nscan = 0;
+#if defined(MIOC_STAMPS)
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+#pragma nounroll
+  for (int i = nt - 2; i >= 0; --i) {
+    const double *fin_ = fbase + ((i + 1) & 1) * f1off;  // Φ_{i+1}
+    double *fout = fbase + (i & 1) * f1off;               // Φ_i
+    const double *Kt = Ktb + (i & 1) * (L * ND);
+    // b̃ of every target, in SGPRs for the whole step
+    const int su0 = __builtin_amdgcn_readfirstlane(cu0), su1 = __builtin_amdgcn_readfirstlane(cu1);
+    auto btof = [&](int l) { return abs(base0 + l % N0 - su0) + abs(base1 + l / N0 - su1); };
+    // U_i[l][c] through a buffer resource: 32-bit offsets (no per-target 64-bit address arithmetic for the
+    // compiler to hoist into VGPRs), bounds-checked to the step's L·R bytes: a store at an offset past them is
+    // dropped, which makes every U store branch-free
+    const __amdgpu_buffer_rsrc_t Ur =
+        __builtin_amdgcn_make_buffer_rsrc(Uk + (size_t)i * ((size_t)L * R), 0, L * R, 0x00020000);
+    double na0 = 0.0, na1 = 0.0, nu0 = 0.0, nu1 = 0.0;
+    if (i >= 1) inputs(i - 1, na0, na1, nu0, nu1);  // the next step's inputs
+    FU_T(q0);
+    unsigned long long scan = 0;  // targets resolved by the exact scan
+    // (row, target) pairs of this wave inside the trust region: a wave with very few (the rows next to B)
+    // resolves them all by exact scans instead of running the transform
+    int npairs = 0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) npairs += min(max(B - 64 * w - btof(l) + 1, 0), 64);
+    if (npairs <= FSP_FEW_PAIRS) {
+#pragma unroll
+      for (int l = 0; l < L; ++l) scan |= (unsigned long long)((unsigned)(btof(l) - room - 1) >> 31) << l;
+    } else {
+    // ---- this lane's row of Φ_{i+1} -----------------------------------------------------------------------
+    double o[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) o[j] = fin_[cps * FS + j];
+    const double a0 = ca0, a1 = ca1;
+    // ---- row statistics over the finite sources ------------------------------------------------------------
+    double pmn = o[0], pmx = o[0];
+#pragma unroll
+    for (int j = 1; j < L; ++j) {
+      pmn = fu_min(pmn, o[j]);
+      pmx = fmax(pmx, o[j]);
+    }
+    const bool infrow = !(pmx < INFINITY);
+    if (__ballot(infrow && pmn < INFINITY)) {  // some sources unreachable: the maximum over the finite ones
+      pmx = pmn;
+#pragma unroll
+      for (int j = 0; j < L; ++j) pmx = fmax(pmx, o[j] < INFINITY ? o[j] : pmn);
+    }
+    // ---- the binade: values base + (Ψ - Ψmin)/β + d lie in [base, 2·base), grid g = 2^7 ulp(base) ---------
+    const double rs = (pmx - pmn) * inv + (double)SMAX;
+    const bool scale_ok = rs < 0x1p36;
+    const int E = ilogb(fmin(rs, 0x1p36) * (1.0 + 0x1p-20) + 1.0) + 2;
+    const double base = ldexp(1.0, E), g = ldexp(1.0, E - 45);
+    const double qmax = beta * (double)SMAX + fmax(fabs(pmn), fabs(pmx)) + fabs(a0) * numx0 + fabs(a1) * numx1;
+    // 2 x stamping error (< g) + 2 x the reference's rounding (<= 4u·qmax per candidate), in units of β
+    const double tol = 3.0 * g + 0x1p-49 * qmax * inv;
+    const bool none = !(pmn < INFINITY);
+    const bool direct = !none && !(scale_ok && tol < 0.25);
+    if (none) pmn = 0.0;  // every source +Inf: stamps stay +Inf (no NaN), payload 0
+    // ---- stamp: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) | x0 | x1 << 3 -------------------------------------------
+    const bool anyinf = __ballot(infrow) != 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const double y = (o[j] - pmn) * inv + base;
+      const int hi = __double2hiint(y);
+      int lo = (__double2loint(y) & ~(2 * FSP_FLAG - 1)) | ((j % N0) | (j / N0) << 3);
+      if (anyinf) lo = hi == 0x7FF00000 ? 0 : lo;  // +Inf stays +Inf (payload bits would make it a NaN)
+      o[j] = __hiloint2double(hi, lo);
+    }
+    FU_T(q1);
+    FU_ACC(0, q0, q1);
+    // ---- pass over x0 (lines of N0 along each x1), then over x1 --------------------------------------------
+#pragma unroll
+    for (int x1 = 0; x1 < N1; ++x1) {
+#pragma unroll
+      for (int x0 = 1; x0 < N0; ++x0)
+        o[x1 * N0 + x0] = fsp_merge(o[x1 * N0 + x0], o[x1 * N0 + x0 - 1] + 1.0, tol);
+#pragma unroll
+      for (int x0 = N0 - 2; x0 >= 0; --x0)
+        o[x1 * N0 + x0] = fsp_merge(o[x1 * N0 + x0], o[x1 * N0 + x0 + 1] + 1.0, tol);
+    }
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) {
+#pragma unroll
+      for (int x1 = 1; x1 < N1; ++x1)
+        o[x1 * N0 + x0] = fsp_merge(o[x1 * N0 + x0], o[(x1 - 1) * N0 + x0] + 1.0, tol);
+#pragma unroll
+      for (int x1 = N1 - 2; x1 >= 0; --x1)
+        o[x1 * N0 + x0] = fsp_merge(o[x1 * N0 + x0], o[(x1 + 1) * N0 + x0] + 1.0, tol);
+    }
+    FU_T(q2);
+    FU_ACC(1, q1, q2);
+    // ---- targets: Φ_i[c' + b̃_l, l] = R(l, j*) = fl(fl(T1_l + fl(β·d)) + Ψ_j*) for the winner j*, written at once
+    // with U (a target outside the trust region writes the lane's pad slot).  Flags are only OR-ed here; a
+    // flagged target, or any target of a row outside the binade, is rewritten by the exact scan below (same
+    // wave, program order, for the LDS cell and for the U byte) -----------------------------------------------
+    int flagacc = 0;
+    const int cpFS = cp * FS;
+#pragma unroll
+    for (int x1 = 0; x1 < N1; ++x1) {  // one grid line of N0 targets: its 2·N0 LDS gathers issue together
+      double kv[N0], pv[N0];
+      int jv[N0];
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        const int l = x1 * N0 + x0;
+        const int lo = __double2loint(o[l]);
+        const unsigned pb = (unsigned)(lo & 7) | ((unsigned)(lo & 0x38) << 5);  // x0, x1 one byte each
+        jv[x0] = (lo & 7) + N0 * ((unsigned)(lo >> 3) & 7u);
+        const int d = (int)__builtin_amdgcn_sad_u8(pb, (unsigned)(x0 | x1 << 8), 0u);
+        kv[x0] = Kt[l * ND + d];
+        pv[x0] = fin_[cps * FS + jv[x0]];
+      }
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        const int l = x1 * N0 + x0;
+        const int b = btof(l);
+        const bool valid = b <= room;
+        const bool ok = valid && o[l] < INFINITY;
+        flagacc |= __double2loint(o[l]);
+        fout[valid ? cpFS + (b * FS + l) : padw] = ok ? kv[x0] + pv[x0] : INFINITY;
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)jv[x0], Ur, ok ? cp + b : 0x40000000, l * R, 0);
+      }
+    }
+    if (__ballot(!none && (direct || (flagacc & FSP_FLAG)))) {  // rare: list the targets for the exact scan
+      const unsigned lanemode = none ? 0u : (direct ? 1u : 2u);
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        const unsigned valid = (unsigned)(btof(l) - room - 1) >> 31;
+        const int lo = __double2loint(o[l]);
+        const unsigned fin = valid & (lanemode >> 1) & (unsigned)(o[l] < INFINITY);
+        const unsigned flg = ((unsigned)lo >> 6) & 1u;
+        scan |= (unsigned long long)((valid & (lanemode & 1u)) | (fin & flg)) << l;
+      }
+      nflag += lanemode == 2u ? __popcll(scan) : 0;
+    }
+    FU_T(q3i);
+    FU_ACC(2, q2, q3i);
+    }
+    FU_T(q3);
+    nscan += __popcll(scan);
+    // ---- exact scans, one (row, target) pair at a time across the wave: lane j evaluates source j with the
+    // reference's expression (HelpFunctions.jl:60-77), then a (value, rank) minimum over the lanes, ties to the
+    // lower rank -----------------------------------------------------------------------------------------------
+    if (__ballot(scan != 0)) {
+#pragma unroll 1
+      for (int l = 0; l < L; ++l) {
+        unsigned long long rows = __ballot((scan >> l) & 1);
+        if (rows) {
+          const int dj = abs(lane % N0 - l % N0) + abs(lane / N0 - l / N0);
+          const double kl = lane < L ? Kt[l * ND + min(dj, SMAX)] : INFINITY;
+          const int bl = abs(base0 + l % N0 - su0) + abs(base1 + l / N0 - su1);
+          while (rows) {
+            const int r = __builtin_ctzll(rows);
+            rows &= rows - 1;
+            const int rowr = 64 * w + r;  // the source row of lane r
+            double bv = lane < L ? kl + fin_[rowr * FS + min(lane, L - 1)] : INFINITY;
+            int bj = lane < L && bv < INFINITY ? lane : 0xFF;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+              const double ov = __shfl_xor(bv, off);
+              const int oj = __shfl_xor(bj, off);
+              if (ov < bv || (ov == bv && oj < bj)) {
+                bv = ov;
+                bj = oj;
+              }
+            }
+            if (lane == 0) {
+              fout[(rowr + bl) * FS + l] = bv;
+              __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bj, Ur, bv < INFINITY ? rowr + bl : 0x40000000,
+                                                   l * R, 0);
+            }
+          }
+        }
+      }
+    }
+    // ---- cells below the target's own budget class: +Inf (target l by wave l % nw) ------------------------
+#pragma unroll 1
+    for (int l = w; l < L; l += nw) {
+      const int b = min(btof(l), R);
+      for (int c = lane; c < b; c += 64) fout[c * FS + l] = INFINITY;
+    }
+    if (i >= 1 && prep_wave) prepare(na0, na1, (i - 1) & 1);
+    ca0 = na0;
+    ca1 = na1;
+    cu0 = fsp_uint(nu0);
+    cu1 = fsp_uint(nu1);
+    FU_T(q5);
+    FU_ACC(3, q3, q5);
+    fu_lds_barrier();  // Φ_i complete: the next step reads it
+    FU_T(q6);
+    FU_ACC(4, q5, q6);
+    FU_ACC(7, q0, q6);
+  }
+#if defined(MIOC_STAMPS)
+  if (lane == 0)  // per wave: block k, wave w at (8k + w) mod 4096
+    for (int q = 0; q < 8; ++q) g_fu_stamps[(8 * k + w) & 4095][q] = acc[q];
+#endif
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    nflag += __shfl_xor(nflag, off);
+    nscan += __shfl_xor(nscan, off);
+  }
+  if (lane == 0 && (nflag | nscan)) {  // diagnostics: [0] near-tie targets, [1] targets of rows out of the binade
+    atomicAdd(&counters[0], nflag);
+    atomicAdd(&counters[1], nscan - nflag);
+  }
+  // ---- Φ_0 to HBM in the generic layout [L][RP] (the backtrack's argmin reads it) --------------------------
+  const double *f0s = fbase;
+  double *f0 = front0_all + (size_t)k * front_stride;
+  for (int e = tid; e < L * P.RP; e += nthr) {
+    const int l = e / P.RP, c = e - l * P.RP;
+    f0[e] = c < R ? f0s[c * FS + l] : INFINITY;
+  }
+}
+
+bool fsep_supported(const PyrGeom &G, int B, size_t *lds_out, int *threads_out) {
+  if (G.M != 2 || B < 0 || B + 1 > 512) return false;
+  const int n0 = G.n[0], n1 = G.n[1];
+  const bool shape = (n0 == 6 && n1 == 6) || (n0 == 4 && n1 == 4) || (n0 == 8 && n1 == 8) || (n0 == 8 && n1 == 4);
+  if (!shape) return false;
+  const FspLayout F = fsp_layout(n0, n1, B);
+  if (F.bytes > 160 * 1024) return false;
+  if (lds_out) *lds_out = F.bytes;
+  if (threads_out) *threads_out = 64 * ((B + 1 + 63) / 64);
+  return true;
+}
+
+int fused_blocks_per_cu(int algo_sep, const PyrGeom &G, int L, int B) {
+  int n = 0;
+  size_t lds = 0;
+  int thr = 512;
+  if (algo_sep) {
+    if (!fsep_supported(G, B, &lds, &thr)) return 0;
+    const void *f = G.n[0] == 6 ? (const void *)k_fsep_run<6, 6> : G.n[0] == 4 ? (const void *)k_fsep_run<4, 4>
+                    : G.n[1] == 8 ? (const void *)k_fsep_run<8, 8> : (const void *)k_fsep_run<8, 4>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, thr, lds) != hipSuccess) return 0;
+  } else {
+    if (!fused_supported(L, B, &lds)) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void *)k_fused_run<36>, 512, lds) != hipSuccess) return 0;
+  }
+  return n;
+}
+
+hipError_t launch_fsep_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, double *front0,
+                           size_t front_stride, uint8_t *U, size_t u_stride_k, int32_t *counters) {
+  size_t lds = 0;
+  int thr = 0;
+  if (!fsep_supported(G, P.B, &lds, &thr)) return hipErrorInvalidValue;
+  if (P.M != 2) return hipErrorInvalidValue;
+#define FSP_LAUNCH(A, Bv)                                                                                          \
+  hipLaunchKernelGGL((k_fsep_run<A, Bv>), dim3(P.K), dim3(thr), lds, s, P, Lv, G.base[0], G.base[1], front0,       \
+                     front_stride, U, u_stride_k, counters)
+  if (G.n[0] == 6)
+    FSP_LAUNCH(6, 6);
+  else if (G.n[0] == 4)
+    FSP_LAUNCH(4, 4);
+  else if (G.n[1] == 8)
+    FSP_LAUNCH(8, 8);
+  else
+    FSP_LAUNCH(8, 4);
+#undef FSP_LAUNCH
+  return hipGetLastError();
 }
 
 bool fused_supported(int L, int B, size_t *lds_out) {
@@ -312,5 +761,14 @@ hipError_t launch_fused_run(hipStream_t s, const ProblemDev &P, const LevelsDev 
 #undef FU_LAUNCH
   return hipGetLastError();
 }
+
+#if defined(MIOC_STAMPS)
+extern "C" int32_t mioc_debug_fused_stamps(unsigned long long *out, int64_t nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fu_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long)) ==
+                 hipSuccess
+             ? 0
+             : -4;
+}
+#endif
 
 }  // namespace mioc

@@ -109,6 +109,11 @@ hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev
 bool fused_supported(int L, int B, size_t *lds_out);
 hipError_t launch_fused_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, double *front0,
                             size_t front_stride, uint8_t *U, size_t u_stride_k);
+// p = 1 on a 2-D product grid of consecutive levels: the fused DP with the separable L1 transform
+bool fsep_supported(const PyrGeom &G, int B, size_t *lds_out, int *threads_out);
+int fused_blocks_per_cu(int algo_sep, const PyrGeom &G, int L, int B);  // occupancy query (diagnostics [7])
+hipError_t launch_fsep_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, double *front0,
+                           size_t front_stride, uint8_t *U, size_t u_stride_k, int32_t *counters);
 
 // ---- p = Inf collapse (mioc_pinf.hip) -----------------------------------------------------------
 struct PinfDev {
@@ -172,6 +177,7 @@ struct mioc_ctx {
 
   // pyramid (p = 1, product grid, unit gaps)
   bool pyr_ok = false;
+  bool grid_ok = false;            // product grid of consecutive integer levels in grid order (PyrGeom valid)
   mioc::PyrGeom pyr;
   double *d_stage = nullptr;       // [2][K][B+1][L] source-row-major fronts, each row in sphere order
   size_t stage_cap = 0;
@@ -183,6 +189,7 @@ struct mioc_ctx {
   int32_t *h_run_err = nullptr;    // pinned copy of err
   bool run_pending = false;
   int32_t *d_counters = nullptr;   // [8] diagnostics: value-collision targets, multi-level targets, ...
+  int64_t occupancy = 0;           // diagnostics [7]: resident workgroups per CU of the last fused launch
 
   // generic buffers
   double *d_front = nullptr;       // [2][K][L][RP]

@@ -28,7 +28,7 @@ MIOC_ENONFINITE = -7
 MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
 MIOC_OPT_ALGO, MIOC_OPT_TIMING, MIOC_OPT_PERSIST = 1, 2, 3
 MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID, MIOC_ALGO_SEPARABLE = 0, 1, 2, 3, 4
-MIOC_ALGO_FUSED = 5
+MIOC_ALGO_FUSED, MIOC_ALGO_FUSED_SEPARABLE = 5, 6
 
 EXPORTED = [
     "mioc_version", "mioc_create", "mioc_destroy", "mioc_last_error", "mioc_set_option", "mioc_set_levels",
@@ -295,7 +295,24 @@ def fused_eligible(L, B):
     if nrb * L > 8 * 24:
         return False
     o = (R * (LP + 2) * 8 + 15) // 16 * 16 + 2 * L * LP * 8 + 2 * LP * 4 + 2 * 8 * 24 * 2
-    return (o + 15) // 16 * 16 + 16 <= 160 * 1024
+    return (o + 15) // 16 * 16 + 16 + L * 8 * 8 <= 160 * 1024
+
+
+def fused_separable_eligible(levels: LevelTable, B):
+    """Mirror of the library's fused separable domain (p = 1 and beta > 0 are checked by the library): a 2-D
+    product grid of consecutive integer levels of shape 6x6, 4x4, 8x8 or 8x4, both fronts in one CU's LDS."""
+    if levels.M != 2 or not (0 <= B < 512) or levels.L != int(np.prod(levels.counts)):
+        return False
+    n0, n1 = int(levels.counts[0]), int(levels.counts[1])
+    if (n0, n1) not in ((6, 6), (4, 4), (8, 8), (8, 4)):
+        return False
+    FS = (n0 * n1 + 1) | 1  # two fronts of (B+1) rows + the per-step K table (double-buffered) in 160 KiB of LDS
+    if 2 * (((B + 1) * FS * 8 + 15) // 16 * 16) + 2 * n0 * n1 * (n0 + n1 - 1) * 8 > 160 * 1024:
+        return False
+    strides = np.cumprod(np.concatenate([[1], levels.counts[:-1]]))
+    if not np.array_equal(((levels.tuples - 1) * strides).sum(axis=1), np.arange(levels.L)):
+        return False
+    return all(list(v) == list(range(v[0], v[0] + len(v))) for v in levels.nu)
 
 
 def separable_eligible(levels: LevelTable):

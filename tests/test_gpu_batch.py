@@ -56,10 +56,10 @@ def test_c5_batch_1024_fused_equals_generic():
     lt, _, _, ddf, duo = _batch(cfg, 1024)
     B = cfg.B
     res = {}
-    for algo in (native.MIOC_ALGO_AUTO, native.MIOC_ALGO_GENERIC):
+    for algo in (native.MIOC_ALGO_AUTO, native.MIOC_ALGO_FUSED, native.MIOC_ALGO_GENERIC):
         ctx, u, phi, st = _run(lt, cfg, algo, ddf, duo, B, B)
         if algo == native.MIOC_ALGO_AUTO:
-            assert ctx.last_algo() == native.MIOC_ALGO_FUSED
+            assert ctx.last_algo() == native.MIOC_ALGO_FUSED_SEPARABLE
         assert np.all(st == 0)
         import torch
         du = torch.empty_like(ddf)
@@ -68,20 +68,23 @@ def test_c5_batch_1024_fused_equals_generic():
         ctx.synchronize()
         res[algo] = (u, phi, du.cpu().numpy(), dphi.cpu().numpy())
         ctx.close()
-    a, g = res[native.MIOC_ALGO_AUTO], res[native.MIOC_ALGO_GENERIC]
-    for x, y in zip(a, g):
-        bad = np.flatnonzero([not np.array_equal(p, q) for p, q in zip(x, y)])
-        assert bad.size == 0, f"restarts {bad[:8]} differ"
+    g = res[native.MIOC_ALGO_GENERIC]
+    for algo in (native.MIOC_ALGO_AUTO, native.MIOC_ALGO_FUSED):
+        for x, y in zip(res[algo], g):
+            bad = np.flatnonzero([not np.array_equal(p, q) for p, q in zip(x, y)])
+            assert bad.size == 0, f"algo {algo}: restarts {bad[:8]} differ"
 
 
+@pytest.mark.parametrize("algo", ["fused", "fused_separable"])
 @pytest.mark.parametrize("k0", [0, 517])
-def test_c5_batch_restarts_vs_oracle(oracle_c, k0):
+def test_c5_batch_restarts_vs_oracle(oracle_c, k0, algo):
     """Seeded restarts of a 1024-batch at full nt = 4096, B = 256 against the CPU oracle: u and Φ* at B and
     B/2, and every U cell the reference writes on 64 sampled steps."""
     cfg = CONFIGS["C5"]
     K = 1024
     lt, dfs, uos, ddf, duo = _batch(cfg, K)
-    ctx, u, phi, st = _run(lt, cfg, native.MIOC_ALGO_FUSED, ddf, duo, cfg.B, cfg.B)
+    algo = {"fused": native.MIOC_ALGO_FUSED, "fused_separable": native.MIOC_ALGO_FUSED_SEPARABLE}[algo]
+    ctx, u, phi, st = _run(lt, cfg, algo, ddf, duo, cfg.B, cfg.B)
     lv = Levels(lt.nu, [tuple(int(x) for x in t) for t in lt.tuples])
     rng = np.random.default_rng(k0)
     picks = sorted({k0 + int(x) for x in rng.integers(0, 512, size=4)} | {k0})
@@ -112,13 +115,15 @@ def _halved(ctx, ddf, Bp):
     return du.cpu().numpy(), dphi.cpu().numpy(), dst.cpu().numpy()
 
 
-@pytest.mark.parametrize("mode", ["zero", "integer", "outside"])
-def test_fused_tie_heavy_and_off_grid_vs_oracle(oracle_c, mode):
+@pytest.mark.parametrize("algo", ["fused", "fused_separable"])
+@pytest.mark.parametrize("mode", ["zero", "integer", "outside", "steep"])
+def test_fused_tie_heavy_and_off_grid_vs_oracle(oracle_c, mode, algo):
     """Batches whose DP is dominated by exact ties (zero / integer gradients) or whose u_old leaves the level
     grid (integral, not admissible): the fused DP against the oracle, restart by restart, every U cell."""
     cfg = CONFIGS["C5"]
     K, nt, B = 5, 80, 40
-    rng = np.random.default_rng({"zero": 1, "integer": 2, "outside": 3}[mode])
+    rng = np.random.default_rng({"zero": 1, "integer": 2, "outside": 3, "steep": 4}[mode])
+    beta = 1e-13 if mode == "steep" else cfg.beta  # value spread ~1e13 beta: rows leave the transform's binade
     lt = cfg.levels()
     lv = Levels(lt.nu, [tuple(int(x) for x in t) for t in lt.tuples])
     dfs, uos = [], []
@@ -128,6 +133,8 @@ def test_fused_tie_heavy_and_off_grid_vs_oracle(oracle_c, mode):
             df = np.zeros_like(df)
         elif mode == "integer":
             df = rng.integers(-3, 4, size=df.shape).astype(float)
+        elif mode == "steep":
+            df = df * 1e3
         else:
             uo = uo.copy()
             for i in rng.choice(nt, size=10, replace=False):
@@ -137,9 +144,17 @@ def test_fused_tie_heavy_and_off_grid_vs_oracle(oracle_c, mode):
     import torch
     ddf = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in dfs])), dtype=torch.float64, device="cuda")
     duo = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in uos])), dtype=torch.float64, device="cuda")
-    ctx, u, phi, st = _run(lt, cfg, native.MIOC_ALGO_FUSED, ddf, duo, B, B)
+    algo = {"fused": native.MIOC_ALGO_FUSED, "fused_separable": native.MIOC_ALGO_FUSED_SEPARABLE}[algo]
+    import dataclasses
+    ctx, u, phi, st = _run(lt, dataclasses.replace(cfg, beta=beta), algo, ddf, duo, B, B)
+    diag = ctx.diagnostics()
+    if algo == native.MIOC_ALGO_FUSED_SEPARABLE:
+        if mode in ("zero", "integer"):
+            assert diag[0] > 0, diag  # targets with a near-tie winner went to the exact scan
+        if mode == "steep":
+            assert diag[1] > 0, diag  # rows outside the binade went to the exact scan
     for k in range(K):
-        ophi, oU = oracle_c.bellman(lv, dfs[k], uos[k], B, P_ONE, cfg.beta, cfg.dt)
+        ophi, oU = oracle_c.bellman(lv, dfs[k], uos[k], B, P_ONE, beta, cfg.dt)
         ou, ops = oracle_c.backtrack(lv, uos[k], ophi, oU, B, B)
         assert np.array_equal(u[k].T, ou) and phi[k] == ops, f"{mode} restart {k}"
         for i in range(nt - 1):

@@ -36,6 +36,8 @@ def _oracle_levels(lt):
 
 def _algos(p_kind, lt=None, B=None):
     fused = (native.MIOC_ALGO_FUSED,) if lt is not None and B is not None and native.fused_eligible(lt.L, B) else ()
+    if p_kind == P_ONE and lt is not None and B is not None and native.fused_separable_eligible(lt, B):
+        fused += (native.MIOC_ALGO_FUSED_SEPARABLE,)
     if p_kind == P_INF:
         return ALGOS_PINF + fused
     if p_kind == P_ONE and lt is not None and native.separable_eligible(lt):
@@ -167,7 +169,7 @@ def test_full_size_c5_restart_vs_oracle(oracle_c):
     lv = _oracle_levels(lt)
     phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_ONE, cfg.beta, cfg.dt)
     ou, ops = oracle_c.backtrack(lv, uo, phi, U, cfg.B, cfg.B)
-    for algo in (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_FUSED):
+    for algo in (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_FUSED, native.MIOC_ALGO_FUSED_SEPARABLE):
         ctx = _ctx(lt, P_ONE, cfg.beta, algo)
         ctx.bellman(df, uo, cfg.B, cfg.dt)
         u, ps, _ = ctx.backtrack(cfg.B)
@@ -289,7 +291,7 @@ def test_batch_device_api_equals_single():
         _, df, uo = make_inputs(cfg, k=k, nt=nt, levels=lt)
         dfs.append(df)
         uos.append(uo)
-    for pk, algos in ((P_ONE, (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_FUSED)),
+    for pk, algos in ((P_ONE, (native.MIOC_ALGO_GENERIC, native.MIOC_ALGO_FUSED, native.MIOC_ALGO_FUSED_SEPARABLE)),
                       (P_INF, ALGOS_PINF + (native.MIOC_ALGO_FUSED,))):
         for algo in algos:
             ctx = _ctx(lt, pk, cfg.beta, algo)
