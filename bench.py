@@ -3,19 +3,31 @@
 A "step" is one pass of the hot path over one batch of synthetic input: per rank, `--batch`
 independent subproblems (default 1), each a full bellman_TRM! (DP over nt=65536 steps x 4096 levels
 x B+1=257 budget rows) followed by eval_u_TRM! (backtrack), inputs already resident in HBM.
-Multi-GPU (torchrun, one process per GPU): the problem descriptor is broadcast once over RCCL, each
-rank solves its own restarts (weak scaling, no data-path collective) and the controls (as uint16
-level ranks) plus Φ* are gathered to rank 0 over RCCL at the end of every step.
 
-Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel, measured with HIP events on
-the library's stream; `roofline_valu` gives the FP64-VALU view (the p=1 sweep is VALU-bound);
-`cpu_baseline` times the C restatement of the reference loop (oracle/) on a bounded sample.
+Alongside the headline it measures the batch config C5 (`batch`: `--batch-size` random restarts of the
+36-level heat-shaped subproblem per GPU, the fused small-state DP) and the p=Inf variant of C4.
+
+Multi-GPU: `python bench.py --gpus N` launches N ranks itself (one process per GPU, before anything
+touches a GPU); under torchrun it uses the given RANK / WORLD_SIZE.  The problem descriptor is broadcast
+once over RCCL, each rank solves its own block of every step's global batch (weak scaling: the per-GPU
+work is fixed, no data-path collective), and the controls (uint16 level ranks from the library) plus Φ*
+are gathered to rank 0 over RCCL at the end of every step.  `value` = subproblems of all ranks / the
+max-over-ranks time.
+
+Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel, measured with HIP events on the
+library's stream; `roofline_valu` gives the FP64-VALU view; `cpu_baseline` times the C restatement of the
+reference loop (oracle/) on a bounded sample, on this job's host cores.
+
+`--solver oracle --backend gloo` (CPU only, tests): the same launcher, sharding and gather, with the CPU
+oracle as the per-rank solver on truncated inputs -- the product path on GPUs is libmioc.
 """
 import argparse
 import json
 import math
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,21 +40,211 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md
 FP64_VALU_PEAK_TOPS = 39.3     # 256 CU x 64 FP64 lanes/clk x 2.4 GHz (78.6 TFLOP/s counts an FMA as 2)
+METRIC = "bellman_TRM! subproblems/sec (nt=65536, 4096 levels, budget=256) + HBM GB/s"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C4")
     ap.add_argument("--p", default=None, help="override p: 1 or inf")
-    ap.add_argument("--batch", type=int, default=1, help="subproblems per rank per step")
+    ap.add_argument("--batch", type=int, default=1, help="subproblems per rank per step (headline config)")
     ap.add_argument("--nt", type=int, default=None, help="truncate nt (profiling passes only; not a bench line)")
-    ap.add_argument("--variant", default="pinf", help="extra p=Inf line on the same config ('' to skip)")
+    ap.add_argument("--variant", default="pinf", help="extra p=Inf line on the same config ('' or none to skip)")
+    ap.add_argument("--batch-config", default="C5", help="the batch line's config ('none' to skip)")
+    ap.add_argument("--batch-size", type=int, default=1024, help="batch line: subproblems per rank per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=5, help="recursion steps timed for the CPU baseline")
-    return ap.parse_args()
+    ap.add_argument("--cpu-steps", type=int, default=5, help="recursion steps timed for the C4 CPU baseline")
+    ap.add_argument("--solver", default="native", choices=["native", "oracle"],
+                    help="oracle: CPU test double for the launcher / sharding tests (no GPU)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------------------------------------------
+# launcher: one process per GPU, started before anything touches a GPU (no exec from a GPU process)
+# ------------------------------------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args):
+    port = str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
+
+
+# ------------------------------------------------------------------------------------------------------
+# per-rank solvers
+# ------------------------------------------------------------------------------------------------------
+class NativeSolver:
+    """libmioc (the product path): inputs resident in HBM, batched bellman + backtrack, ranks on device."""
+
+    def __init__(self, device, levels, p, beta, torch):
+        from mioc import native
+        self.torch, self.native = torch, native
+        self.device = device
+        self.ctx = native.Context(device)
+        self.ctx.set_levels(levels)
+        self.ctx.set_cost(p, beta)
+        self.ctx.set_option(native.MIOC_OPT_TIMING, 1)
+
+    def load(self, dfs, uos, nsets, K, M):
+        torch = self.torch
+        nt = dfs[0].shape[1]
+        # (sets, K, nt, nx) C-contiguous: each subproblem's nx x nt block column-major (mioc_bellman_batch_device)
+        self.d_df = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in dfs])), dtype=torch.float64,
+                                 device=self.device).reshape(nsets, K, nt, M).contiguous()
+        self.d_uo = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in uos])), dtype=torch.float64,
+                                 device=self.device).reshape(nsets, K, nt, M).contiguous()
+        self.d_u = torch.empty((K, nt, M), dtype=torch.float64, device=self.device)
+        self.d_phi = torch.empty(K, dtype=torch.float64, device=self.device)
+        self.d_st = torch.empty(K, dtype=torch.int32, device=self.device)
+        self.d_rk = torch.empty((K, nt), dtype=torch.int32, device=self.device)
+
+    def solve(self, s, B, dt):
+        self.ctx.bellman_batch_tensors(self.d_df[s], self.d_uo[s], B, dt)
+        self.ctx.backtrack_batch_tensors(B, self.d_u, self.d_phi, self.d_st)
+
+    def results(self):
+        """(level ranks int16 [K, nt], Φ* [K]) on the device, after solve()."""
+        self.ctx.ranks_tensor(self.d_rk)
+        self.ctx.synchronize()
+        return self.d_rk.to(self.torch.int16), self.d_phi
+
+    def sync(self):
+        self.ctx.synchronize()
+        self.torch.cuda.synchronize(self.device)
+
+    def reset(self):
+        self.ctx.reset_stats()
+
+    def finish(self, res):
+        st = self.d_st.cpu().numpy()
+        if np.any(st != 0):
+            raise RuntimeError(f"infeasible subproblem status {st}")
+        dom_ms, dom_n, dom_name = self.ctx.kernel_stats(0)
+        walk_ms, walk_n, _ = self.ctx.kernel_stats(1)
+        res.update(algo=self.ctx.last_algo(), dom_ms=dom_ms, dom_n=dom_n, dom_name=dom_name, walk_ms=walk_ms,
+                   diag=self.ctx.diagnostics(), phi=self.d_phi.cpu().numpy().tolist())
+        self.ctx.close()
+
+
+class OracleSolver:
+    """CPU test double (tests of the launcher / sharding / gather over gloo): the C restatement."""
+
+    def __init__(self, device, levels, p, beta, torch):
+        from oracle.oracle import Levels, OracleC, P_INF, P_ONE
+        self.torch = torch
+        self.oc = OracleC()
+        self.lv = Levels(levels.nu, [tuple(int(x) for x in t) for t in levels.tuples])
+        self.kind = P_INF if p == math.inf else P_ONE
+        self.beta = beta
+        self.nuval = levels.nuval
+
+    def load(self, dfs, uos, nsets, K, M):
+        self.dfs, self.uos, self.K = dfs, uos, K
+
+    def solve(self, s, B, dt):
+        rk, ph = [], []
+        for k in range(self.K):
+            df, uo = self.dfs[s * self.K + k], self.uos[s * self.K + k]
+            phi, U = self.oc.bellman(self.lv, df, uo, B, self.kind, self.beta, dt)
+            u, ps = self.oc.backtrack(self.lv, uo, phi, U, B, B)
+            rk.append([int(np.flatnonzero((self.nuval == u[:, i]).all(axis=1))[0]) for i in range(u.shape[1])])
+            ph.append(ps)
+        self._r = (self.torch.tensor(rk, dtype=self.torch.int16), self.torch.tensor(ph, dtype=self.torch.float64))
+
+    def results(self):
+        return self._r
+
+    def sync(self):
+        pass
+
+    def reset(self):
+        pass
+
+    def finish(self, res):
+        res.update(algo=0, dom_ms=0.0, dom_n=0, dom_name="oracle", walk_ms=0.0, diag=[0] * 8,
+                   phi=self._r[1].numpy().tolist())
+
+
+# ------------------------------------------------------------------------------------------------------
+def run(args, cfg_name, K, p_over, nt_over, rank, world, device, dist, torch, steps, warmup):
+    """One config: `steps` timed + `warmup` untimed steps, each a global batch of world*K subproblems."""
+    from mioc.batch import gather_results, shard
+    from mioc.synth import CONFIGS, make_inputs
+
+    cfg = CONFIGS[cfg_name]
+    p = cfg.p if p_over is None else (math.inf if p_over == "inf" else float(p_over))
+    nt = cfg.nt if nt_over is None else nt_over
+    levels = cfg.levels()
+    B = cfg.B
+    # descriptor: broadcast once from rank 0 (RCCL) -- seeds, sizes, parameters
+    dev = torch.device("cpu") if args.backend == "gloo" else torch.device("cuda", device)
+    desc = torch.tensor([cfg.seed_df, cfg.seed_u, nt, B, cfg.dt, cfg.beta, p if p != math.inf else -1.0],
+                        dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.broadcast(desc, src=0)
+    seed_df, seed_u, nt, B, dt, beta, pv = desc.tolist()
+    nt, B = int(nt), int(B)
+    p = math.inf if pv < 0 else pv
+
+    solver = (NativeSolver if args.solver == "native" else OracleSolver)(device, levels, p, beta, torch)
+    nsets = warmup + steps
+    dfs, uos = [], []
+    lo, hi = shard(world * K, world, rank)  # this rank's contiguous block of each step's global batch
+    for s in range(nsets):
+        for b in range(lo, hi):
+            _, df, uo = make_inputs(cfg, k=s * world * K + b, nt=nt, levels=levels)
+            dfs.append(df)
+            uos.append(uo)
+    solver.load(dfs, uos, nsets, hi - lo, levels.M)
+    gathered = []
+
+    def step(s):
+        solver.solve(s, B, dt)
+        if world > 1:  # controls as level ranks (uint16 payload) + Φ*, gathered to rank 0 over RCCL
+            r, ph = solver.results()
+            gathered.append(gather_results(dist, r, ph, world * K, world, rank))
+
+    for s in range(warmup):
+        step(s)
+    solver.sync()
+    solver.reset()
+    if world > 1:
+        dist.barrier()
+    solver.sync()
+    t0 = time.perf_counter()
+    for s in range(warmup, nsets):
+        step(s)
+    solver.sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    res = dict(config=cfg_name, elapsed=elapsed, K=K, nt=nt, B=B, p=p, levels=levels, uo=uos[-1], steps=steps,
+               world=world)
+    if world > 1 and rank == 0:
+        R, PH = gathered[-1]
+        res["gathered_checksum"] = float(PH.double().sum().item()) + float(R.double().sum().item())
+    elif world == 1:
+        r, ph = solver.results()
+        res["gathered_checksum"] = float(ph.double().sum().item()) + float(r.double().sum().item())
+    solver.finish(res)
+    return res
 
 
 def candidates_per_step(levels, uo, B):
@@ -57,227 +259,225 @@ def candidates_per_step(levels, uo, B):
     return levels.L * tot / max(1, nt - 1)
 
 
-def run(args, rank, world, device, dist, torch):
-    from mioc import native
-    from mioc.batch import gather_results, level_ranks, shard
-    from mioc.synth import CONFIGS, make_inputs
-
-    cfg = CONFIGS[args.config]
-    p = cfg.p if args.p is None else (math.inf if args.p == "inf" else float(args.p))
-    nt = cfg.nt if args.nt is None else args.nt
-    levels = cfg.levels()
-    B = cfg.B
-
-    # descriptor: broadcast once from rank 0 (RCCL) -- seeds, sizes, parameters
-    desc = torch.tensor([cfg.seed_df, cfg.seed_u, nt, B, cfg.dt, cfg.beta, p if p != math.inf else -1.0],
-                        dtype=torch.float64, device=device)
-    if world > 1:
-        dist.broadcast(desc, src=0)
-    seed_df, seed_u, nt, B, dt, beta, pv = desc.tolist()
-    nt, B = int(nt), int(B)
-    p = math.inf if pv < 0 else pv
-
-    ctx = native.Context(device)
-    ctx.set_levels(levels)
-    ctx.set_cost(p, beta)
-    ctx.set_option(native.MIOC_OPT_TIMING, 1)
-
-    K = args.batch
-    nsets = args.warmup + args.steps
-    dfs, uos = [], []
-    lo, hi = shard(world * K, world, rank)  # this rank's contiguous block of each step's global batch
-    for s in range(nsets):
-        for b in range(lo, hi):
-            k = s * world * K + b
-            _, df, uo = make_inputs(cfg, k=k, nt=nt, levels=levels)
-            dfs.append(df)
-            uos.append(uo)
-    # (sets, K, nt, nx) C-contiguous: each subproblem's nx x nt block column-major (mioc_bellman_batch_device)
-    d_df = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in dfs])), dtype=torch.float64,
-                        device=device).reshape(nsets, K, nt, -1).contiguous()
-    d_uo = torch.tensor(np.ascontiguousarray(np.stack([d.T for d in uos])), dtype=torch.float64,
-                        device=device).reshape(nsets, K, nt, -1).contiguous()
-    d_u = torch.empty((K, nt, levels.M), dtype=torch.float64, device=device)
-    d_phi = torch.empty(K, dtype=torch.float64, device=device)
-    d_st = torch.empty(K, dtype=torch.int32, device=device)
-    nuval = torch.tensor(levels.nuval, dtype=torch.float64, device=device)
-
-    def step(s):
-        ctx.bellman_batch_tensors(d_df[s], d_uo[s], B, dt)
-        ctx.backtrack_batch_tensors(B, d_u, d_phi, d_st)
-        if world > 1:
-            ctx.synchronize()
-            # controls as level ranks (uint16 payload) + Φ*, gathered to rank 0 over RCCL
-            gather_results(dist, level_ranks(d_u, nuval), d_phi, world * K, world, rank)
-
-    for s in range(args.warmup):
-        step(s)
-    ctx.synchronize()
-    torch.cuda.synchronize(device)
-    ctx.reset_stats()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for s in range(args.warmup, nsets):
-        step(s)
-    ctx.synchronize()
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    st = d_st.cpu().numpy()
-    if np.any(st != 0):
-        raise RuntimeError(f"rank {rank}: infeasible subproblem status {st}")
-
-    dom_ms, dom_n, dom_name = ctx.kernel_stats(0)
-    walk_ms, walk_n, walk_name = ctx.kernel_stats(1)
-    algo = ctx.last_algo()
-    res = dict(elapsed=elapsed, K=K, nt=nt, B=B, p=p, algo=algo, dom_ms=dom_ms, dom_n=dom_n, dom_name=dom_name,
-               walk_ms=walk_ms, walk_n=walk_n, walk_name=walk_name, levels=levels, uo=uos[-1],
-               phi=d_phi.cpu().numpy().tolist(), diag=ctx.diagnostics())
-    ctx.close()
-    return res
-
-
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/roundN_pmc_traffic.json,
     made by scripts/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None."""
     import glob
     import re
     files = glob.glob(os.path.join(ROOT, "profiles", "round*_pmc_traffic.json"))
-    if not files:
+    found = []
+    for f in files:
+        try:
+            with open(f) as fh:
+                e = json.load(fh)["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if e and "hbm_bytes_per_launch" in e:
+            found.append((int(re.search(r"round(\d+)_", os.path.basename(f)).group(1)), e["hbm_bytes_per_launch"], f))
+    if not found:
         return None, None
-    f = max(files, key=lambda x: int(re.search(r"round(\d+)_", os.path.basename(x)).group(1)))
-    try:
-        with open(f) as fh:
-            e = json.load(fh)["kernels"].get(kernel)
-    except (OSError, ValueError, KeyError):
-        return None, None
-    if not e or "hbm_bytes_per_launch" not in e:
-        return None, None
-    return e["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    _, b, f = max(found)
+    return b, os.path.relpath(f, ROOT)
 
 
-def roofline_of(res, args):
+def roofline_of(res):
     """Algorithmic bytes / flops of the dominant kernel per launch (SURVEY §8 d), over its HIP-event time."""
     lv, B, K, nt = res["levels"], res["B"], res["K"], res["nt"]
-    L = lv.L
+    L, M = lv.L, lv.M
     avg_s = (res["dom_ms"] / 1e3) / max(1, res["dom_n"])
     steps = 1  # DP recursion steps per launch
-    if res["dom_name"] == "k_generic_step":
+    name = res["dom_name"]
+    ncand_step = candidates_per_step(lv, res["uo"], B)
+    note = None
+    if name == "k_generic_step":
         # front in + front out (fp64) + compact U (uint16/uint8) per step, per subproblem
         ub = 1 if L <= 256 else 2
         bytes_per_launch = K * (B + 1) * L * (8 + 8 + ub)
-        ncand = K * candidates_per_step(lv, res["uo"], B)
-        ops = 2.0 * ncand  # one v_add_f64 + one v_min_f64 per candidate
-        roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
-                     "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
-                     "candidates_per_launch": ncand}
-    elif res["dom_name"] in ("k_sdt_step", "k_sdt_run"):
+        ops = 2.0 * K * ncand_step  # one v_add_f64 + one v_min_f64 per candidate
+    elif name in ("k_sdt_step", "k_sdt_run"):
         # the same algorithmic traffic as the reference DP step: front in + front out + compact U, per step;
         # k_sdt_run is one persistent launch over all nt - 1 steps
-        steps = (nt - 1) if res["dom_name"] == "k_sdt_run" else 1
+        steps = (nt - 1) if name == "k_sdt_run" else 1
         bytes_per_launch = steps * K * (B + 1) * L * (8 + 8 + 2)
-        M = lv.M
-        # per pass and 8-point line: 20 merges (7 forward, 6 backward, 7 combine), each add + min + sub + cmp
-        ops = 1.0 * steps * K * (B + 1) * L * M * (20 / 8) * 4
-        ncand = steps * K * candidates_per_step(lv, res["uo"], B)
-        roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
-                     "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
-                     "note": "separable transform FP64 ops (4 per merge); brute-force-equivalent candidates/s "
-                             f"= {ncand / avg_s:.4g}"}
-    elif res["dom_name"] == "k_pyr_step":
-        # the same algorithmic traffic as the reference DP step: front in + front out + compact U
+        # per pass and 8-point line: 14 merges (7 forward, 7 backward), each add + min + sub + cmp (4 FP64 ops)
+        ops = 1.0 * steps * K * (B + 1) * L * M * (14 / 8) * 4
+        note = "separable transform FP64 ops (4 per merge); brute-force-equivalent candidates/s = " \
+               f"{steps * K * ncand_step / avg_s:.4g}"
+    elif name in ("k_fused_run", "k_fsep_run"):
+        # one launch = every step of K subproblems; the value fronts never leave the CU's LDS, so the HBM bytes
+        # the DP must move are U (one byte per cell), df and u_old in, and Φ_0 out for the backtrack's argmin
+        steps = nt - 1
+        bytes_per_launch = K * (steps * (B + 1) * L + nt * M * 16 + L * (B + 1) * 8)
+        if name == "k_fused_run":
+            ops = 2.0 * K * steps * ncand_step  # v_add_f64 + v_min_f64 per candidate
+            note = "min-plus candidates: 2 FP64 ops each"
+        else:
+            n0 = len(lv.nu[0])
+            merges = 2 * (n0 - 1) * L // n0 + 2 * (L // n0 - 1) * L // (L // n0)  # both passes, both sweeps
+            ops = 4.0 * K * steps * (B + 1) * merges
+            note = (f"separable transform FP64 ops ({merges} merges x 4 per row); brute-force-equivalent "
+                    f"candidates/s = {K * steps * ncand_step / avg_s:.4g}")
+        sur = K * (steps * (B + 1) * L * (8 + 8 + 1) + nt * M * 24)
+        note = (note + "; " if note else "") + (
+            f"SURVEY §8 d's Q (fronts through HBM) would be {sur / avg_s / 1e9:.1f} GB/s = "
+            f"{sur / avg_s / 1e9 / HBM_PEAK_GBS:.3f} of peak: the fused DP keeps the fronts in LDS instead")
+    elif name == "k_pyr_step":
         bytes_per_launch = K * (B + 1) * L * (8 + 8 + 2)
-        M = lv.M
         smax = int(sum(max(v) - min(v) for v in lv.nu))
         ops = 1.0 * K * (B + 1) * L * (smax + 1) * (2 * M + 2)  # upper bound: every level, 2M min + 2 add
-        ncand = K * candidates_per_step(lv, res["uo"], B)
-        roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
-                     "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS,
-                     "note": "pyramid ops upper bound (all levels); brute-force-equivalent candidates/s "
-                             f"= {ncand / avg_s:.4g}"}
+        note = "pyramid ops upper bound (all levels)"
     else:
         # k_pinf_recur: one launch per subproblem batch; reads the class table, writes R rows
         bw = int(min(B, sum(max(v) - min(v) for v in lv.nu))) + 1
         bytes_per_launch = K * nt * (bw * 8 + (B + 1) * 8)
         ops = 2.0 * K * (nt - 1) * (B + 1) * bw
-        roof_valu = {"bound": "valu", "achieved": ops / avg_s / 1e12, "peak": FP64_VALU_PEAK_TOPS,
-                     "unit": "TFP64op/s", "frac": ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS}
     ach = bytes_per_launch / avg_s / 1e9
-    traffic, tsrc = pmc_traffic(res["dom_name"])
+    traffic, tsrc = pmc_traffic(name)
     roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None if traffic is None else round(traffic),
-            "traffic_source": tsrc, "kernel": res["dom_name"],
+            "traffic_source": tsrc, "kernel": name,
             "avg_launch_us": round(avg_s * 1e6, 3), "bytes_per_launch": bytes_per_launch,
             "us_per_dp_step": round(avg_s * 1e6 / steps, 3)}
-    roof_valu = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in roof_valu.items()}
-    return roof, roof_valu
+    valu = {"bound": "valu", "achieved": round(ops / avg_s / 1e12, 6), "peak": FP64_VALU_PEAK_TOPS,
+            "unit": "TFP64op/s", "frac": round(ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS, 6)}
+    if note:
+        valu["note"] = note
+    return roof, valu
 
 
-def cpu_baseline(args):
-    """The reference recurrence (C restatement, oracle/) on the host: a bounded truncated sample."""
+def _cpu_info():
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    # this job's CPU share: OMP_NUM_THREADS where the launcher sets it (16 per GPU on the GPU box), else the
+    # affinity mask
+    threads = int(os.environ.get("OMP_NUM_THREADS") or aff)
+    return model, aff, max(1, min(threads, aff))
+
+
+def cpu_baseline(cfg_name, p_over, cpu_steps):
+    """The reference recurrence (C restatement, oracle/) on the host: a bounded sample of the config."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle.oracle import OracleC, Levels, P_INF, P_ONE
     from mioc.synth import CONFIGS, make_inputs
-    cfg = CONFIGS[args.config]
-    p = cfg.p if args.p is None else (math.inf if args.p == "inf" else float(args.p))
-    # BASELINE.md §2: single-thread (the reference is single-threaded Julia) and OpenMP over the target levels
-    # on the host cores this job may use (OMP_NUM_THREADS on the GPU box; os.cpu_count() there is the machine's)
-    threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+    cfg = CONFIGS[cfg_name]
+    p = cfg.p if p_over is None else (math.inf if p_over == "inf" else float(p_over))
     kind = P_INF if p == math.inf else P_ONE
+    model, aff, threads = _cpu_info()
     oc = OracleC()
+    host = f"host: {model}, {aff} CPUs in the affinity mask, {threads} threads used (this job's CPU share)"
+    if cfg.levels().L <= 64:
+        # batch config: independent subproblems, one per thread (the reference is single-threaded per subproblem);
+        # the sample is `threads` restarts at full nt, extrapolated to subproblems/s
+        lt = cfg.levels()
+        lv = Levels(lt.nu, [tuple(t) for t in lt.tuples])
+        jobs = [make_inputs(cfg, k=10_000 + k, levels=lt)[1:] for k in range(threads)]
+
+        def one(j):
+            df, uo = j
+            return oc.bellman_steps(lv, df, uo, cfg.B, kind, cfg.beta, cfg.dt, cfg.nt - 1)
+
+        t0 = time.perf_counter()
+        one(jobs[0])
+        t1 = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(one, jobs))
+        tn = time.perf_counter() - t0
+        return {"value": round(threads / tn, 6), "unit": "subproblems/s", "cores": threads, "kind": "port",
+                "value_1thread": round(1.0 / t1, 6),
+                "sample": f"{threads} full restarts (nt={cfg.nt}, L={lt.L}, B={cfg.B}) of the reference loop "
+                          f"(C restatement), one per thread: {tn:.2f} s; one alone {t1:.2f} s; {host}"}
     per_step = {}
-    for nthr, steps in ((1, args.cpu_steps), (threads, args.cpu_steps * max(1, min(threads, 8)))):
+    for nthr, steps in ((1, cpu_steps), (threads, cpu_steps * max(1, min(threads, 8)))):
         lt, df, uo = make_inputs(cfg, nt=steps + 1)
         lv = Levels(lt.nu, [tuple(t) for t in lt.tuples])
         t0 = time.perf_counter()
         oc.bellman_steps(lv, df, uo, cfg.B, kind, cfg.beta, cfg.dt, steps, threads=nthr)
         per_step[nthr] = (time.perf_counter() - t0) / steps
     per_sub = {k: v * (cfg.nt - 1) for k, v in per_step.items()}
-    return {"value": 1.0 / per_sub[threads], "unit": "subproblems/s", "cores": threads, "kind": "port",
-            "value_1thread": 1.0 / per_sub[1],
+    return {"value": round(1.0 / per_sub[threads], 9), "unit": "subproblems/s", "cores": threads, "kind": "port",
+            "value_1thread": round(1.0 / per_sub[1], 9),
             "sample": f"recursion steps of the reference loop (C restatement) at L={lt.L}, B={cfg.B}: "
-                      f"{args.cpu_steps} steps on 1 thread ({per_step[1]:.3f} s/step) and "
-                      f"{args.cpu_steps * max(1, min(threads, 8))} steps on {threads} OpenMP threads "
-                      f"({per_step[threads]:.3f} s/step), extrapolated x{cfg.nt - 1}; host {platform.processor() or platform.machine()}, "
-                      f"{os.cpu_count()} CPUs visible"}
+                      f"{cpu_steps} steps on 1 thread ({per_step[1]:.3f} s/step) and "
+                      f"{cpu_steps * max(1, min(threads, 8))} steps on {threads} OpenMP threads "
+                      f"({per_step[threads]:.3f} s/step), extrapolated x{cfg.nt - 1}; {host}"}
+
+
+def workload(res):
+    lv = res["levels"]
+    counts = "x".join(str(len(v)) for v in lv.nu)
+    kind = "product" if lv.L == int(np.prod([len(v) for v in lv.nu])) else "SOS1-filtered"
+    return (f"{res['config']}: nt={res['nt']}, {lv.L} levels ({counts} {kind}), B={res['B']}, "
+            f"p={'inf' if res['p'] == math.inf else int(res['p'])}, {res['K']} subproblem(s) per GPU per step")
+
+
+def native_name(algo):
+    return {1: "generic min-plus sweep", 2: "p=Inf exact collapse", 3: "p=1 exact L1-ball pyramid",
+            4: "p=1 separable L1 transform, certified argmin", 5: "fused small-state DP (front in LDS)",
+            6: "fused separable DP (p=1, front in LDS, certified argmin)", 0: "oracle (CPU test double)"}.get(
+        algo, str(algo))
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     device = local
-    res = run(args, rank, world, device, dist, torch)
-    variant = None
+    res = run(args, args.config, args.batch, args.p, args.nt, rank, world, device, dist, torch, args.steps,
+              args.warmup)
+    variant = batch = None
     if args.variant == "pinf" and args.p is None and args.nt is None and math.isfinite(res["p"]):
-        a2 = argparse.Namespace(**vars(args))
-        a2.p = "inf"
-        a2.steps = max(args.steps, 3)
-        r2 = run(a2, rank, world, device, dist, torch)
-        roof2, valu2 = roofline_of(r2, a2)
-        variant = {"p": "inf", "value": round(world * r2["K"] * a2.steps / r2["elapsed"], 6),
-                   "unit": "subproblems/s", "ms_per_step": round(1e3 * r2["elapsed"] / a2.steps, 3),
-                   "algorithm": "p=Inf exact collapse (k_pinf_prep/recur/walk)", "roofline": roof2,
-                   "roofline_valu": valu2, "backtrack_ms": round(r2["walk_ms"] / max(1, a2.steps), 3)}
+        r2 = run(args, args.config, args.batch, "inf", None, rank, world, device, dist, torch,
+                 max(args.steps, 3), args.warmup)
+        roof2, valu2 = roofline_of(r2)
+        variant = {"p": "inf", "value": round(world * r2["K"] * r2["steps"] / r2["elapsed"], 6),
+                   "unit": "subproblems/s", "ms_per_step": round(1e3 * r2["elapsed"] / r2["steps"], 3),
+                   "algorithm": native_name(r2["algo"]), "roofline": roof2, "roofline_valu": valu2,
+                   "backtrack_ms": round(r2["walk_ms"] / max(1, r2["steps"]), 3)}
+    if args.batch_config not in ("", "none") and args.nt is None:
+        r3 = run(args, args.batch_config, args.batch_size, None, None, rank, world, device, dist, torch,
+                 max(args.steps, 3), args.warmup)
+        batch = {"config": {"workload": workload(r3), "parallelism": f"dp{world} (independent restarts)"},
+                 "value": round(world * r3["K"] * r3["steps"] / r3["elapsed"], 3), "unit": "subproblems/s",
+                 "n_gpus": world, "scaling": "weak", "steps": r3["steps"],
+                 "ms_per_step": round(1e3 * r3["elapsed"] / r3["steps"], 3),
+                 "algorithm": {native_name(r3["algo"]): r3["dom_name"]},
+                 "exact_scan_targets": {"near_tie": r3["diag"][0], "out_of_binade_or_few": r3["diag"][1]},
+                 "checksum": r3.get("gathered_checksum")}
+        if args.solver == "native":
+            batch["roofline"], batch["roofline_valu"] = roofline_of(r3)
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            batch["cpu_baseline"] = cpu_baseline(args.batch_config, None, args.cpu_steps)
     if rank == 0:
-        roof, valu = roofline_of(res, args)
         value = world * res["K"] * args.steps / res["elapsed"]
         out = {
-            "metric": "bellman_TRM! subproblems/sec (nt=65536, 4096 levels, budget=256) + HBM GB/s",
+            "metric": METRIC,
             "value": round(value, 6),
             "unit": "subproblems/s",
             "n_gpus": world,
@@ -289,30 +489,26 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded N(0,1) df, rand_func_int-shaped u_old; SURVEY §8 d)",
-            "config": {"workload": f"{args.config}: nt={res['nt']}, 4096 levels (8^4 product), B={res['B']}, "
-                                   f"beta=1e-3, p={'inf' if res['p'] == math.inf else int(res['p'])}, "
-                                   f"{res['K']} subproblem(s) per GPU per step",
-                       "parallelism": f"replicas x{world} (independent subproblems, RCCL gather of results)"},
+            "config": {"workload": workload(res),
+                       "parallelism": f"dp{world} (independent subproblems, RCCL broadcast + gather of results)"},
             "algorithm": {native_name(res["algo"]): res["dom_name"]},
-            "roofline": roof,
-            "roofline_valu": valu,
-            "backtrack_ms": round(res["walk_ms"] / max(1, args.steps), 3),
-            "exact_scan_targets": {"near_tie": res["diag"][0], "direct_rows": res["diag"][1],
-                                   "of_cells": res["K"] * (res["nt"] - 1) * (res["B"] + 1) * res["levels"].L,
-                                   "note": "last bellman call (mioc_diagnostics[0..1])"},
+            "checksum": res.get("gathered_checksum"),
         }
+        if args.solver == "native":
+            out["roofline"], out["roofline_valu"] = roofline_of(res)
+            out["backtrack_ms"] = round(res["walk_ms"] / max(1, args.steps), 3)
+            out["exact_scan_targets"] = {"near_tie": res["diag"][0], "direct_rows": res["diag"][1],
+                                         "of_cells": res["K"] * (res["nt"] - 1) * (res["B"] + 1) * res["levels"].L,
+                                         "note": "last bellman call (mioc_diagnostics[0..1])"}
         if variant:
             out["variant_p_inf"] = variant
-        if not args.no_cpu_baseline and world == 1 and args.nt is None:
-            out["cpu_baseline"] = cpu_baseline(args)
+        if batch:
+            out["batch"] = batch
+        if not args.no_cpu_baseline and world == 1 and args.nt is None and args.solver == "native":
+            out["cpu_baseline"] = cpu_baseline(args.config, args.p, args.cpu_steps)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def native_name(algo):
-    return {1: "generic min-plus sweep", 2: "p=Inf exact collapse", 3: "p=1 exact L1-ball pyramid",
-            4: "p=1 separable L1 transform, certified argmin"}.get(algo, str(algo))
 
 
 if __name__ == "__main__":

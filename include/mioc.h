@@ -126,6 +126,14 @@ int32_t mioc_backtrack_batch_device(mioc_ctx *ctx, int64_t B_use, double *d_u_ou
                                     int32_t *d_status);
 int32_t mioc_synchronize(mioc_ctx *ctx);
 
+/*
+ * The controls of the last backtrack as 0-based level ranks in iterator order (obj.iterator of
+ * eval_u_TRM!, HelpFunctions.jl:110-118: u[:, i] = ν(l_i)): d_ranks_out receives K x nt int32 (device
+ * pointer), enqueued on the context's stream.  The multi-GPU batch gathers these (one 16-bit rank per step
+ * instead of nx level values) without recovering them from u.
+ */
+int32_t mioc_get_ranks_device(mioc_ctx *ctx, int32_t *d_ranks_out);
+
 /* The HIP stream the context enqueues on (hipStream_t), for callers that order their own work. */
 void *mioc_stream(mioc_ctx *ctx);
 

@@ -416,6 +416,7 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
     ev_end(ctx, 1, 1);
   }
   HIP_TRY(ctx, launch_expand(ctx->stream, P, Lv, ctx->d_start, ctx->d_ranks, d_u_out, d_phi_star, d_status));
+  ctx->have_path = true;
   return MIOC_OK;
 }
 
@@ -450,6 +451,7 @@ int set_problem(mioc_ctx *ctx, int64_t K, int64_t nx, int64_t nt, int64_t B, dou
   ctx->RP = (int)(((B + 1 + kRowTile - 1) / kRowTile) * kRowTile);
   ctx->dt = dt;
   ctx->have_dp = false;
+  ctx->have_path = false;
   size_t need = (size_t)K * nx * nt * sizeof(double);
   size_t cap = ctx->in_cap, cap2 = ctx->in_cap;
   int rc = grow(ctx, &ctx->d_df, &cap, need, "df copy");
@@ -735,6 +737,15 @@ int32_t mioc_synchronize(mioc_ctx *ctx) {
 }
 
 void *mioc_stream(mioc_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int32_t mioc_get_ranks_device(mioc_ctx *ctx, int32_t *d_ranks_out) {
+  if (!ctx || !d_ranks_out) return MIOC_EINVAL;
+  if (!ctx->have_path) return fail(ctx, MIOC_ESTATE, "no backtrack result to read");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipMemcpyAsync(d_ranks_out, ctx->d_ranks, (size_t)ctx->K * ctx->nt * sizeof(int32_t),
+                              hipMemcpyDeviceToDevice, ctx->stream));
+  return MIOC_OK;
+}
 
 int32_t mioc_kernel_stats(mioc_ctx *ctx, int32_t which, double *total_ms, int64_t *launches, const char **name) {
   if (!ctx || which < 0 || which >= kStats) return MIOC_EINVAL;

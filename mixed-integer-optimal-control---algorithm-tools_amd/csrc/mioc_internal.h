@@ -203,6 +203,7 @@ struct mioc_ctx {
   size_t pinf_cap_k = 0, pinf_cap_R = 0;
 
   // backtrack scratch
+  bool have_path = false;          // d_ranks holds the controls of the last backtrack
   mioc::Start *d_start = nullptr;
   int32_t *d_ranks = nullptr;      // [K][nt] level ranks of the path, then [K][nt] ranks of u_old
   size_t ranks_cap = 0;

@@ -34,7 +34,7 @@ EXPORTED = [
     "mioc_version", "mioc_create", "mioc_destroy", "mioc_last_error", "mioc_set_option", "mioc_set_levels",
     "mioc_set_cost", "mioc_bellman", "mioc_backtrack", "mioc_bellman_batch_device",
     "mioc_backtrack_batch_device", "mioc_synchronize", "mioc_stream", "mioc_kernel_stats",
-    "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics", "mioc_get_argmin_table",
+    "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics", "mioc_get_argmin_table", "mioc_get_ranks_device",
 ]
 
 
@@ -88,6 +88,7 @@ def load_library(path=None):
         "mioc_last_algo": (i32, [vp]),
         "mioc_diagnostics": (i32, [vp, vp, i32]),
         "mioc_get_argmin_table": (i32, [vp, i64, i64, vp]),
+        "mioc_get_ranks_device": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -234,6 +235,12 @@ class Context:
                 raise ValueError(f"{name} must be a contiguous {dt_} tensor with K entries")
         self.backtrack_batch_device(B_use, u.data_ptr(), 0 if phi is None else phi.data_ptr(),
                                     0 if status is None else status.data_ptr())
+
+    def ranks_tensor(self, out):
+        """Level ranks (iterator order) of the last backtrack into `out`, an int32 CUDA tensor (K, nt)."""
+        if not out.is_cuda or str(out.dtype) != "torch.int32" or not out.is_contiguous():
+            raise ValueError("out must be a contiguous int32 CUDA tensor (K, nt)")
+        self._check(self.lib.mioc_get_ranks_device(self.h, ctypes.c_void_p(out.data_ptr())))
 
     def synchronize(self):
         self._check(self.lib.mioc_synchronize(self.h))

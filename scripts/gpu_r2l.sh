@@ -1,0 +1,11 @@
+# round 2: GPU suite, default bench (C4 + p=Inf variant + C5 batch + CPU baselines), smoke
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r2l
+mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
+rc=$?; echo "tests exit=$rc"; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
+rc=$?; echo "bench exit=$rc"; cat $O/bench.json; tail -3 $O/bench.err; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+rc=$?; echo "smoke exit=$rc"; tail -2 $O/smoke.log; exit $rc
