@@ -168,7 +168,8 @@ int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n);
  * (0 <= i < nt-1), U_out[c + (B+1)*g] = 0-based iterator rank of the source j minimising Φ_i at budget
  * c and the target level with grid-linear index g (levels in column-major grid order), as an int32.
  * Cells the reference never writes because Φ_i = +Inf there hold -1 when c < b̃(l, i) and are
- * unspecified otherwise (the reference leaves them at whatever `U` held before).  U_out has
+ * unspecified otherwise (the reference leaves them at whatever `U` held before); the separable transform
+ * (MIOC_ALGO_SEPARABLE) reports -1 for every such cell, so its tables equal the reference's.  U_out has
  * (B+1) * prod(counts) entries.  The p=Inf collapse stores class tables instead (MIOC_EINVAL).
  */
 int32_t mioc_get_argmin_table(mioc_ctx *ctx, int64_t k, int64_t step, int32_t *U_out);

@@ -263,7 +263,10 @@ int run_bellman(mioc_ctx *ctx) {
     int nwg = 0;
     bool persist = false;
     // (B + 1)·L·8 < 2^31: the persistent kernel addresses a staging block with 32-bit buffer offsets
-    if (algo == MIOC_ALGO_SEPARABLE && ctx->opt_persist && nt >= 2 && s_stride * sizeof(double) < (1ull << 31)) {
+    // ... and every b̃ within the kernel's dependency window (7 per dimension: u_old on the level grid); a u_old
+    // off the grid reaches rows further back than the window waits for, so those problems take per-step launches
+    if (algo == MIOC_ALGO_SEPARABLE && ctx->opt_persist && nt >= 2 && s_stride * sizeof(double) < (1ull << 31) &&
+        bmax <= 7 * ctx->pyr.M && !ctx->force_steps) {
       int ncu = 0;
       HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
       const int bpc = sdt_run_blocks_per_cu(ctx->pyr, run_lds);
@@ -296,9 +299,19 @@ int run_bellman(mioc_ctx *ctx) {
       // the whole DP as one persistent launch: rows handed between resident workgroups by flags
       HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, runflag_bytes, ctx->stream));
       ev_begin(ctx, 0, "k_sdt_run");
-      HIP_TRY(ctx, launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_stage, K * s_stride,
-                                  (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters, ctx->d_runflags,
-                                  nwg, run_lds));
+      const hipError_t le = launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_stage, K * s_stride,
+                                           (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters,
+                                           ctx->d_runflags, nwg, run_lds);
+      if (le == hipErrorCooperativeLaunchTooLarge) {  // not every workgroup can be resident: one launch per step
+        (void)hipGetLastError();
+        ev_end(ctx, 0, 0);
+        ctx->n_persist_fallbacks += 1;
+        ctx->force_steps = true;
+        const int rcs = run_bellman(ctx);
+        ctx->force_steps = false;
+        return rcs;
+      }
+      HIP_TRY(ctx, le);
       ev_end(ctx, 0, 1);
       HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + 2 * K * (size_t)(ctx->B + 1), sizeof(int32_t),
                                   hipMemcpyDeviceToHost, ctx->stream));
@@ -420,13 +433,20 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
   return MIOC_OK;
 }
 
-// after a synchronisation: did the persistent DP's dependency waits time out?
+// after a synchronisation: did the persistent DP's dependency waits time out (workgroups not co-resident, e.g.
+// another context's kernels holding CUs)?  Then the DP is redone from the terminal step with one launch per
+// step, which needs no co-residency, and the caller sees only the extra time.
 int check_run(mioc_ctx *ctx) {
   if (!ctx->run_pending) return MIOC_OK;
   ctx->run_pending = false;
   if (ctx->h_run_err && *ctx->h_run_err) {
     ctx->have_dp = false;
-    return fail(ctx, MIOC_EHIP, "persistent DP: a workgroup's dependency wait timed out (workgroups not co-resident?)");
+    ctx->n_persist_fallbacks += 1;
+    ctx->force_steps = true;
+    const int rc = run_bellman(ctx);
+    ctx->force_steps = false;
+    if (rc) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   }
   return MIOC_OK;
 }

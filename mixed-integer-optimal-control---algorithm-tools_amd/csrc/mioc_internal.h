@@ -184,6 +184,8 @@ struct mioc_ctx {
   uint32_t *d_perm = nullptr;      // [K][nt][L] sphere order of u_old(i): rank | (L1 distance << 16)
   size_t perm_cap = 0;
   bool opt_persist = true;         // separable transform: one persistent launch (MIOC_OPT_PERSIST)
+  bool force_steps = false;        // redo of a persistent DP whose waits timed out: per-step launches
+  int64_t n_persist_fallbacks = 0; // persistent DPs redone with per-step launches (diagnostics [6] of the sdt)
   int32_t *d_runflags = nullptr;   // persistent DP: [K][B+1] done, [K][B+1] loaded, err
   size_t runflag_cap = 0;
   int32_t *h_run_err = nullptr;    // pinned copy of err

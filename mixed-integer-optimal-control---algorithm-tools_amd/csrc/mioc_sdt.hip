@@ -422,6 +422,8 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       sd_store16<PERSIST>(Sout, L * 8, 2 * (tid + T * q), 0x7FF0000000000000ull, 0x7FF0000000000000ull);
+    // and the U row: no cell written (0xFFFF), as in the reference, where U keeps nothing for Φ_i = +Inf
+    *reinterpret_cast<ulonglong2 *>(UU + 8 * tid) = make_ulonglong2(~0ull, ~0ull);
     return;
   }
 
@@ -918,13 +920,13 @@ hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &L
                           const uint32_t *perm, double *S, size_t buf_stride, uint16_t *UU, size_t s_stride,
                           size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, size_t lds) {
   if (!sdt_supported(G)) return hipErrorInvalidValue;
+  // cooperative launch: the runtime checks at launch time that every workgroup can be resident at once (the
+  // row hand-off spins on other workgroups), and refuses the launch otherwise (hipErrorCooperativeLaunchTooLarge)
+  void *args[] = {(void *)&P, (void *)&Lv, (void *)&G, (void *)&perm, (void *)&S, (void *)&buf_stride, (void *)&UU,
+                  (void *)&s_stride, (void *)&uu_stride_k, (void *)&counters, (void *)&flags, (void *)&nwg};
   if (G.M == 4)
-    hipLaunchKernelGGL(k_sdt_run<4>, dim3(nwg), dim3(512), lds, s, P, Lv, G, perm, S, buf_stride, UU, s_stride,
-                       uu_stride_k, counters, flags, nwg);
-  else
-    hipLaunchKernelGGL(k_sdt_run<3>, dim3(nwg), dim3(64), lds, s, P, Lv, G, perm, S, buf_stride, UU, s_stride,
-                       uu_stride_k, counters, flags, nwg);
-  return hipGetLastError();
+    return hipLaunchCooperativeKernel((const void *)k_sdt_run<4>, dim3(nwg), dim3(512), args, (unsigned)lds, s);
+  return hipLaunchCooperativeKernel((const void *)k_sdt_run<3>, dim3(nwg), dim3(64), args, (unsigned)lds, s);
 }
 
 int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds) {

@@ -375,7 +375,7 @@ def test_trm_on_gpu_matches_trm_on_oracle():
 
 
 @pytest.mark.parametrize("algo", ["pyramid", "separable", "separable_steps"])
-@pytest.mark.parametrize("mode", ["gauss", "integer", "zero", "dyadic", "steep"])
+@pytest.mark.parametrize("mode", ["gauss", "integer", "zero", "dyadic", "steep", "outside"])
 def test_pyramid_vs_oracle_512_levels(oracle_c, mode, algo):
     """8x8x8 product grid, p=1: clean rows (pyramid + value lookup / certified transform argmin) and
     dirty rows (exact scan).  "steep": value spread ~1e14 times beta, outside the separable
@@ -383,7 +383,7 @@ def test_pyramid_vs_oracle_512_levels(oracle_c, mode, algo):
     persist = algo != "separable_steps"
     algo = {"pyramid": native.MIOC_ALGO_PYRAMID, "separable": native.MIOC_ALGO_SEPARABLE,
             "separable_steps": native.MIOC_ALGO_SEPARABLE}[algo]
-    rng = np.random.default_rng({"gauss": 1, "integer": 2, "zero": 3, "dyadic": 4, "steep": 5}[mode])
+    rng = np.random.default_rng({"gauss": 1, "integer": 2, "zero": 3, "dyadic": 4, "steep": 5, "outside": 6}[mode])
     lv = Levels.product([list(range(8))] * 3)
     lt = LevelTable(lv.nu, [tuple(t) for t in lv.tuples])
     n, B = 12, 20
@@ -398,7 +398,12 @@ def test_pyramid_vs_oracle_512_levels(oracle_c, mode, algo):
     else:
         df = rng.integers(-64, 65, size=(3, n)) / 64.0
     uo = np.array([lv.nuval[rng.integers(lv.L)] for _ in range(n)], dtype=np.float64).T
-    beta, dt = {"gauss": (1e-3, 2.0 ** -10), "steep": (1e-12, 2.0 ** -10)}.get(mode, (0.125, 0.25))
+    if mode == "outside":  # u_old off the level grid (integral, not admissible): b̃ beyond the 7·M window
+        df = rng.standard_normal((3, n))
+        for i in rng.choice(n, size=5, replace=False):
+            uo[:, i] = [-1.0, 8.0, 3.0][: 3]
+    beta, dt = {"gauss": (1e-3, 2.0 ** -10), "steep": (1e-12, 2.0 ** -10),
+                "outside": (1e-3, 2.0 ** -10)}.get(mode, (0.125, 0.25))
     phi, U = oracle_c.bellman(lv, df, uo, B, P_ONE, beta, dt)
     ctx = _ctx(lt, P_ONE, beta, algo)
     ctx.set_option(native.MIOC_OPT_PERSIST, int(persist))
@@ -406,7 +411,12 @@ def test_pyramid_vs_oracle_512_levels(oracle_c, mode, algo):
     diag = ctx.diagnostics()
     _assert_U(ctx, U, n, mode)
     for Bp in (B, B // 2, 3):
-        ou, ops = oracle_c.backtrack(lv, uo, phi, U, B, Bp)
+        try:
+            ou, ops = oracle_c.backtrack(lv, uo, phi, U, B, Bp)
+        except Exception:  # no finite value within B' (off-grid u_old costs budget at every such step)
+            with pytest.raises(native.MiocNativeError):
+                ctx.backtrack(Bp)
+            continue
         u, ps, _ = ctx.backtrack(Bp)
         assert np.array_equal(u, ou), f"{mode} Bp={Bp} diag={diag}"
         assert ps == ops
