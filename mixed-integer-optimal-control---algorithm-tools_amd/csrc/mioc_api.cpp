@@ -259,8 +259,9 @@ int run_bellman(mioc_ctx *ctx) {
     // persistent separable transform: every workgroup resident, one per CU (96 KB of LDS keeps a second one
     // off the CU: its register file would not hold it), kSdtBuffers staging buffers; B + 1 rows on B
     // workgroups, workgroup 0 taking rows 0 and B (k_sdt_run)
+    // 96 KB keeps the workgroups one per CU (the register file holds one: k_sdt_run needs 256 VGPRs per lane)
     const size_t run_lds = std::max<size_t>(sdt_lds_bytes(ctx->pyr), 96 * 1024);
-    int nwg = 0;
+    int nwg = 0, kint = 1;
     bool persist = false;
     // (B + 1)·L·8 < 2^31: the persistent kernel addresses a staging block with 32-bit buffer offsets
     // ... and every b̃ within the kernel's dependency window (7 per dimension: u_old on the level grid); a u_old
@@ -270,11 +271,19 @@ int run_bellman(mioc_ctx *ctx) {
       int ncu = 0;
       HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
       const int bpc = sdt_run_blocks_per_cu(ctx->pyr, run_lds);
-      // contiguous row chunks, nwg / K workgroups per subproblem
       const size_t slots = (size_t)ncu * (size_t)std::max(bpc, 0);
-      const size_t per_k = std::min<size_t>((size_t)std::max<int64_t>(ctx->B, 1), K ? slots / K : 0);  // B: rows 0, B share one
-      nwg = (int)(per_k * K);
-      persist = per_k > 0;
+      const size_t Bw = (size_t)std::max<int64_t>(ctx->B, 1);  // one row per workgroup: B (rows 0, B share one)
+      if (K * Bw <= slots || K > 8 || Bw > slots) {
+        // contiguous row chunks, nwg / K workgroups per subproblem
+        const size_t per_k = std::min<size_t>(Bw, K ? slots / K : 0);
+        nwg = (int)(per_k * K);
+        kint = 1;
+      } else {
+        // more subproblems than the CUs hold one row each of: every workgroup keeps one row of all K, interleaved
+        nwg = (int)Bw;
+        kint = (int)K;
+      }
+      persist = nwg > 0;
     }
     const size_t runflag_bytes = ((2 * K * (size_t)(ctx->B + 1) + 1) * sizeof(int32_t) + 15) / 16 * 16;
     if (persist) {
@@ -301,7 +310,7 @@ int run_bellman(mioc_ctx *ctx) {
       ev_begin(ctx, 0, "k_sdt_run");
       const hipError_t le = launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_stage, K * s_stride,
                                            (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters,
-                                           ctx->d_runflags, nwg, run_lds);
+                                           ctx->d_runflags, nwg, kint, run_lds);
       if (le == hipErrorCooperativeLaunchTooLarge) {  // not every workgroup can be resident: one launch per step
         (void)hipGetLastError();
         ev_end(ctx, 0, 0);

@@ -97,7 +97,7 @@ hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
                            size_t uu_stride_k, int32_t *counters);
 hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
                           const uint32_t *perm, double *S, size_t buf_stride, uint16_t *UU, size_t s_stride,
-                          size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, size_t lds);
+                          size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, int kint, size_t lds);
 int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds);
 hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
                                 const double *S0, size_t s_stride, int Bu, Start *start);

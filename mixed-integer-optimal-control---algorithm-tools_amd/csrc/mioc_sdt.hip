@@ -45,6 +45,12 @@ constexpr int SD_FEW = 4;                // rows with at most this many targets 
 constexpr int SD_SPARSE = 4;             // rows with at most this many finite sources: direct minimum over them
 constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, the scan sweeps every rank
 constexpr int SD_BLAG = 2;               // persistent kernel: row B runs this many steps behind row 0
+#ifndef SDT_RUN_MINW
+#define SDT_RUN_MINW 2                   // persistent kernel: waves per SIMD the registers must allow (4: two workgroups per CU, but the row code then spills)
+#endif
+#ifndef SDT_PREFETCH
+#define SDT_PREFETCH 1                   // load the sphere orders ahead of the dependency wait
+#endif
 
 // Diagnostic build only (make stamps -> libmioc_stamps.so): per-workgroup phase clocks of the last launch.
 #if defined(MIOC_STAMPS) && !defined(MIOC_STAMPS_TL)
@@ -804,20 +810,22 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
 // every workgroup resident there is no deadlock; a wait that exceeds its spin bound sets *err and every
 // workgroup leaves.
 template <int M>
-__global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_run(ProblemDev P, LevelsDev Lv, PyrGeom G,
+__global__ __launch_bounds__(1 << (3 * M - 3), SDT_RUN_MINW) void k_sdt_run(ProblemDev P, LevelsDev Lv, PyrGeom G,
                                                           const uint32_t *__restrict__ perm_all, double *S_all,
                                                           size_t buf_stride, uint16_t *__restrict__ UU_all,
                                                           size_t s_stride, size_t uu_stride_k,
-                                                          int32_t *__restrict__ counters, int32_t *flags, int nwg) {
+                                                          int32_t *__restrict__ counters, int32_t *flags, int nwg,
+                                                          int kint) {
   constexpr int Smax = 7 * M, NB = kSdtBuffers;
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
   const int R = P.B + 1, nrows = P.K * R, tid = threadIdx.x;
   int32_t *done = flags, *loaded = flags + nrows, *err = flags + 2 * nrows;
-  // this workgroup's chunk
-  const int W = nwg / P.K;  // workgroups per subproblem (>= 1: the host guarantees nwg >= K)
-  const int k = (int)blockIdx.x / W, wl = (int)blockIdx.x - k * W;
-  if (k >= P.K) return;
+  // this workgroup's chunk of rows, in every one of its group's kint subproblems (interleaved: while one
+  // subproblem's row hand-off is in flight, the workgroup computes the same row of the next one)
+  const int W = nwg / (P.K / kint);  // workgroups per group of kint subproblems (the host guarantees >= 1)
+  const int kg = (int)blockIdx.x / W, wl = (int)blockIdx.x - kg * W;
+  if (kg * kint >= P.K) return;
   const int base = R / W, extra = R - base * W;
   const bool split = W == R - 1 && R >= 2, edges = split && wl == 0;
   int lo, hi;  // rows [lo, hi), contiguous, the longer chunks highest
@@ -833,72 +841,84 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_run(ProblemDev P, Leve
   auto buf = [&](int step) { return S_all + (size_t)(step % NB) * buf_stride; };
 #pragma nounroll
   for (int i = P.nt - 2; i >= (edges ? -SD_BLAG : 0); --i) {
-    const int iB = i + SD_BLAG;                   // workgroup 0: the step of its row B
-    const bool do0 = i >= 0, doB = edges && iB <= P.nt - 2;
-    const int g = k * R + lo;  // timeline stamps: the chunk's first row
-    (void)g;
-    SdPerm pm, pmB;  // static: in flight during the wait
-    if (do0) sd_perm_load<M>(pm, perm_all, P.nt, k, i);
-    if (doB) sd_perm_load<M>(pmB, perm_all, P.nt, k, iB);
-    SD_TL(0);
-    if (tid < 64) {  // wave 0: dependency wait
-      const int lane = tid;
-      const int s = lane < 32 ? lane + 1 : lane - 31;
-      int32_t *fp = nullptr;
-      int need = 0;
-      // RAW: inputs of row lo at step i (workgroup 0: of row B at step iB)
-      const int rlo = edges ? R - 1 : lo, sraw = edges ? iB : i;
-      // WAR: readers of the buffer row lo .. hi-1 overwrites at step i (workgroup 0: row 0 at step i)
-      const int whi = edges ? 1 : hi;
-      if (lane < 32 && s <= Smax && s <= rlo && (!edges || doB)) {
-        fp = done + k * R + rlo - s;
-        need = tok_of(sraw + 1);
-      } else if (lane >= 32 && s <= Smax && whi - 1 + s < R && do0) {
-        fp = loaded + k * R + whi - 1 + s;
-        need = tok_of(i + NB - 1);
-      }
-      unsigned spins = 0;
-      for (;;) {
-        const bool ok = !fp || need <= 0 || __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
-        if (__all(ok)) break;
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > (1u << 24)) {
-          if (lane == 0) {
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sh.stop = 1;
-          }
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __syncthreads();
-    SD_TL(1);
-    if (sh.stop) return;
-    if (edges) {
-      if (do0)
-        sdt_row0<M, true>(P, Lv, k, i, pm, buf(i + 1), buf(i), UU_all, s_stride, uu_stride_k, G.base,
-                          loaded + k * R, tok_of(i));
-      if (doB)
-        sdt_rowB<M, true>(P, Lv, k, iB, pmB, buf(iB + 1), buf(iB), UU_all, s_stride, uu_stride_k, G.base,
-                          counters, sh, loaded + k * R + R - 1, tok_of(iB));
-      SD_TL(2);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
-      __syncthreads();
-      if (tid == 0) {
-        if (do0) __hip_atomic_store(done + k * R, tok_of(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (doB) __hip_atomic_store(done + k * R + R - 1, tok_of(iB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      SD_TL(3);
-    }
 #pragma nounroll
-    for (int cp = lo; cp < hi && !edges; ++cp) {
-      sdt_row<M, true>(P, Lv, G, k, cp, i, pm, buf(i + 1), buf(i), UU_all, s_stride, uu_stride_k, counters, sh,
-                       sds, loaded + k * R + cp, tok_of(i));
-      SD_TL(2);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
+    for (int kk = 0; kk < kint; ++kk) {
+      const int k = kg * kint + kk;
+      const int iB = i + SD_BLAG;                   // workgroup 0: the step of its row B
+      const bool do0 = i >= 0, doB = edges && iB <= P.nt - 2;
+      const int g = k * R + lo;  // timeline stamps: the chunk's first row
+      (void)g;
+      SdPerm pm, pmB;  // static; SDT_PREFETCH: in flight during the wait (costs VGPRs)
+#if SDT_PREFETCH
+      if (do0) sd_perm_load<M>(pm, perm_all, P.nt, k, i);
+      if (doB) sd_perm_load<M>(pmB, perm_all, P.nt, k, iB);
+#endif
+      SD_TL(0);
+      if (tid < 64) {  // wave 0: dependency wait
+        const int lane = tid;
+        const int s = lane < 32 ? lane + 1 : lane - 31;
+        int32_t *fp = nullptr;
+        int need = 0;
+        // RAW: inputs of row lo at step i (workgroup 0: of row B at step iB)
+        const int rlo = edges ? R - 1 : lo, sraw = edges ? iB : i;
+        // WAR: readers of the buffer row lo .. hi-1 overwrites at step i (workgroup 0: row 0 at step i)
+        const int whi = edges ? 1 : hi;
+        if (lane < 32 && s <= Smax && s <= rlo && (!edges || doB)) {
+          fp = done + k * R + rlo - s;
+          need = tok_of(sraw + 1);
+        } else if (lane >= 32 && s <= Smax && whi - 1 + s < R && do0) {
+          fp = loaded + k * R + whi - 1 + s;
+          need = tok_of(i + NB - 1);
+        }
+        unsigned spins = 0;
+        for (;;) {
+          const bool ok =
+              !fp || need <= 0 || __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
+          if (__all(ok)) break;
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > (1u << 24)) {
+            if (lane == 0) {
+              __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              sh.stop = 1;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(done + k * R + cp, tok_of(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      SD_TL(3);
+      SD_TL(1);
+      if (sh.stop) return;
+#if !SDT_PREFETCH
+      if (do0) sd_perm_load<M>(pm, perm_all, P.nt, k, i);
+      if (doB) sd_perm_load<M>(pmB, perm_all, P.nt, k, iB);
+#endif
+      if (edges) {
+        if (do0)
+          sdt_row0<M, true>(P, Lv, k, i, pm, buf(i + 1), buf(i), UU_all, s_stride, uu_stride_k, G.base,
+                            loaded + k * R, tok_of(i));
+        if (doB)
+          sdt_rowB<M, true>(P, Lv, k, iB, pmB, buf(iB + 1), buf(iB), UU_all, s_stride, uu_stride_k, G.base,
+                            counters, sh, loaded + k * R + R - 1, tok_of(iB));
+        SD_TL(2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
+        __syncthreads();
+        if (tid == 0) {
+          if (do0) __hip_atomic_store(done + k * R, tok_of(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (doB)
+            __hip_atomic_store(done + k * R + R - 1, tok_of(iB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        SD_TL(3);
+      }
+#pragma nounroll
+      for (int cp = lo; cp < hi && !edges; ++cp) {
+        sdt_row<M, true>(P, Lv, G, k, cp, i, pm, buf(i + 1), buf(i), UU_all, s_stride, uu_stride_k, counters,
+                         sh, sds, loaded + k * R + cp, tok_of(i));
+        SD_TL(2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(done + k * R + cp, tok_of(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        SD_TL(3);
+      }
     }
     if (i == 0) SD_FLUSH();
   }
@@ -918,12 +938,13 @@ bool sdt_supported(const PyrGeom &G) {
 
 hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
                           const uint32_t *perm, double *S, size_t buf_stride, uint16_t *UU, size_t s_stride,
-                          size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, size_t lds) {
+                          size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, int kint, size_t lds) {
   if (!sdt_supported(G)) return hipErrorInvalidValue;
   // cooperative launch: the runtime checks at launch time that every workgroup can be resident at once (the
   // row hand-off spins on other workgroups), and refuses the launch otherwise (hipErrorCooperativeLaunchTooLarge)
   void *args[] = {(void *)&P, (void *)&Lv, (void *)&G, (void *)&perm, (void *)&S, (void *)&buf_stride, (void *)&UU,
-                  (void *)&s_stride, (void *)&uu_stride_k, (void *)&counters, (void *)&flags, (void *)&nwg};
+                  (void *)&s_stride, (void *)&uu_stride_k, (void *)&counters, (void *)&flags, (void *)&nwg,
+                  (void *)&kint};
   if (G.M == 4)
     return hipLaunchCooperativeKernel((const void *)k_sdt_run<4>, dim3(nwg), dim3(512), args, (unsigned)lds, s);
   return hipLaunchCooperativeKernel((const void *)k_sdt_run<3>, dim3(nwg), dim3(64), args, (unsigned)lds, s);
