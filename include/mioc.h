@@ -65,6 +65,8 @@ extern "C" {
 #define MIOC_OPT_TIMING 2   /* 1: record HIP events around the dominant kernel (mioc_kernel_stats) */
 #define MIOC_OPT_PERSIST 3  /* separable transform: 1 (default) runs the whole DP as one persistent launch
                                whose workgroups hand rows to each other; 0: one launch per step */
+#define MIOC_OPT_PRED_FMA 4 /* mioc_pred*: 1 accumulates each ∇f[:,j]'(u_old[:,j] - u[:,j]) with fma, as an
+                               FMA-contracted BLAS ddot does; 0 (default): products rounded, then added */
 
 typedef struct mioc_ctx mioc_ctx;
 
@@ -133,6 +135,33 @@ int32_t mioc_synchronize(mioc_ctx *ctx);
  * instead of nx level values) without recovering them from u.
  */
 int32_t mioc_get_ranks_device(mioc_ctx *ctx, int32_t *d_ranks_out);
+
+/*
+ * Trust-region quantities of the last backtrack, multi-trust.jl:117-127 (pred) with TV_p of
+ * HelpFunctions.jl:251-268 (p = the context's cost; p = Inf is the true max norm here, unlike the DP's cost):
+ *   int_val = Δt · Σ_j ∇f[:,j]'(u_old[:,j] − u[:,j]);   tv_old = TV_p(u_old, p);   tv_new = TV_p(u, p)
+ *   pred    = int_val + β·(tv_old − tv_new)
+ * u is the path of the last mioc_backtrack*, ∇f and u_old those of the last mioc_bellman*.  All sums are
+ * accumulated in the reference's loop order, so TV_p is bit-identical for p = 1, Inf and MIOC_P_INTLUT (the
+ * summand is the host table's Julia pow) and int_val differs from the reference's BLAS dot only by its FMA use
+ * (MIOC_OPT_PRED_FMA).  MIOC_P_TABLE needs both controls on the level grid (else MIOC_EINVAL).
+ * Outputs are nullable.  mioc_pred: the single-subproblem (host) API, synchronous.
+ * mioc_pred_batch_device: K values per output (device pointers), enqueued; errors surface at mioc_synchronize.
+ */
+int32_t mioc_pred(mioc_ctx *ctx, double *int_val, double *tv_old, double *tv_new, double *pred);
+int32_t mioc_pred_batch_device(mioc_ctx *ctx, double *d_int_val, double *d_tv_old, double *d_tv_new, double *d_pred);
+
+/* TV_p(u, p) of K device controls d_u (K x nx x nt, each column-major) into d_tv[K]; enqueued. */
+int32_t mioc_tv_device(mioc_ctx *ctx, int64_t K, const double *d_u, int64_t nx, int64_t nt, double *d_tv);
+
+/*
+ * The trust-region step decision of multi-trust.jl:127-158 per subproblem, on the device:
+ *   ared = J_old − J_new + β·(tv_old − tv_new);   decision = 2 if pred <= 0 (stop: optimal),
+ *   1 if ared < σ·pred (bad step: halve Δ), else 0 (good step: accept).  d_ared nullable; enqueued.
+ */
+int32_t mioc_trm_decide_device(mioc_ctx *ctx, int64_t K, const double *d_J_old, const double *d_J_new,
+                               const double *d_tv_old, const double *d_tv_new, const double *d_pred, double sigma,
+                               double *d_ared, int32_t *d_decision);
 
 /* The HIP stream the context enqueues on (hipStream_t), for callers that order their own work. */
 void *mioc_stream(mioc_ctx *ctx);

@@ -96,7 +96,7 @@ void free_all(mioc_ctx *ctx) {
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
                   ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm,
-                  ctx->d_vals,  ctx->d_voff,    ctx->d_g2r};
+                  ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (ctx->h_flags) hipHostFree(ctx->h_flags);
@@ -147,6 +147,16 @@ int build_cost_tables(mioc_ctx *ctx) {
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_costtab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
     lut.assign(1, 0.0);
+  }
+  // TV_p's summand uses the unscaled weights (HelpFunctions.jl:262): keep the host table on the device as is
+  if (ctx->d_tvw) hipFree(ctx->d_tvw), ctx->d_tvw = nullptr;
+  ctx->tvw_len = 0;
+  if ((ctx->p_kind == MIOC_P_INTLUT || ctx->p_kind == MIOC_P_TABLE) && !ctx->table.empty()) {
+    size_t wcap = 0;
+    int rc = grow(ctx, &ctx->d_tvw, &wcap, ctx->table.size() * sizeof(double), "TV weight table");
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(ctx->d_tvw, ctx->table.data(), ctx->table.size() * sizeof(double), hipMemcpyHostToDevice));
+    ctx->tvw_len = (int64_t)ctx->table.size();
   }
   size_t cap = 0;
   if (ctx->d_costlut) hipFree(ctx->d_costlut), ctx->d_costlut = nullptr;
@@ -511,7 +521,7 @@ int32_t mioc_create(int32_t device, mioc_ctx **out) {
     return MIOC_EHIP;
   }
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&ctx->d_flags, 16) != hipSuccess || hipHostMalloc(&ctx->h_flags, 16, 0) != hipSuccess) {
+      hipMalloc(&ctx->d_flags, 16) != hipSuccess || hipMalloc(&ctx->d_pred_own, 64) != hipSuccess || hipHostMalloc(&ctx->h_flags, 16, 0) != hipSuccess) {
     free_all(ctx);
     delete ctx;
     return MIOC_EHIP;
@@ -544,6 +554,10 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   }
   if (option == MIOC_OPT_PERSIST) {
     ctx->opt_persist = value != 0;
+    return MIOC_OK;
+  }
+  if (option == MIOC_OPT_PRED_FMA) {
+    ctx->pred_fma = value != 0;
     return MIOC_OK;
   }
   return fail(ctx, MIOC_EINVAL, "unknown option");
@@ -757,11 +771,22 @@ int32_t mioc_backtrack(mioc_ctx *ctx, int64_t B_use, double *u_out, double *phi_
   return MIOC_OK;
 }
 
+extern "C++" {
+namespace {
+int trm_check_err(mioc_ctx *ctx);
+}  // namespace
+}
+
 int32_t mioc_synchronize(mioc_ctx *ctx) {
   if (!ctx) return MIOC_EINVAL;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   ev_collect(ctx);
+  if (ctx->trm_pending) {
+    ctx->trm_pending = false;
+    int rc = trm_check_err(ctx);
+    if (rc) return rc;
+  }
   return check_run(ctx);
 }
 
@@ -773,6 +798,120 @@ int32_t mioc_get_ranks_device(mioc_ctx *ctx, int32_t *d_ranks_out) {
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipMemcpyAsync(d_ranks_out, ctx->d_ranks, (size_t)ctx->K * ctx->nt * sizeof(int32_t),
                               hipMemcpyDeviceToDevice, ctx->stream));
+  return MIOC_OK;
+}
+
+// ---- trust-region quantities (multi-trust.jl:117-158, HelpFunctions.jl:251-268) -------------------------
+extern "C++" {
+namespace {
+
+TrmDev trm_dev(const mioc_ctx *ctx, int mode, int64_t K, int64_t nt) {
+  TrmDev T;
+  T.K = (int)K;
+  T.M = (int)ctx->M;
+  T.nt = (int)nt;
+  T.L = (int)ctx->L;
+  T.dt = ctx->dt;
+  T.beta = ctx->beta;
+  T.p_kind = ctx->p_kind;
+  T.p_int = (int)ctx->p_int;
+  T.mode = mode;
+  T.fma = ctx->pred_fma ? 1 : 0;
+  T.df = ctx->d_df;
+  T.uold = ctx->d_uold;
+  T.ranks = ctx->d_ranks;
+  T.nuval = ctx->d_nuval;
+  T.vals = ctx->d_vals;
+  T.voff = ctx->d_voff;
+  T.g2r = ctx->d_g2r;
+  T.tvw = ctx->d_tvw;
+  T.tvw_len = ctx->tvw_len;
+  T.err = reinterpret_cast<int32_t *>(ctx->d_pred_own + 4);
+  return T;
+}
+
+int trm_ready(mioc_ctx *ctx) {
+  if (!ctx) return MIOC_EINVAL;
+  if (!ctx->have_levels || !ctx->have_cost) return fail(ctx, MIOC_ESTATE, "levels and cost must be set first");
+  if (ctx->p_kind == MIOC_P_TABLE && !ctx->d_g2r)
+    return fail(ctx, MIOC_EINVAL, "TV_p with MIOC_P_TABLE needs the level grid lookup (grid too large)");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, MIOC_EHIP, "hipSetDevice failed");
+  return MIOC_OK;
+}
+
+int trm_check_err(mioc_ctx *ctx) {
+  int32_t e = 0;
+  HIP_TRY(ctx, hipMemcpy(&e, ctx->d_pred_own + 4, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (e) return fail(ctx, MIOC_EINVAL, "TV_p: a control difference is outside the weight table (MIOC_P_INTLUT key "
+                                       "beyond table_len, or MIOC_P_TABLE control off the level grid)");
+  return MIOC_OK;
+}
+
+}  // namespace
+}  // extern "C++"
+
+int32_t mioc_pred(mioc_ctx *ctx, double *int_val, double *tv_old, double *tv_new, double *pred) {
+  int rc = trm_ready(ctx);
+  if (rc) return rc;
+  if (!ctx->have_path || !ctx->d_df || !ctx->d_uold || !ctx->d_ranks)
+    return fail(ctx, MIOC_ESTATE, "pred needs a backtrack result (mioc_backtrack first)");
+  if (ctx->K != 1) return fail(ctx, MIOC_ESTATE, "host pred after a batched bellman: use mioc_pred_batch_device");
+  double *o = ctx->d_pred_own;
+  TrmDev T = trm_dev(ctx, 7, 1, ctx->nt);
+  T.out_int = o, T.out_told = o + 1, T.out_tnew = o + 2, T.out_pred = o + 3;
+  HIP_TRY(ctx, hipMemsetAsync(o + 4, 0, sizeof(double), ctx->stream));
+  HIP_TRY(ctx, launch_trm_pred(ctx->stream, T));
+  double h[5];
+  HIP_TRY(ctx, hipMemcpyAsync(h, o, 5 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  int32_t e;
+  std::memcpy(&e, &h[4], sizeof(e));
+  if (e) return trm_check_err(ctx);
+  if (int_val) *int_val = h[0];
+  if (tv_old) *tv_old = h[1];
+  if (tv_new) *tv_new = h[2];
+  if (pred) *pred = h[3];
+  return MIOC_OK;
+}
+
+int32_t mioc_pred_batch_device(mioc_ctx *ctx, double *d_int_val, double *d_tv_old, double *d_tv_new, double *d_pred) {
+  int rc = trm_ready(ctx);
+  if (rc) return rc;
+  if (!ctx->have_path || !ctx->d_df || !ctx->d_uold || !ctx->d_ranks)
+    return fail(ctx, MIOC_ESTATE, "pred needs a backtrack result");
+  TrmDev T = trm_dev(ctx, 7, ctx->K, ctx->nt);
+  T.out_int = d_int_val, T.out_told = d_tv_old, T.out_tnew = d_tv_new, T.out_pred = d_pred;
+  HIP_TRY(ctx, hipMemsetAsync(ctx->d_pred_own + 4, 0, sizeof(double), ctx->stream));
+  HIP_TRY(ctx, launch_trm_pred(ctx->stream, T));
+  ctx->trm_pending = true;
+  return MIOC_OK;
+}
+
+int32_t mioc_tv_device(mioc_ctx *ctx, int64_t K, const double *d_u, int64_t nx, int64_t nt, double *d_tv) {
+  int rc = trm_ready(ctx);
+  if (rc) return rc;
+  if (!d_u || !d_tv) return fail(ctx, MIOC_EINVAL, "null pointer");
+  if (K < 1 || nt < 1 || nt > INT32_MAX || K > INT32_MAX) return fail(ctx, MIOC_EINVAL, "bad K / nt");
+  if (nx != ctx->M) return fail(ctx, MIOC_EINVAL, "nx must equal the number of controls of the levels");
+  TrmDev T = trm_dev(ctx, 4, K, nt);
+  T.u = d_u;
+  T.out_tnew = d_tv;
+  HIP_TRY(ctx, hipMemsetAsync(ctx->d_pred_own + 4, 0, sizeof(double), ctx->stream));
+  HIP_TRY(ctx, launch_trm_pred(ctx->stream, T));
+  ctx->trm_pending = true;
+  return MIOC_OK;
+}
+
+int32_t mioc_trm_decide_device(mioc_ctx *ctx, int64_t K, const double *d_J_old, const double *d_J_new,
+                               const double *d_tv_old, const double *d_tv_new, const double *d_pred, double sigma,
+                               double *d_ared, int32_t *d_decision) {
+  int rc = trm_ready(ctx);
+  if (rc) return rc;
+  if (K < 1 || K > INT32_MAX) return fail(ctx, MIOC_EINVAL, "bad K");
+  if (!d_J_old || !d_J_new || !d_tv_old || !d_tv_new || !d_pred || !d_decision)
+    return fail(ctx, MIOC_EINVAL, "null pointer");
+  HIP_TRY(ctx, launch_trm_decide(ctx->stream, (int)K, d_J_old, d_J_new, d_tv_old, d_tv_new, d_pred, ctx->beta, sigma,
+                                 d_ared, d_decision));
   return MIOC_OK;
 }
 

@@ -131,6 +131,30 @@ hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev
 hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
                             const Start *start, int32_t *ranks, int32_t *nfallback);
 
+
+// ---- trust-region quantities around the DP (mioc_trm.hip) ---------------------------------------
+struct TrmDev {
+  int K = 0, M = 0, nt = 0, L = 0;
+  double dt = 0.0, beta = 0.0;
+  int p_kind = MIOC_P_ONE, p_int = 1;
+  int mode = 0;                    // 1: int_val, 2: TV(u_old), 4: TV(u)
+  int fma = 0;                     // int_val accumulated with fma (MIOC_OPT_PRED_FMA)
+  const double *df = nullptr;      // [K][nt][M]
+  const double *uold = nullptr;    // [K][nt][M]
+  const double *u = nullptr;       // [K][nt][M] control values, or null: the levels of `ranks`
+  const int32_t *ranks = nullptr;  // [K][nt] iterator ranks of u (u == null)
+  const double *nuval = nullptr;   // [L][M]
+  const int32_t *vals = nullptr, *voff = nullptr, *g2r = nullptr;  // grid lookup (MIOC_P_TABLE)
+  const double *tvw = nullptr;     // unscaled weights: by key (MIOC_P_INTLUT) or [L][L] (MIOC_P_TABLE)
+  long long tvw_len = 0;
+  double *out_int = nullptr, *out_told = nullptr, *out_tnew = nullptr, *out_pred = nullptr;  // [K] each
+  int32_t *err = nullptr;          // bit 0: a TV key / rank outside the weight table
+};
+hipError_t launch_trm_pred(hipStream_t s, const TrmDev &T);
+hipError_t launch_trm_decide(hipStream_t s, int K, const double *J_old, const double *J_new, const double *tv_old,
+                             const double *tv_new, const double *pred, double beta, double sigma, double *ared,
+                             int32_t *decision);
+
 }  // namespace mioc
 
 // ---- the context ----------------------------------------------------------------------------------
@@ -163,6 +187,11 @@ struct mioc_ctx {
   std::vector<double> table;
   double *d_costlut = nullptr;
   double *d_costtab = nullptr;
+  double *d_tvw = nullptr;         // unscaled weight table for TV_p (MIOC_P_INTLUT / MIOC_P_TABLE)
+  int64_t tvw_len = 0;
+  bool pred_fma = false;           // MIOC_OPT_PRED_FMA
+  double *d_pred_own = nullptr;    // mioc_pred staging: 4 doubles, then the TV error flag (int32)
+  bool trm_pending = false;        // a device pred / TV launch whose error flag mioc_synchronize reads
   int64_t costlut_len = 0;
 
   // owned problem inputs (device)

@@ -26,7 +26,7 @@ MIOC_ESTATE = -6
 MIOC_ENONFINITE = -7
 
 MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
-MIOC_OPT_ALGO, MIOC_OPT_TIMING, MIOC_OPT_PERSIST = 1, 2, 3
+MIOC_OPT_ALGO, MIOC_OPT_TIMING, MIOC_OPT_PERSIST, MIOC_OPT_PRED_FMA = 1, 2, 3, 4
 MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID, MIOC_ALGO_SEPARABLE = 0, 1, 2, 3, 4
 MIOC_ALGO_FUSED, MIOC_ALGO_FUSED_SEPARABLE = 5, 6
 
@@ -35,6 +35,7 @@ EXPORTED = [
     "mioc_set_cost", "mioc_bellman", "mioc_backtrack", "mioc_bellman_batch_device",
     "mioc_backtrack_batch_device", "mioc_synchronize", "mioc_stream", "mioc_kernel_stats",
     "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics", "mioc_get_argmin_table", "mioc_get_ranks_device",
+    "mioc_pred", "mioc_pred_batch_device", "mioc_tv_device", "mioc_trm_decide_device",
 ]
 
 
@@ -89,6 +90,11 @@ def load_library(path=None):
         "mioc_diagnostics": (i32, [vp, vp, i32]),
         "mioc_get_argmin_table": (i32, [vp, i64, i64, vp]),
         "mioc_get_ranks_device": (i32, [vp, vp]),
+        "mioc_pred": (i32, [vp, ctypes.POINTER(dbl), ctypes.POINTER(dbl), ctypes.POINTER(dbl),
+                            ctypes.POINTER(dbl)]),
+        "mioc_pred_batch_device": (i32, [vp, vp, vp, vp, vp]),
+        "mioc_tv_device": (i32, [vp, i64, vp, i64, i64, vp]),
+        "mioc_trm_decide_device": (i32, [vp, i64, vp, vp, vp, vp, vp, dbl, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -241,6 +247,46 @@ class Context:
         if not out.is_cuda or str(out.dtype) != "torch.int32" or not out.is_contiguous():
             raise ValueError("out must be a contiguous int32 CUDA tensor (K, nt)")
         self._check(self.lib.mioc_get_ranks_device(self.h, ctypes.c_void_p(out.data_ptr())))
+
+    # -- trust-region quantities of the last backtrack (multi-trust.jl:117-158) -------------------
+    def pred(self):
+        """(int_val, TV_p(u_old), TV_p(u), pred) of the last single-subproblem backtrack, on the device."""
+        out = [ctypes.c_double(0.0) for _ in range(4)]
+        self._check(self.lib.mioc_pred(self.h, *[ctypes.byref(x) for x in out]))
+        return tuple(x.value for x in out)
+
+    def pred_batch_tensors(self, int_val=None, tv_old=None, tv_new=None, pred=None):
+        """Per-subproblem int_val / TV_p(u_old) / TV_p(u) / pred of the last batch backtrack into (K,) float64
+        CUDA tensors (each optional); enqueued on the context's stream."""
+        for name, t in (("int_val", int_val), ("tv_old", tv_old), ("tv_new", tv_new), ("pred", pred)):
+            if t is not None and (not t.is_cuda or not t.is_contiguous() or str(t.dtype) != "torch.float64"):
+                raise ValueError(f"{name} must be a contiguous float64 CUDA tensor (K,)")
+        ptr = [ctypes.c_void_p(t.data_ptr()) if t is not None else None for t in (int_val, tv_old, tv_new, pred)]
+        self._check(self.lib.mioc_pred_batch_device(self.h, *ptr))
+
+    def tv_tensors(self, u, out):
+        """TV_p of controls u (K, nt, nx) float64 CUDA tensor into out (K,) float64; enqueued."""
+        if u.dim() != 3 or not u.is_contiguous() or not u.is_cuda or str(u.dtype) != "torch.float64":
+            raise ValueError("u must be a contiguous float64 CUDA tensor of shape (K, nt, nx)")
+        if not out.is_cuda or not out.is_contiguous() or str(out.dtype) != "torch.float64" or \
+                out.numel() != u.shape[0]:
+            raise ValueError("out must be a contiguous float64 CUDA tensor (K,)")
+        K, nt, nx = u.shape
+        self._check(self.lib.mioc_tv_device(self.h, K, ctypes.c_void_p(u.data_ptr()), nx, nt,
+                                            ctypes.c_void_p(out.data_ptr())))
+
+    def trm_decide_tensors(self, J_old, J_new, tv_old, tv_new, pred, sigma, decision, ared=None):
+        """multi-trust.jl:127-158 per subproblem: decision (K,) int32 = 2 stop / 1 halve / 0 accept."""
+        ts = (J_old, J_new, tv_old, tv_new, pred)
+        K = decision.numel()
+        for t in ts + ((ared,) if ared is not None else ()):
+            if not t.is_cuda or not t.is_contiguous() or str(t.dtype) != "torch.float64" or t.numel() != K:
+                raise ValueError("J_old / J_new / tv_old / tv_new / pred / ared: contiguous float64 (K,)")
+        if not decision.is_cuda or str(decision.dtype) != "torch.int32" or not decision.is_contiguous():
+            raise ValueError("decision must be a contiguous int32 CUDA tensor (K,)")
+        self._check(self.lib.mioc_trm_decide_device(
+            self.h, K, *[ctypes.c_void_p(t.data_ptr()) for t in ts], float(sigma),
+            ctypes.c_void_p(ared.data_ptr()) if ared is not None else None, ctypes.c_void_p(decision.data_ptr())))
 
     def synchronize(self):
         self._check(self.lib.mioc_synchronize(self.h))

@@ -89,6 +89,11 @@ class SubproblemSolver:
         u, phi, _sw = self.ctx.backtrack(B_use)
         return u, phi
 
+    def pred(self):
+        """(int_val, TV_p(u_old), TV_p(u), pred) of the last backtrack, reduced on the device
+        (multi-trust.jl:117-126; mioc_pred)."""
+        return self.ctx.pred()
+
 
 def bellman_TRM_(solver, df, u_old, B, dt):
     """bellman_TRM!(∇f, u_old, B, β, p, Δt, nu, U, Φ, iterator) -- U/Φ are the solver's device state."""
@@ -149,10 +154,11 @@ def TRM(obj, par=None, x0=None, solver=None, device=0, rng=None):
     it = 1
     stop = False
     J_old = eval_f_(obj)
+    tv_u = TV_p(u, p)  # TV of the current u; afterwards every trial's TV_new from the device
     if par.log:
         print(" Iter |   k |   Δᵏ   |      J      |   pred   |   ared   |       step            ")
         print("-" * 81)
-        print(f"{0:5d} |{0:4d} | {D0:6.2f} | {J_old + beta * TV_p(u, p):.5e} | {0.0:8.4f} | {0.0:8.4f} | "
+        print(f"{0:5d} |{0:4d} | {D0:6.2f} | {J_old + beta * tv_u:.5e} | {0.0:8.4f} | {0.0:8.4f} | "
               f"Initial Value   ")
     while not stop and it <= maxiter:
         Dk = D0
@@ -160,7 +166,7 @@ def TRM(obj, par=None, x0=None, solver=None, device=0, rng=None):
         ared = 0.0
         pred = 1.0
         halved = False
-        TV_old = TV_p(u, p)
+        TV_old = tv_u  # TV_p(u, p) (multi-trust.jl:99): u is the last trial or the accepted control
         eval_df_(obj)
         grad = obj.df
         while ared < sigma * pred and k <= kmax:
@@ -170,14 +176,9 @@ def TRM(obj, par=None, x0=None, solver=None, device=0, rng=None):
             else:
                 bellman_TRM_(solver, grad, u_old, B, dt)
                 eval_u_TRM_(solver, u, u_old, B)
-            int_val = 0.0
-            for j in range(n):
-                s = 0.0
-                for m in range(u.shape[0]):
-                    s += grad[m, j] * (u_old[m, j] - u[m, j])
-                int_val += s
-            int_val *= dt
-            TV_new = TV_p(u, p)
+            # int_val = Δt Σ_j ∇f_j'(u_old_j - u_j) and TV_new = TV_p(u, p): O(nt) reductions on the device
+            int_val, _tv_uold, TV_new, _ = solver.pred()
+            tv_u = TV_new
             J_new = eval_f_(obj)
             pred = int_val + beta * (TV_old - TV_new)
             ared = J_old - J_new + beta * (TV_old - TV_new)
@@ -205,7 +206,7 @@ def TRM(obj, par=None, x0=None, solver=None, device=0, rng=None):
             k += 1
         it += 1
     eval_df_(obj)
-    return J + beta * TV_p(u, p)
+    return J + beta * tv_u
 
 
 __all__ = ["TRM_parameters", "TRM", "TV_p", "SubproblemSolver", "bellman_TRM_", "eval_u_TRM_", "rand_func",

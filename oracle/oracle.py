@@ -19,6 +19,7 @@ Reference citations (paths relative to the reference root):
   bellman_TRM!        HelpFunctions.jl:20-83
   eval_u_TRM!         HelpFunctions.jl:98-124
   TV_p                HelpFunctions.jl:251-268
+  pred (int_val, TV)  multi-trust.jl:117-126;  ared / step decision  multi-trust.jl:127-158
   product_iterator    julia_opt/AdmissibleIterators.jl:9-18
   bounded_sum_iterator/check_sum  julia_opt/AdmissibleIterators.jl:26-49
 """
@@ -292,6 +293,61 @@ def tv_p_py(u, p):
         else:
             raise ValueError("Only positive integer valued `p` are accepted!")
     return val
+
+
+def tv_p_kind(u, p_kind, p_int=1, wtab=None, lv=None):
+    """TV_p (HelpFunctions.jl:251-268) under mioc_set_cost's weight conventions: p = 1 / Inf computed, integer
+    p >= 2 as wtab[sum |d|^p] (Julia's Float64(S)^(1/p), host-supplied), MIOC_P_TABLE as wtab[r_{i-1} L + r_i].
+    Summed over i = 2..n in order from 0.0, as the reference's loop."""
+    u = np.asarray(u, dtype=np.float64)
+    M, n = u.shape
+    rank = None
+    if p_kind == P_TABLE:
+        rank = {tuple(float(x) for x in lv.nuval[r]): r for r in range(lv.L)}
+    val = 0.0
+    for i in range(1, n):
+        d = [abs(float(u[m, i]) - float(u[m, i - 1])) for m in range(M)]
+        if p_kind == P_INF:
+            t = max(d)
+        elif p_kind == P_ONE:
+            t = 0.0
+            for x in d:
+                t += x
+        elif p_kind == P_INTLUT:
+            t = float(wtab[sum(int(x) ** p_int for x in d)])
+        else:
+            ra = rank[tuple(float(x) for x in u[:, i - 1])]
+            rb = rank[tuple(float(x) for x in u[:, i])]
+            t = float(wtab[ra * lv.L + rb])
+        val += t
+    return val
+
+
+def _fma(a, b, c):
+    """fl(a*b + c) with one rounding (Fraction -> float rounds correctly)."""
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def pred_py(df, u_old, u, dt, beta, tv_old, tv_new, fma=False):
+    """multi-trust.jl:117-126: int_val = Δt·Σ_j ∇f[:,j]'(u_old[:,j] − u[:,j]) (j in order, each dot a left-to-right
+    sum of products as BLAS ddot's tail loop; fma=True: an FMA-contracted ddot), pred = int_val + β(TV_old − TV_new).
+    Returns (int_val, pred)."""
+    M, n = df.shape
+    int_val = 0.0
+    for j in range(n):
+        s = 0.0
+        for m in range(M):
+            v = float(u_old[m, j]) - float(u[m, j])
+            s = _fma(float(df[m, j]), v, s) if fma else s + float(df[m, j]) * v
+        int_val += s
+    int_val *= dt
+    return int_val, int_val + beta * (tv_old - tv_new)
+
+
+def trm_decide_py(J_old, J_new, tv_old, tv_new, pred, beta, sigma):
+    """multi-trust.jl:127-158: ared and the decision (2 stop, 1 halve Δ, 0 accept)."""
+    ared = J_old - J_new + beta * (tv_old - tv_new)
+    return ared, (2 if pred <= 0 else 1 if ared < sigma * pred else 0)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -90,12 +90,20 @@ class OracleSolver:
         self.beta = beta
 
     def bellman(self, df, u_old, B, dt):
+        self.df, self.dt = np.array(df, copy=True), dt
         self.uo = np.array(u_old, order="F", copy=True)
         self.B = B
         self.phi, self.U = self.oc.bellman(self.lv, df, u_old, B, self.pk, self.beta, dt)
 
     def backtrack(self, B_use):
-        return self.oc.backtrack(self.lv, self.uo, self.phi, self.U, self.B, B_use)
+        self.u, phi = self.oc.backtrack(self.lv, self.uo, self.phi, self.U, self.B, B_use)
+        return self.u, phi
+
+    def pred(self):
+        from oracle.oracle import pred_py, tv_p_kind
+        to, tn = tv_p_kind(self.uo, self.pk), tv_p_kind(self.u, self.pk)
+        iv, pr = pred_py(self.df, self.uo, self.u, self.dt, self.beta, to, tn)
+        return iv, to, tn, pr
 
 
 def test_trm_fishing_plumbing_with_oracle():
