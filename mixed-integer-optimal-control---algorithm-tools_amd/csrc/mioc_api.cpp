@@ -393,6 +393,7 @@ int run_bellman(mioc_ctx *ctx) {
     if (!rc) rc = grow(ctx, &D.kfirst, &cap_kf, kcells * sizeof(double), "class first ranks");
     if (rc) return rc;
     ctx->pinf_cap_k = std::min(cap_km, std::min(cap_k2, cap_kf));
+    pinf_plan((int)RP, (int)nt, D);
     rc = grow(ctx, &D.R, &ctx->pinf_cap_R, K * nt * RP * sizeof(double), "row minima R");
     if (rc) return rc;
     ev_begin(ctx, 2, "k_pinf_prep");

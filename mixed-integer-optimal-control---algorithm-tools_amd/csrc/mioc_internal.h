@@ -123,7 +123,10 @@ struct PinfDev {
   double *k2 = nullptr;            // [K][nt][BWP] second-smallest distinct value in the class
   int32_t *kfirst = nullptr;       // [K][nt][BWP] first rank attaining kmin
   double *R = nullptr;             // [K][nt][RP] row minima R_i[c] = min_r Φ_i[c, r]
+  int CH = 0, W = 0;               // the walk's staged steps per chunk and LDS row width (pinf_plan)
 };
+// the walk's chunk and band for a p = Inf problem (mioc_pinf.hip)
+void pinf_plan(int RP, int nt, PinfDev &D);
 hipError_t launch_pinf_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D);
 hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D);
 hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D, int Bu,

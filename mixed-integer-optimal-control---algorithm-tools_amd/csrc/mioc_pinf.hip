@@ -97,7 +97,60 @@ __global__ __launch_bounds__(256) void k_pinf_prep(ProblemDev P, LevelsDev Lv, P
   }
 }
 
+// Small level sets (L <= 64, BWP <= 16: the SOS1 shapes of C1-C3): one THREAD per (step, subproblem) walks the L
+// levels in rank order and keeps the class keys in registers -- the same three quantities as k_pinf_prep (first
+// minimum key, smallest other key, first rank at the minimum; keys compare as okey, so -0.0 < +0.0 as there).
+template <int BWP>
+__global__ __launch_bounds__(256) void k_pinf_prep_small(ProblemDev P, LevelsDev Lv, PinfDev D) {
+  const long long gi = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= (long long)P.K * P.nt) return;
+  const int k = (int)(gi / P.nt), i = (int)(gi % P.nt), M = P.M, BW = D.BW;
+  const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
+  const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
+  const bool term = (i == P.nt - 1);
+  double dfv[kMaxM], uov[kMaxM];
+  for (int m = 0; m < M; ++m) dfv[m] = dfi[m], uov[m] = uoi[m];
+  uint64_t km[BWP], k2[BWP];
+  int kf[BWP];
+#pragma unroll
+  for (int b = 0; b < BWP; ++b) km[b] = ~0ull, k2[b] = ~0ull, kf[b] = -1;
+  for (int r = 0; r < Lv.L; ++r) {
+    const double *nuv = Lv.nuval + (size_t)r * M;
+    const int b = p_bt(nuv, uov, M);
+    if (b >= BW) continue;
+    const double t1 = p_t1(nuv, dfv, M, P.dt);
+    const uint64_t key = okey(term ? t1 : t1 + Lv.beta);
+#pragma unroll
+    for (int q = 0; q < BWP; ++q) {
+      if (q != b) continue;
+      if (key < km[q]) {
+        k2[q] = km[q];  // every key seen so far is >= the old minimum, which is not the new one
+        km[q] = key;
+        kf[q] = r;
+      } else if (key != km[q] && key < k2[q]) {
+        k2[q] = key;
+      }
+    }
+  }
+  const size_t row = ((size_t)k * P.nt + i) * BWP;
+#pragma unroll
+  for (int q = 0; q < BWP; ++q) {
+    D.kmin[row + q] = from_okey(km[q]);
+    D.k2[row + q] = from_okey(k2[q]);
+    D.kfirst[row + q] = kf[q];
+  }
+}
+
 hipError_t launch_pinf_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D) {
+  if (Lv.L <= 64 && D.BWP <= 16) {
+    const long long n = (long long)P.K * P.nt;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (D.BWP == 8)
+      hipLaunchKernelGGL(k_pinf_prep_small<8>, grid, dim3(256), 0, s, P, Lv, D);
+    else
+      hipLaunchKernelGGL(k_pinf_prep_small<16>, grid, dim3(256), 0, s, P, Lv, D);
+    return hipGetLastError();
+  }
   dim3 grid(P.nt, P.K);
   size_t lds = (size_t)D.BW * 20 + 16;
   hipLaunchKernelGGL(k_pinf_prep, grid, dim3(256), lds, s, P, Lv, D);
@@ -364,21 +417,26 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 }
 
 __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, PinfDev D, const Start *start,
-                                                   int32_t *ranks, int32_t *nfallback, int CH) {
+                                                   int32_t *ranks, int32_t *nfallback) {
   extern __shared__ __attribute__((aligned(16))) double wsm[];
-  const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, nthr = blockDim.x;
-  const int M = P.M, nt = P.nt, RP = P.RP, BWP = D.BWP;
-  const bool walker = tid < 64;  // wave 0 walks; every wave stages
+  const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
+  const int M = P.M, nt = P.nt, RP = P.RP, BWP = D.BWP, CH = D.CH, W = D.W;
+  const bool walker = tid < 64;  // wave 0 walks; the other waves stage
   const Start st = start[k];
   if (st.status != MIOC_OK) return;
   int32_t *rk = ranks + (size_t)k * nt;
   if (tid == 0) rk[0] = st.r;
   if (nt == 1) return;
-  // LDS: Rb[2][CH][RP], Km[2][CH][BWP], K2[2][CH][BWP] (doubles), Kf[2][CH][BWP] (int32)
+  // LDS: Rb[2][CH][W], Km[2][CH][BWP], K2[2][CH][BWP] (doubles), Kf[2][CH][BWP] (int32), s_lo[2], s_c[2].
+  // Row `row` of a staged chunk holds R_{i0+2+row}[lo, lo + W): whole rows (lo = 0, W = RP), or, when the class
+  // window is narrow (SOS1 shapes), a band: the walk's budget only decreases, by at most BW - 1 per step, so a
+  // chunk staged while the walk is at budget c (one chunk ahead) reads R_{j+1}[c' - b] with
+  // c - 2 CH (BW - 1) - (BWP - 1) <= c' - b <= c.
   double *Rb = wsm;
-  double *Km = Rb + 2 * (size_t)CH * RP;
+  double *Km = Rb + 2 * (size_t)CH * W;
   double *K2 = Km + 2 * (size_t)CH * BWP;
   int32_t *Kf = reinterpret_cast<int32_t *>(K2 + 2 * (size_t)CH * BWP);
+  int *s_lo = reinterpret_cast<int *>(Kf + 2 * (size_t)CH * BWP);  // [2] band start of each staging buffer
   const double *R = D.R + (size_t)k * nt * RP;
   const size_t crow0 = (size_t)k * nt * BWP;
   const double *dfk = P.df + (size_t)k * nt * M;
@@ -386,17 +444,33 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
   const double beta = Lv.beta;
   const int nsteps = nt - 1;  // walk steps i = 0 .. nt-2
 
-  auto stage = [&](int q, int buf) {
+  auto stage = [&](int q, int buf, int cnow) {
     const int i0 = q * CH;
     const int ni = (i0 + CH <= nsteps ? CH : nsteps - i0);
     // class rows j = i0+1 .. i0+ni
     glds_copy(D.kmin + crow0 + (size_t)(i0 + 1) * BWP, Km + (size_t)buf * CH * BWP, ni * BWP * 8, tid, nthr);
     glds_copy(D.k2 + crow0 + (size_t)(i0 + 1) * BWP, K2 + (size_t)buf * CH * BWP, ni * BWP * 8, tid, nthr);
     glds_copy(D.kfirst + crow0 + (size_t)(i0 + 1) * BWP, Kf + (size_t)buf * CH * BWP, ni * BWP * 4, tid, nthr);
-    // R rows j+1 = i0+2 .. i0+ni+1 (row nt does not exist: the terminal step needs none)
+    // R bands of rows j+1 = i0+2 .. i0+ni+1 (row nt does not exist: the terminal step needs none); lo even, so
+    // every band starts 16-byte aligned (RP is a multiple of 64)
+    int lo = 0;
+    if (W < RP) {
+      lo = cnow - (W - 2);
+      lo = lo < 0 ? 0 : (lo & ~1);
+      if (lo + W > RP) lo = RP - W;
+    }
+    if (tid == 0) s_lo[buf] = lo;
     int nr = ni;
     if (i0 + 1 + nr > nt - 1) nr = nt - 1 - (i0 + 1);
-    if (nr > 0) glds_copy(R + (size_t)(i0 + 2) * RP, Rb + (size_t)buf * CH * RP, nr * RP * 8, tid, nthr);
+    const int per = (W * 8 + 1023) >> 10;  // 1 KiB pieces per band; a wave copies one piece per instruction
+    for (int pc = wave; pc < nr * per; pc += (nthr + 63) >> 6) {
+      const int row = pc / per, off = (pc - row * per) * 1024;
+      if (off + lane * 16 < W * 8)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void *)((const char *)(R + (size_t)(i0 + 2 + row) * RP + lo) +
+                                                             off + lane * 16),
+            (__attribute__((address_space(3))) void *)((char *)(Rb + ((size_t)buf * CH + row) * W) + off), 16, 0, 0);
+    }
   };
 
   int r = st.r, c = st.c, br;
@@ -408,19 +482,24 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
   }
   int fallbacks = 0;
   bool dead = false;
-  stage(0, 0);
+  // s_c[q & 1]: the walk's budget at the start of chunk q, written by the walker at the end of chunk q - 1 and
+  // read by every wave when it stages chunk q + 1 (two slots: a wave that stages late cannot see the next value)
+  int *s_c = s_lo + 2;
+  stage(0, 0, st.c);
+  if (tid == 0) s_c[0] = st.c;
   vm_drain();
   lds_barrier();
   const int nq = (nsteps + CH - 1) / CH;
   for (int q = 0; q < nq; ++q) {
     const int buf = q & 1;
     PI_T(w0);
-    if (q + 1 < nq) stage(q + 1, buf ^ 1);
+    if (q + 1 < nq) stage(q + 1, buf ^ 1, s_c[q & 1]);
     const int i0 = q * CH, i1 = (i0 + CH <= nsteps ? i0 + CH : nsteps);
     const double *KmB = Km + (size_t)buf * CH * BWP;
     const double *K2B = K2 + (size_t)buf * CH * BWP;
     const int32_t *KfB = Kf + (size_t)buf * CH * BWP;
-    const double *RbB = Rb + (size_t)buf * CH * RP;
+    const double *RbB = Rb + (size_t)buf * CH * W;
+    const int blo = s_lo[buf];
     const bool inb = lane < BWP;
     for (int i = i0; walker && !dead && i < i1; ++i) {
       const int row = i - i0, j = i + 1, cp = c - br;
@@ -431,7 +510,8 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
       const double kmr = KmB[row * BWP + lb];
       const double k2r = K2B[row * BWP + lb];
       const int kfr = KfB[row * BWP + lb];
-      const double xr = RbB[(size_t)row * RP + (xi > 0 ? xi : 0)];
+      const int xo = xi - blo;
+      const double xr = RbB[(size_t)row * W + (xo > 0 ? (xo < W ? xo : W - 1) : 0)];
       const double km = inb ? kmr : INFINITY;
       const double k2 = inb ? k2r : INFINITY;
       const int kf = inb ? kfr : INT_MAX;
@@ -474,7 +554,7 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
             if (bs == cp) val = t1;
           } else {
             Ks = t1 + beta;
-            if (cp >= bs && bs < BWP) val = Ks + RbB[(size_t)row * RP + cp - bs];
+            if (cp >= bs && bs < BWP) val = Ks + RbB[(size_t)row * W + cp - bs - blo];
           }
           if (val < INFINITY && Kr + val == target && s < sbest) {
             sbest = s;
@@ -505,6 +585,7 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
       br = winb;
     }
     PI_T(w1);
+    if (tid == 0) s_c[(q + 1) & 1] = c;  // the walker's budget for the next staging decision
     vm_drain();
     lds_barrier();
 #ifdef MIOC_STAMPS
@@ -521,18 +602,28 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
   if (tid == 0 && fallbacks) atomicAdd(nfallback, fallbacks);
 }
 
-int pinf_chunk_walk(int RP, int BWP) {
-  const int per = RP * 8 + BWP * 20;  // bytes per staged step
-  int ch = (96 * 1024) / (2 * per);
-  return ch < 1 ? 1 : (ch > 32 ? 32 : ch);
+// The walk's chunk and LDS row width: a band covering two chunks of budget descent plus one class window when that
+// is at most half a row (the narrow class windows of SOS1 problems: C1-C3 have BW = 4, W = 106 of RP = 832), else
+// whole rows with the largest chunk that fits 96 KB.
+void pinf_plan(int RP, int nt, PinfDev &D) {
+  (void)nt;
+  const int ch = 16, w = (2 * ch * (D.BW - 1) + D.BWP + 2 + 1) & ~1;
+  if (2 * w <= RP) {
+    D.CH = ch;
+    D.W = w;
+    return;
+  }
+  const int per = RP * 8 + D.BWP * 20;  // bytes per staged step
+  int c = (96 * 1024) / (2 * per);
+  D.CH = c < 1 ? 1 : (c > 32 ? 32 : c);
+  D.W = RP;
 }
 
 hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
                             const Start *start, int32_t *ranks, int32_t *nfallback) {
-  if (D.BWP > 64) return hipErrorInvalidValue;
-  const int CH = pinf_chunk_walk(P.RP, D.BWP);
-  size_t lds = (size_t)2 * CH * ((size_t)P.RP * 8 + (size_t)D.BWP * 20);
-  hipLaunchKernelGGL(k_pinf_walk, dim3(P.K), dim3(256), lds, s, P, Lv, D, start, ranks, nfallback, CH);
+  if (D.BWP > 64 || D.CH < 1 || D.W < 2) return hipErrorInvalidValue;
+  size_t lds = (size_t)2 * D.CH * ((size_t)D.W * 8 + (size_t)D.BWP * 20) + 32;
+  hipLaunchKernelGGL(k_pinf_walk, dim3(P.K), dim3(256), lds, s, P, Lv, D, start, ranks, nfallback);
   return hipGetLastError();
 }
 

@@ -1,7 +1,7 @@
-# round 2: GPU suite, default bench (C4 + p=Inf variant + C5 batch + CPU baselines), smoke
+# full GPU check: GPU suite, default bench (C4 + p=Inf variant + C5 batch + CPU baselines), smoke
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r2l
+O=gpurun_out/${1:-full}
 mkdir -p $O
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
 rc=$?; echo "tests exit=$rc"; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc

@@ -12,7 +12,7 @@ import pytest
 
 from mioc import native
 from mioc.synth import CONFIGS, make_inputs
-from oracle.oracle import P_ONE, Levels
+from oracle.oracle import P_INF, P_ONE, Levels
 
 pytestmark = pytest.mark.gpu
 
@@ -30,13 +30,15 @@ def _batch(cfg, K, nt=None, k0=0):
     return lt, dfs, uos, ddf, duo
 
 
-def _run(lt, cfg, algo, ddf, duo, B, Bp):
+def _run(lt, cfg, algo, ddf, duo, B, Bp, opts=None):
     import torch
     K = ddf.shape[0]
     ctx = native.Context(0)
     ctx.set_levels(lt)
     ctx.set_cost(cfg.p, cfg.beta)
     ctx.set_option(native.MIOC_OPT_ALGO, algo)
+    for o, v in (opts or {}).items():
+        ctx.set_option(o, v)
     du = torch.empty_like(ddf)
     dphi = torch.empty(K, dtype=torch.float64, device="cuda")
     dst = torch.empty(K, dtype=torch.int32, device="cuda")
@@ -162,3 +164,56 @@ def test_fused_tie_heavy_and_off_grid_vs_oracle(oracle_c, mode, algo):
             m = o >= 0
             assert np.array_equal(d[m], o[m]), f"{mode} restart {k} step {i}"
     ctx.close()
+
+
+@pytest.mark.parametrize("key,K", [("C2", 1024), ("C3", 256)])
+def test_pinf_batch_vs_generic_and_oracle(oracle_c, key, K):
+    """p = Inf restarts on the C2 / C3 shapes (multi-trust.jl:183-189 runs them at p = Inf): the class collapse
+    batch (per-thread class tables, banded walk) against the generic sweep for every restart, at B and B/2, and
+    against the oracle at full nt for a seeded subset; a zero-gradient batch makes every step a tie."""
+    import torch
+    cfg = CONFIGS[key]
+    lt, dfs, uos, ddf, duo = _batch(cfg, K)
+    res = {}
+    for algo in (native.MIOC_ALGO_PINF, native.MIOC_ALGO_GENERIC):
+        ctx, u, phi, st = _run(lt, cfg, algo, ddf, duo, cfg.B, cfg.B)
+        assert np.all(st == 0)
+        u2, p2, _ = _halved(ctx, ddf, cfg.B // 2)
+        res[algo] = (u, phi, u2, p2)
+        ctx.close()
+    for x, y in zip(res[native.MIOC_ALGO_PINF], res[native.MIOC_ALGO_GENERIC]):
+        bad = np.flatnonzero([not np.array_equal(p, q) for p, q in zip(x, y)])
+        assert bad.size == 0, f"restarts {bad[:8]} differ"
+    lv = Levels(lt.nu, [tuple(int(x) for x in t) for t in lt.tuples])
+    u, phi = res[native.MIOC_ALGO_PINF][:2]
+    rng = np.random.default_rng(K)
+    for k in sorted({0, K - 1} | {int(x) for x in rng.integers(0, K, size=2)}):
+        ophi, oU = oracle_c.bellman(lv, dfs[k], uos[k], cfg.B, P_INF, cfg.beta, cfg.dt)
+        ou, ops = oracle_c.backtrack(lv, uos[k], ophi, oU, cfg.B, cfg.B)
+        assert np.array_equal(u[k].T, ou) and phi[k] == ops, f"restart {k}"
+    # zero gradient: every level of a class has the same K, so every step is a tie that the first rank must win
+    z = torch.zeros_like(ddf[:8])
+    ctx, u, phi, st = _run(lt, cfg, native.MIOC_ALGO_PINF, z, duo[:8].contiguous(), cfg.B, cfg.B)
+    assert ctx.diagnostics()[3] == 0
+    for k in range(8):
+        ophi, oU = oracle_c.bellman(lv, np.zeros_like(dfs[k]), uos[k], cfg.B, P_INF, cfg.beta, cfg.dt)
+        ou, ops = oracle_c.backtrack(lv, uos[k], ophi, oU, cfg.B, cfg.B)
+        assert np.array_equal(u[k].T, ou) and phi[k] == ops, f"zero-gradient restart {k}"
+    ctx.close()
+
+
+@pytest.mark.parametrize("nt", [3, 17, 18, 33, 34, 35, 200])
+def test_pinf_banded_walk_chunk_edges_vs_oracle(oracle_c, nt):
+    """The banded p = Inf walk (a band of each R row staged in LDS) at chunk-boundary step counts, against the
+    oracle restart by restart: C2 levels (B = 819, so the band is narrower than a row) and a budget small enough
+    (B = 5) that the whole row is staged."""
+    cfg = CONFIGS["C2"]
+    lt, dfs, uos, ddf, duo = _batch(cfg, 6, nt=nt)
+    lv = Levels(lt.nu, [tuple(int(x) for x in t) for t in lt.tuples])
+    for B in (cfg.B, 5):
+        ctx, u, phi, st = _run(lt, cfg, native.MIOC_ALGO_PINF, ddf, duo, B, B)
+        for k in range(6):
+            ophi, oU = oracle_c.bellman(lv, dfs[k], uos[k], B, P_INF, cfg.beta, cfg.dt)
+            ou, ops = oracle_c.backtrack(lv, uos[k], ophi, oU, B, B)
+            assert np.array_equal(u[k].T, ou) and phi[k] == ops and st[k] == 0, f"nt={nt} B={B} restart {k}"
+        ctx.close()
