@@ -55,6 +55,8 @@ def parse(argv=None):
     ap.add_argument("--variant", default="pinf", help="extra p=Inf line on the same config ('' or none to skip)")
     ap.add_argument("--batch-config", default="C5", help="the batch line's config ('none' to skip)")
     ap.add_argument("--batch-size", type=int, default=1024, help="batch line: subproblems per rank per step")
+    ap.add_argument("--pinf-batch-config", default="C2",
+                    help="the p=Inf batch line's config (the reference's main() runs C1-C3 at p=Inf; 'none' to skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=5, help="recursion steps timed for the C4 CPU baseline")
     ap.add_argument("--solver", default="native", choices=["native", "oracle"],
@@ -259,7 +261,7 @@ def candidates_per_step(levels, uo, B):
     return levels.L * tot / max(1, nt - 1)
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, cfg=None):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/roundN_pmc_traffic.json,
     made by scripts/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None."""
     import glob
@@ -269,9 +271,12 @@ def pmc_traffic(kernel):
     for f in files:
         try:
             with open(f) as fh:
-                e = json.load(fh)["kernels"].get(kernel)
+                ks = json.load(fh)["kernels"]
         except (OSError, ValueError, KeyError):
             continue
+        # entries recorded from a single-config pass are qualified "kernel@CFG"; plain names come from the default
+        # bench passes, where each kernel belongs to one line (C4 headline / its p=Inf variant / the C5 batch)
+        e = ks.get(f"{kernel}@{cfg}") or (ks.get(kernel) if cfg in (None, "C4", "C5") else None)
         if e and "hbm_bytes_per_launch" in e:
             found.append((int(re.search(r"round(\d+)_", os.path.basename(f)).group(1)), e["hbm_bytes_per_launch"], f))
     if not found:
@@ -331,8 +336,9 @@ def roofline_of(res):
         bw = int(min(B, sum(max(v) - min(v) for v in lv.nu))) + 1
         bytes_per_launch = K * nt * (bw * 8 + (B + 1) * 8)
         ops = 2.0 * K * (nt - 1) * (B + 1) * bw
+        steps = nt - 1  # one launch runs the whole recursion
     ach = bytes_per_launch / avg_s / 1e9
-    traffic, tsrc = pmc_traffic(name)
+    traffic, tsrc = pmc_traffic(name, res["config"])
     roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None if traffic is None else round(traffic),
             "traffic_source": tsrc, "kernel": name,
@@ -391,14 +397,17 @@ def cpu_baseline(cfg_name, p_over, cpu_steps):
         t0 = time.perf_counter()
         one(jobs[0])
         t1 = time.perf_counter() - t0
+        # rounds of `threads` restarts until about 3 s of wall time (small restarts take milliseconds each)
+        rounds = max(1, min(256, int(3.0 / max(t1, 1e-4))))
         t0 = time.perf_counter()
         with ThreadPoolExecutor(threads) as ex:
-            list(ex.map(one, jobs))
+            list(ex.map(one, jobs * rounds))
         tn = time.perf_counter() - t0
-        return {"value": round(threads / tn, 6), "unit": "subproblems/s", "cores": threads, "kind": "port",
+        return {"value": round(threads * rounds / tn, 6), "unit": "subproblems/s", "cores": threads, "kind": "port",
                 "value_1thread": round(1.0 / t1, 6),
-                "sample": f"{threads} full restarts (nt={cfg.nt}, L={lt.L}, B={cfg.B}) of the reference loop "
-                          f"(C restatement), one per thread: {tn:.2f} s; one alone {t1:.2f} s; {host}"}
+                "sample": f"{threads * rounds} full restarts (nt={cfg.nt}, L={lt.L}, B={cfg.B}, p="
+                          f"{'inf' if p == math.inf else int(p)}) of the reference loop (C restatement), "
+                          f"{threads} threads: {tn:.2f} s; one alone {t1:.3f} s; {host}"}
     per_step = {}
     for nthr, steps in ((1, cpu_steps), (threads, cpu_steps * max(1, min(threads, 8)))):
         lt, df, uo = make_inputs(cfg, nt=steps + 1)
@@ -460,20 +469,30 @@ def main():
                    "unit": "subproblems/s", "ms_per_step": round(1e3 * r2["elapsed"] / r2["steps"], 3),
                    "algorithm": native_name(r2["algo"]), "roofline": roof2, "roofline_valu": valu2,
                    "backtrack_ms": round(r2["walk_ms"] / max(1, r2["steps"]), 3)}
-    if args.batch_config not in ("", "none") and args.nt is None:
-        r3 = run(args, args.batch_config, args.batch_size, None, None, rank, world, device, dist, torch,
+    def batch_line(cfg_name):
+        r3 = run(args, cfg_name, args.batch_size, None, None, rank, world, device, dist, torch,
                  max(args.steps, 3), args.warmup)
-        batch = {"config": {"workload": workload(r3), "parallelism": f"dp{world} (independent restarts)"},
-                 "value": round(world * r3["K"] * r3["steps"] / r3["elapsed"], 3), "unit": "subproblems/s",
-                 "n_gpus": world, "scaling": "weak", "steps": r3["steps"],
-                 "ms_per_step": round(1e3 * r3["elapsed"] / r3["steps"], 3),
-                 "algorithm": {native_name(r3["algo"]): r3["dom_name"]},
-                 "exact_scan_targets": {"near_tie": r3["diag"][0], "out_of_binade_or_few": r3["diag"][1]},
-                 "checksum": r3.get("gathered_checksum")}
+        line = {"config": {"workload": workload(r3), "parallelism": f"dp{world} (independent restarts)"},
+                "value": round(world * r3["K"] * r3["steps"] / r3["elapsed"], 3), "unit": "subproblems/s",
+                "n_gpus": world, "scaling": "weak", "steps": r3["steps"],
+                "ms_per_step": round(1e3 * r3["elapsed"] / r3["steps"], 3),
+                "algorithm": {native_name(r3["algo"]): r3["dom_name"]},
+                "checksum": r3.get("gathered_checksum")}
         if args.solver == "native":
-            batch["roofline"], batch["roofline_valu"] = roofline_of(r3)
+            if r3["algo"] == 2:
+                line["backtrack_ms"] = round(r3["walk_ms"] / max(1, r3["steps"]), 3)
+            else:
+                line["exact_scan_targets"] = {"near_tie": r3["diag"][0], "out_of_binade_or_few": r3["diag"][1]}
+            line["roofline"], line["roofline_valu"] = roofline_of(r3)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            batch["cpu_baseline"] = cpu_baseline(args.batch_config, None, args.cpu_steps)
+            line["cpu_baseline"] = cpu_baseline(cfg_name, None, args.cpu_steps)
+        return line
+
+    batch_pinf = None
+    if args.batch_config not in ("", "none") and args.nt is None:
+        batch = batch_line(args.batch_config)
+    if args.pinf_batch_config not in ("", "none") and args.nt is None:
+        batch_pinf = batch_line(args.pinf_batch_config)
     if rank == 0:
         value = world * res["K"] * args.steps / res["elapsed"]
         out = {
@@ -504,6 +523,8 @@ def main():
             out["variant_p_inf"] = variant
         if batch:
             out["batch"] = batch
+        if batch_pinf:
+            out["batch_p_inf"] = batch_pinf
         if not args.no_cpu_baseline and world == 1 and args.nt is None and args.solver == "native":
             out["cpu_baseline"] = cpu_baseline(args.config, args.p, args.cpu_steps)
         print(json.dumps(out), flush=True)

@@ -1,6 +1,7 @@
 """Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into HBM bytes per kernel launch.
 
-Usage: python scripts/pmc_traffic.py OUT.json LABEL=DIR/NAME_counter_collection.csv ...
+Usage: python scripts/pmc_traffic.py OUT.json [CFG:]LABEL=DIR/NAME_counter_collection.csv ...
+A CFG: prefix (a pass over one bench config, e.g. `bench.py --config C2 ...`) stores the kernels as "name@CFG".
 FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE
 reports half the bytes of wide reads, so it is doubled; WRITE_SIZE is taken as is.  Both counters
 count Infinity-Cache hits as memory-side traffic.
@@ -21,12 +22,13 @@ def main():
     res = {}
     for spec in sys.argv[2:]:
         label, path = spec.split("=", 1)
+        cfg = label.split(":", 1)[0] if ":" in label else None
         acc = defaultdict(lambda: defaultdict(list))
         with open(path) as f:
             for row in csv.DictReader(f):
                 acc[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
         for k, d in acc.items():
-            e = res.setdefault(k, {})
+            e = res.setdefault(f"{k}@{cfg}" if cfg else k, {})
             for cname, vals in d.items():
                 scale = 1024.0 * (2.0 if cname == "FETCH_SIZE" else 1.0)
                 e[cname.lower() + "_bytes_per_launch"] = scale * sum(vals) / len(vals)
