@@ -131,4 +131,18 @@ function eval_u_TRM!(ctx::Context, u::Matrix{Float64}, B::Int64)
     phi[]
 end
 
+"""
+    pred(ctx) -> (int_val, TV_old, TV_new, pred)
+
+The reductions of multi-trust.jl:117-126 for the last eval_u_TRM! on the device: int_val = Δt·Σ_j
+∇f[:,j]'(u_old[:,j] - u[:,j]), TV_p (HelpFunctions.jl:251-268) of u_old and of u with the context's p, and
+pred = int_val + β(TV_old - TV_new).  Sums run in the reference's loop order.
+"""
+function pred(ctx::Context)
+    iv, to, tn, pr = Ref(0.0), Ref(0.0), Ref(0.0), Ref(0.0)
+    check(ctx, ccall((:mioc_pred, libmioc), Int32,
+                     (Ptr{Cvoid}, Ref{Float64}, Ref{Float64}, Ref{Float64}, Ref{Float64}), ctx.ptr, iv, to, tn, pr))
+    (iv[], to[], tn[], pr[])
+end
+
 end # module
