@@ -163,6 +163,33 @@ int32_t mioc_trm_decide_device(mioc_ctx *ctx, int64_t K, const double *d_J_old, 
                                const double *d_tv_old, const double *d_tv_new, const double *d_pred, double sigma,
                                double *d_ared, int32_t *d_decision);
 
+/*
+ * Multi-device batch from one process (SURVEY §8 b, `mioc_batch_multi`): K subproblems in host arrays (K x nx x nt,
+ * each nx x nt column-major) are split into contiguous blocks over the nctx contexts -- one per device, each with
+ * the same levels and cost already set -- and every block is solved on its context's device from its own host
+ * thread: bellman_TRM! at B, then eval_u_TRM! at B_use (<= B).  u_out: K x nx x nt; phi_star, status: K entries
+ * (nullable).  Synchronous.  On error the return is the first failing context's status, and
+ * mioc_last_error(ctxs[0]) names that context.  (For one process per GPU over RCCL see INTEGRATION.md.)
+ */
+int32_t mioc_batch_multi(mioc_ctx *const *ctxs, int32_t nctx, int64_t K, const double *df, const double *u_old,
+                         int64_t nx, int64_t nt, int64_t B, double dt, int64_t B_use, double *u_out, double *phi_star,
+                         int32_t *status);
+
+/*
+ * The ODE gradient producer of the reference's TRM examples, batched on the device:
+ * eval_f! / eval_df! of julia_opt/ODEObjective.jl:125-184 (explicit Euler forward, trapezoid cost, explicit-Euler
+ * adjoint, df = Gu - Fu'λ) with the hooks of example_fishing.jl / example_doubletank.jl / example_vanderpol.jl.
+ * d_x: K x nx x nt controls (nx = 3, the DP's input layout); d_J: K objective values (nullable); d_df: K x nx x nt
+ * gradients (nullable), ready for mioc_bellman_batch_device.  τ = (T1 - T0) / nt.  params (nullable: the examples'
+ * values) holds, in order: fishing α, β, γ, δ, c1, c2, v1[3], v2[3], y0[2] (14); doubletank k1, k2, c[3], y0[2] (7);
+ * vanderpol c[3], y0[2] (5).  Enqueued on the context's stream.
+ */
+#define MIOC_ODE_FISHING 1
+#define MIOC_ODE_DOUBLETANK 2
+#define MIOC_ODE_VANDERPOL 3
+int32_t mioc_ode_eval_device(mioc_ctx *ctx, int32_t problem, int64_t K, const double *d_x, int64_t nx, int64_t nt,
+                             double T0, double T1, const double *params, int32_t nparams, double *d_J, double *d_df);
+
 /* The HIP stream the context enqueues on (hipStream_t), for callers that order their own work. */
 void *mioc_stream(mioc_ctx *ctx);
 

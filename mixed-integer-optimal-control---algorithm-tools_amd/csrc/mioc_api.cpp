@@ -8,6 +8,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mioc_internal.h"
@@ -96,7 +97,7 @@ void free_all(mioc_ctx *ctx) {
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
                   ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm,
-                  ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own};
+                  ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own, ctx->d_ode_state};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (ctx->h_flags) hipHostFree(ctx->h_flags);
@@ -769,6 +770,101 @@ int32_t mioc_backtrack(mioc_ctx *ctx, int64_t B_use, double *u_out, double *phi_
       switch_mask[i] = sw;
     }
   }
+  return MIOC_OK;
+}
+
+// One context's share of mioc_batch_multi: host arrays in, host arrays out, synchronous.
+static int32_t batch_host(mioc_ctx *ctx, int64_t K, const double *df, const double *u_old, int64_t nx, int64_t nt,
+                          int64_t B, double dt, int64_t B_use, double *u_out, double *phi_star, int32_t *status) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  rc = set_problem(ctx, K, nx, nt, B, dt);
+  if (rc) return rc;
+  const size_t n = (size_t)K * nx * nt;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->d_df, df, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->d_uold, u_old, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  rc = run_bellman(ctx);
+  if (rc) return rc;
+  double *d_u = nullptr, *d_phi = nullptr;
+  int32_t *d_st = nullptr;
+  size_t c0 = 0, c1 = 0, c2 = 0;
+  rc = grow(ctx, &d_u, &c0, n * sizeof(double), "multi-device u staging");
+  if (!rc) rc = grow(ctx, &d_phi, &c1, (size_t)K * sizeof(double), "multi-device phi staging");
+  if (!rc) rc = grow(ctx, &d_st, &c2, (size_t)K * sizeof(int32_t), "multi-device status staging");
+  if (!rc) rc = run_backtrack(ctx, B_use, d_u, d_phi, d_st);
+  if (!rc && hipMemcpyAsync(u_out, d_u, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    rc = fail(ctx, MIOC_EHIP, "u copy-out failed");
+  if (!rc && phi_star &&
+      hipMemcpyAsync(phi_star, d_phi, K * sizeof(double), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    rc = fail(ctx, MIOC_EHIP, "phi copy-out failed");
+  if (!rc && status &&
+      hipMemcpyAsync(status, d_st, K * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    rc = fail(ctx, MIOC_EHIP, "status copy-out failed");
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess && !rc) rc = fail(ctx, MIOC_EHIP, "hipStreamSynchronize failed");
+  if (!rc) rc = check_run(ctx);
+  for (void *p : {(void *)d_u, (void *)d_phi, (void *)d_st})
+    if (p) hipFree(p);
+  ev_collect(ctx);
+  return rc;
+}
+
+int32_t mioc_ode_eval_device(mioc_ctx *ctx, int32_t problem, int64_t K, const double *d_x, int64_t nx, int64_t nt,
+                             double T0, double T1, const double *params, int32_t nparams, double *d_J, double *d_df) {
+  if (!ctx) return MIOC_EINVAL;
+  // the examples' constants (example_fishing.jl, example_doubletank.jl, example_vanderpol.jl)
+  static const double fishing[14] = {1, 1, 1, 1, 1, 1, 0.2, 0.4, 0.01, 0.1, 0.2, 0.1, 0.5, 0.7};
+  static const double tank[7] = {2, 3, 1, 0.5, 2, 2, 2};
+  static const double vdp[5] = {-1, 0.75, -2, 1, 0};
+  const double *def = problem == MIOC_ODE_FISHING ? fishing : problem == MIOC_ODE_DOUBLETANK ? tank : vdp;
+  const int np = problem == MIOC_ODE_FISHING ? 14 : problem == MIOC_ODE_DOUBLETANK ? 7 : 5;
+  if (problem < MIOC_ODE_FISHING || problem > MIOC_ODE_VANDERPOL) return fail(ctx, MIOC_EINVAL, "unknown ODE problem");
+  if (nx != 3) return fail(ctx, MIOC_EINVAL, "the ODE examples have nx = 3 controls");
+  if (K < 1 || nt < 1 || K > INT32_MAX || nt > INT32_MAX || !d_x) return fail(ctx, MIOC_EINVAL, "bad K / nt / x");
+  if (params && nparams != np) return fail(ctx, MIOC_EINVAL, "wrong parameter count for this ODE problem");
+  if (!(T1 > T0)) return fail(ctx, MIOC_EINVAL, "need T1 > T0");
+  double par[14] = {};
+  for (int q = 0; q < np; ++q) par[q] = params ? params[q] : def[q];
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (d_df) {
+    int rc = grow(ctx, &ctx->d_ode_state, &ctx->ode_cap, (size_t)K * nt * 2 * sizeof(double), "ODE states");
+    if (rc) return rc;
+  } else if (!ctx->d_ode_state) {
+    int rc = grow(ctx, &ctx->d_ode_state, &ctx->ode_cap, (size_t)K * nt * 2 * sizeof(double), "ODE states");
+    if (rc) return rc;
+  }
+  const double tau = (T1 - T0) / (double)nt;  // ODEObjective.jl: τ = (T1 - T0) / nt
+  HIP_TRY(ctx, launch_ode_eval(ctx->stream, problem, (int)K, (int)nt, tau, par, np - 2, d_x, d_J, d_df,
+                               ctx->d_ode_state));
+  return MIOC_OK;
+}
+
+int32_t mioc_batch_multi(mioc_ctx *const *ctxs, int32_t nctx, int64_t K, const double *df, const double *u_old,
+                         int64_t nx, int64_t nt, int64_t B, double dt, int64_t B_use, double *u_out, double *phi_star,
+                         int32_t *status) {
+  if (!ctxs || nctx < 1 || !ctxs[0]) return MIOC_EINVAL;
+  for (int32_t d = 0; d < nctx; ++d) {
+    if (!ctxs[d]) return fail(ctxs[0], MIOC_EINVAL, "null context in the list");
+    for (int32_t e = 0; e < d; ++e)
+      if (ctxs[e] == ctxs[d]) return fail(ctxs[0], MIOC_EINVAL, "a context appears twice (contexts are not thread-safe)");
+  }
+  if (K < 1 || nx < 1 || nt < 1 || !df || !u_old || !u_out) return fail(ctxs[0], MIOC_EINVAL, "bad batch arguments");
+  std::vector<int32_t> rcs(nctx, MIOC_OK);
+  std::vector<std::thread> th;
+  const size_t per = (size_t)nx * nt;
+  for (int32_t d = 0; d < nctx; ++d) {
+    const int64_t lo = K * d / nctx, hi = K * (d + 1) / nctx;  // contiguous block, as mioc.batch.shard
+    if (hi <= lo) continue;
+    th.emplace_back([=, &rcs] {
+      rcs[d] = batch_host(ctxs[d], hi - lo, df + lo * per, u_old + lo * per, nx, nt, B, dt, B_use, u_out + lo * per,
+                          phi_star ? phi_star + lo : nullptr, status ? status + lo : nullptr);
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int32_t d = 0; d < nctx; ++d)
+    if (rcs[d] != MIOC_OK) {
+      if (d > 0) ctxs[0]->err = "context " + std::to_string(d) + ": " + ctxs[d]->err;
+      return rcs[d];
+    }
   return MIOC_OK;
 }
 

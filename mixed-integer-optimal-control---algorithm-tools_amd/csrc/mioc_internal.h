@@ -158,6 +158,9 @@ hipError_t launch_trm_decide(hipStream_t s, int K, const double *J_old, const do
                              const double *tv_new, const double *pred, double beta, double sigma, double *ared,
                              int32_t *decision);
 
+hipError_t launch_ode_eval(hipStream_t s, int problem, int K, int nt, double tau, const double *params, int y0off,
+                           const double *X, double *J, double *DF, double *ST);
+
 }  // namespace mioc
 
 // ---- the context ----------------------------------------------------------------------------------
@@ -194,7 +197,9 @@ struct mioc_ctx {
   int64_t tvw_len = 0;
   bool pred_fma = false;           // MIOC_OPT_PRED_FMA
   double *d_pred_own = nullptr;    // mioc_pred staging: 4 doubles, then the TV error flag (int32)
-  bool trm_pending = false;        // a device pred / TV launch whose error flag mioc_synchronize reads
+  bool trm_pending = false;
+  double *d_ode_state = nullptr;   // [K][nt][2] forward states of mioc_ode_eval_device
+  size_t ode_cap = 0;        // a device pred / TV launch whose error flag mioc_synchronize reads
   int64_t costlut_len = 0;
 
   // owned problem inputs (device)

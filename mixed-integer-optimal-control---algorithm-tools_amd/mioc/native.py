@@ -29,13 +29,15 @@ MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
 MIOC_OPT_ALGO, MIOC_OPT_TIMING, MIOC_OPT_PERSIST, MIOC_OPT_PRED_FMA = 1, 2, 3, 4
 MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID, MIOC_ALGO_SEPARABLE = 0, 1, 2, 3, 4
 MIOC_ALGO_FUSED, MIOC_ALGO_FUSED_SEPARABLE = 5, 6
+MIOC_ODE_FISHING, MIOC_ODE_DOUBLETANK, MIOC_ODE_VANDERPOL = 1, 2, 3
 
 EXPORTED = [
     "mioc_version", "mioc_create", "mioc_destroy", "mioc_last_error", "mioc_set_option", "mioc_set_levels",
     "mioc_set_cost", "mioc_bellman", "mioc_backtrack", "mioc_bellman_batch_device",
     "mioc_backtrack_batch_device", "mioc_synchronize", "mioc_stream", "mioc_kernel_stats",
     "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics", "mioc_get_argmin_table", "mioc_get_ranks_device",
-    "mioc_pred", "mioc_pred_batch_device", "mioc_tv_device", "mioc_trm_decide_device",
+    "mioc_pred", "mioc_pred_batch_device", "mioc_tv_device", "mioc_trm_decide_device", "mioc_batch_multi",
+    "mioc_ode_eval_device",
 ]
 
 
@@ -95,6 +97,8 @@ def load_library(path=None):
         "mioc_pred_batch_device": (i32, [vp, vp, vp, vp, vp]),
         "mioc_tv_device": (i32, [vp, i64, vp, i64, i64, vp]),
         "mioc_trm_decide_device": (i32, [vp, i64, vp, vp, vp, vp, vp, dbl, vp, vp]),
+        "mioc_batch_multi": (i32, [vp, i32, i64, vp, vp, i64, i64, i64, dbl, i64, vp, vp, vp]),
+        "mioc_ode_eval_device": (i32, [vp, i32, i64, vp, i64, i64, dbl, dbl, vp, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -288,6 +292,23 @@ class Context:
             self.h, K, *[ctypes.c_void_p(t.data_ptr()) for t in ts], float(sigma),
             ctypes.c_void_p(ared.data_ptr()) if ared is not None else None, ctypes.c_void_p(decision.data_ptr())))
 
+    def ode_eval_tensors(self, problem, x, T0, T1, J=None, df=None, params=None):
+        """eval_f! / eval_df! of an ODE example for K controls x (K, nt, 3) float64 CUDA tensor: J (K,) and df
+        (K, nt, 3) float64 CUDA tensors (each optional); enqueued (mioc_ode_eval_device)."""
+        if x.dim() != 3 or not x.is_contiguous() or not x.is_cuda or str(x.dtype) != "torch.float64":
+            raise ValueError("x must be a contiguous float64 CUDA tensor of shape (K, nt, nx)")
+        K, nt, nx = x.shape
+        for name, t, n in (("J", J, K), ("df", df, x.numel())):
+            if t is not None and (not t.is_cuda or not t.is_contiguous() or str(t.dtype) != "torch.float64" or
+                                  t.numel() != n):
+                raise ValueError(f"{name} must be a contiguous float64 CUDA tensor with {n} entries")
+        par = None if params is None else np.ascontiguousarray(params, dtype=np.float64)
+        self._check(self.lib.mioc_ode_eval_device(
+            self.h, int(problem), K, ctypes.c_void_p(x.data_ptr()), nx, nt, float(T0), float(T1),
+            None if par is None else _p(par), 0 if par is None else par.size,
+            ctypes.c_void_p(J.data_ptr()) if J is not None else None,
+            ctypes.c_void_p(df.data_ptr()) if df is not None else None))
+
     def synchronize(self):
         self._check(self.lib.mioc_synchronize(self.h))
 
@@ -323,6 +344,26 @@ class Context:
         out = np.zeros(8, dtype=np.int64)
         self._check(self.lib.mioc_diagnostics(self.h, _p(out), 8))
         return out.tolist()
+
+
+def batch_multi(ctxs, df, u_old, B, dt, B_use=None):
+    """mioc_batch_multi: K subproblems (host float64 arrays of shape (K, nt, nx), C-contiguous) split over the
+    contexts (one per device, levels and cost set), each block solved from its own host thread.
+    Returns (u (K, nt, nx), phi_star (K,), status (K,))."""
+    df = np.ascontiguousarray(df, dtype=np.float64)
+    u_old = np.ascontiguousarray(u_old, dtype=np.float64)
+    if df.ndim != 3 or df.shape != u_old.shape:
+        raise ValueError("df and u_old must have the same shape (K, nt, nx)")
+    K, nt, nx = df.shape
+    u = np.empty_like(df)
+    phi = np.empty(K, dtype=np.float64)
+    st = np.empty(K, dtype=np.int32)
+    arr = (ctypes.c_void_p * len(ctxs))(*[c.h.value for c in ctxs])
+    lib = ctxs[0].lib
+    rc = lib.mioc_batch_multi(arr, len(ctxs), K, _p(df), _p(u_old), nx, nt, int(B), float(dt),
+                              int(B if B_use is None else B_use), _p(u), _p(phi), _p(st))
+    ctxs[0]._check(rc)
+    return u, phi, st
 
 
 def pyramid_eligible(levels: LevelTable):

@@ -217,3 +217,27 @@ def test_pinf_banded_walk_chunk_edges_vs_oracle(oracle_c, nt):
             ou, ops = oracle_c.backtrack(lv, uos[k], ophi, oU, B, B)
             assert np.array_equal(u[k].T, ou) and phi[k] == ops and st[k] == 0, f"nt={nt} B={B} restart {k}"
         ctx.close()
+
+
+def test_batch_multi_contexts_equal_single_batch():
+    """mioc_batch_multi (SURVEY §8 b): a C5 batch split over two contexts on the one visible device (each block
+    from its own host thread) equals the single-context device batch restart by restart, at B and B/2."""
+    cfg = CONFIGS["C5"]
+    K = 96
+    lt, dfs, uos, ddf, duo = _batch(cfg, K, nt=512)
+    ctxs = []
+    for _ in range(2):
+        c = native.Context(0)
+        c.set_levels(lt)
+        c.set_cost(cfg.p, cfg.beta)
+        ctxs.append(c)
+    hdf, huo = ddf.cpu().numpy(), duo.cpu().numpy()
+    for Bu in (cfg.B, cfg.B // 2):
+        u, phi, st = native.batch_multi(ctxs, hdf, huo, cfg.B, cfg.dt, Bu)
+        ref, ru, rphi, rst = _run(lt, cfg, native.MIOC_ALGO_AUTO, ddf, duo, cfg.B, Bu)
+        assert np.array_equal(u, ru) and np.array_equal(phi, rphi) and np.array_equal(st, rst)
+        ref.close()
+    with pytest.raises(native.MiocNativeError):
+        native.batch_multi([ctxs[0], ctxs[0]], hdf, huo, cfg.B, cfg.dt)
+    for c in ctxs:
+        c.close()
