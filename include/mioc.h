@@ -190,6 +190,15 @@ int32_t mioc_batch_multi(mioc_ctx *const *ctxs, int32_t nctx, int64_t K, const d
 int32_t mioc_ode_eval_device(mioc_ctx *ctx, int32_t problem, int64_t K, const double *d_x, int64_t nx, int64_t nt,
                              double T0, double T1, const double *params, int32_t nparams, double *d_J, double *d_df);
 
+/*
+ * Random admissible starts, rand_func_int (HelpFunctions.jl:204-225) on the device: K piecewise-constant controls
+ * d_u_out (K x nx x nt, nx = the levels' M) with `jumps` distinct jump times drawn uniformly from steps 1..nt-1
+ * (the reference's 2..nt) and a uniformly random admissible level per segment.  jumps < 0: floor(nt / 10), the
+ * reference's default.  The stream is counter-based (seed, restart, draw), so a seed reproduces its controls on
+ * any device; it is not Julia's MersenneTwister stream (not reproducible outside Julia).  Enqueued.
+ */
+int32_t mioc_rand_start_device(mioc_ctx *ctx, int64_t K, int64_t nt, int64_t jumps, uint64_t seed, double *d_u_out);
+
 /* The HIP stream the context enqueues on (hipStream_t), for callers that order their own work. */
 void *mioc_stream(mioc_ctx *ctx);
 

@@ -838,6 +838,17 @@ int32_t mioc_ode_eval_device(mioc_ctx *ctx, int32_t problem, int64_t K, const do
   return MIOC_OK;
 }
 
+int32_t mioc_rand_start_device(mioc_ctx *ctx, int64_t K, int64_t nt, int64_t jumps, uint64_t seed, double *d_u_out) {
+  if (!ctx) return MIOC_EINVAL;
+  if (!ctx->have_levels) return fail(ctx, MIOC_ESTATE, "levels must be set first");
+  if (K < 1 || K > INT32_MAX || nt < 1 || nt > (1 << 24) || !d_u_out) return fail(ctx, MIOC_EINVAL, "bad K / nt / u");
+  if (jumps < 0) jumps = nt / 10;
+  if (jumps > nt - 1) return fail(ctx, MIOC_EINVAL, "jumps > nt - 1 (the reference's sample would throw)");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, launch_rand_start(ctx->stream, (int)K, (int)nt, (int)jumps, seed, levels_dev(ctx), d_u_out));
+  return MIOC_OK;
+}
+
 int32_t mioc_batch_multi(mioc_ctx *const *ctxs, int32_t nctx, int64_t K, const double *df, const double *u_old,
                          int64_t nx, int64_t nt, int64_t B, double dt, int64_t B_use, double *u_out, double *phi_star,
                          int32_t *status) {

@@ -158,6 +158,7 @@ hipError_t launch_trm_decide(hipStream_t s, int K, const double *J_old, const do
                              const double *tv_new, const double *pred, double beta, double sigma, double *ared,
                              int32_t *decision);
 
+hipError_t launch_rand_start(hipStream_t s, int K, int nt, int jumps, uint64_t seed, const LevelsDev &Lv, double *U);
 hipError_t launch_ode_eval(hipStream_t s, int problem, int K, int nt, double tau, const double *params, int y0off,
                            const double *X, double *J, double *DF, double *ST);
 

@@ -187,4 +187,71 @@ hipError_t launch_ode_eval(hipStream_t s, int problem, int K, int nt, double tau
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Restart generator: rand_func_int (HelpFunctions.jl:204-225) on the device.  The reference draws `jumps` distinct
+// jump times from 2..nt (1-based; here 1..nt-1) with MersenneTwister + StatsBase.sample and a random admissible
+// level per segment.  Julia's stream cannot be reproduced outside Julia, so this generator keeps the algorithm and
+// its distribution with a counter-based stream instead: value(seed, k, stream, idx) = mix(mix(seed + φ(k+1)) ^
+// (stream << 56) ^ idx), mix = splitmix64's finaliser; a uniform draw in [0, n) is (v >> 32) * n >> 32.  Jump times:
+// Robert Floyd's sampling without replacement (one lane, an LDS bitmap of the nt steps); segment s takes the level
+// of rank uniform_L(stream 2, s).  The tests restate the same stream on the host bit for bit.
+// ---------------------------------------------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ uint64_t rs_mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t rs_uniform(uint64_t key, uint64_t stream, uint64_t idx, uint32_t n) {
+  const uint64_t v = rs_mix(key ^ (stream << 56) ^ idx);
+  return (uint32_t)(((v >> 32) * (uint64_t)n) >> 32);
+}
+
+__global__ __launch_bounds__(256) void k_rand_start(int nt, int jumps, uint64_t seed, LevelsDev Lv, double *U) {
+  extern __shared__ uint32_t bits[];  // [nw] jump-time bitmap, then [256] per-thread segment counts
+  const int k = blockIdx.x, tid = threadIdx.x, nw = (nt + 31) >> 5, M = Lv.M;
+  uint32_t *cnt = bits + nw;
+  const uint64_t key = rs_mix(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(k + 1));
+  for (int w = tid; w < nw; w += 256) bits[w] = 0u;
+  __syncthreads();
+  if (tid == 0) {  // Floyd: a uniform `jumps`-subset of the N = nt - 1 candidate steps 1 .. nt-1
+    const int N = nt - 1;
+    for (int j = N - jumps + 1, q = 0; j <= N; ++j, ++q) {
+      const int t = 1 + (int)rs_uniform(key, 1, (uint64_t)q, (uint32_t)j);  // in [1, j]
+      const int pick = (bits[t >> 5] >> (t & 31)) & 1u ? j : t;
+      bits[pick >> 5] |= 1u << (pick & 31);
+    }
+  }
+  __syncthreads();
+  // segment index of step i = number of jump times <= i: each thread owns a contiguous range of words
+  const int wpt = (nw + 255) / 256, w0 = tid * wpt, w1 = min(nw, w0 + wpt);
+  uint32_t c = 0;
+  for (int w = w0; w < w1; ++w) c += __popc(bits[w]);
+  cnt[tid] = c;
+  __syncthreads();
+  uint32_t seg = 0;
+  for (int q = 0; q < tid; ++q) seg += cnt[q];
+  double *u = U + (size_t)k * nt * M;
+  int rank = -1;
+  uint32_t rseg = 0xFFFFFFFFu;
+  for (int i = w0 * 32; i < min(nt, w1 * 32); ++i) {
+    seg += (bits[i >> 5] >> (i & 31)) & 1u;
+    if (seg != rseg) {
+      rseg = seg;
+      rank = (int)rs_uniform(key, 2, (uint64_t)seg, (uint32_t)Lv.L);
+    }
+    for (int m = 0; m < M; ++m) u[(size_t)i * M + m] = Lv.nuval[(size_t)rank * M + m];
+  }
+}
+
+}  // namespace
+
+hipError_t launch_rand_start(hipStream_t s, int K, int nt, int jumps, uint64_t seed, const LevelsDev &Lv, double *U) {
+  const size_t lds = ((size_t)(nt + 31) / 32 + 256) * sizeof(uint32_t);
+  hipLaunchKernelGGL(k_rand_start, dim3(K), dim3(256), lds, s, nt, jumps, seed, Lv, U);
+  return hipGetLastError();
+}
+
 }  // namespace mioc

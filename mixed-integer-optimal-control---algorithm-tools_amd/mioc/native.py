@@ -37,7 +37,7 @@ EXPORTED = [
     "mioc_backtrack_batch_device", "mioc_synchronize", "mioc_stream", "mioc_kernel_stats",
     "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics", "mioc_get_argmin_table", "mioc_get_ranks_device",
     "mioc_pred", "mioc_pred_batch_device", "mioc_tv_device", "mioc_trm_decide_device", "mioc_batch_multi",
-    "mioc_ode_eval_device",
+    "mioc_ode_eval_device", "mioc_rand_start_device",
 ]
 
 
@@ -99,6 +99,7 @@ def load_library(path=None):
         "mioc_trm_decide_device": (i32, [vp, i64, vp, vp, vp, vp, vp, dbl, vp, vp]),
         "mioc_batch_multi": (i32, [vp, i32, i64, vp, vp, i64, i64, i64, dbl, i64, vp, vp, vp]),
         "mioc_ode_eval_device": (i32, [vp, i32, i64, vp, i64, i64, dbl, dbl, vp, i32, vp, vp]),
+        "mioc_rand_start_device": (i32, [vp, i64, i64, i64, ctypes.c_uint64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -308,6 +309,17 @@ class Context:
             None if par is None else _p(par), 0 if par is None else par.size,
             ctypes.c_void_p(J.data_ptr()) if J is not None else None,
             ctypes.c_void_p(df.data_ptr()) if df is not None else None))
+
+    def rand_start_tensor(self, out, seed, jumps=-1):
+        """rand_func_int (HelpFunctions.jl:204-225) for K restarts into out, a (K, nt, M) float64 CUDA tensor;
+        jumps < 0: floor(nt / 10).  Enqueued (mioc_rand_start_device)."""
+        if out.dim() != 3 or not out.is_contiguous() or not out.is_cuda or str(out.dtype) != "torch.float64":
+            raise ValueError("out must be a contiguous float64 CUDA tensor of shape (K, nt, M)")
+        K, nt, M = out.shape
+        if M != self.M:
+            raise ValueError("out's last dimension must be the levels' M")
+        self._check(self.lib.mioc_rand_start_device(self.h, K, nt, int(jumps), ctypes.c_uint64(int(seed)),
+                                                    ctypes.c_void_p(out.data_ptr())))
 
     def synchronize(self):
         self._check(self.lib.mioc_synchronize(self.h))

@@ -97,3 +97,73 @@ def test_device_trust_region_iteration_equals_host():
         host.close()
     assert set(np.unique(dec.cpu().numpy())) <= {0, 1, 2}
     ctx.close()
+
+
+# ---- rand_func_int on the device (HelpFunctions.jl:204-225) -------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def _mix(z):
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def _uniform(key, stream, idx, n):
+    v = _mix(key ^ ((stream << 56) & _M64) ^ idx)
+    return ((v >> 32) * n) >> 32
+
+
+def _rand_start_host(levels, nt, jumps, seed, k):
+    """Host restatement of k_rand_start's stream (test-only): Floyd's sample of the jump times, a level per segment."""
+    key = _mix((seed + 0x9E3779B97F4A7C15 * (k + 1)) & _M64)
+    N, S = nt - 1, set()
+    for q, j in enumerate(range(N - jumps + 1, N + 1)):
+        t = 1 + _uniform(key, 1, q, j)
+        S.add(j if t in S else t)
+    u = np.zeros((levels.M, nt))
+    seg = 0
+    for i in range(nt):
+        seg += i in S
+        u[:, i] = levels.nuval[_uniform(key, 2, seg, levels.L)]
+    return u, S
+
+
+@pytest.mark.parametrize("shape", ["sos1", "c5", "c4"])
+def test_rand_start_device(shape):
+    """Admissible piecewise-constant starts with exactly `jumps` distinct candidate jump times in 1..nt-1; the
+    device stream equals its host restatement bit for bit; seeds reproduce; jump times are uniform over steps."""
+    import torch
+    from mioc.synth import CONFIGS
+    lt = {"sos1": LevelTable([[0, 1]] * 3, mioc.bounded_sum_iterator([[0, 1]] * 3, 1, 1)),
+          "c5": CONFIGS["C5"].levels(), "c4": CONFIGS["C4"].levels()}[shape]
+    nt = {"sos1": 512, "c5": 4096, "c4": 65536}[shape]
+    K = {"sos1": 256, "c5": 64, "c4": 4}[shape]
+    ctx = native.Context(0)
+    ctx.set_levels(lt)
+    out = torch.empty(K, nt, lt.M, dtype=torch.float64, device="cuda")
+    ctx.rand_start_tensor(out, seed=1234)
+    out2 = torch.empty_like(out)
+    ctx.rand_start_tensor(out2, seed=1234)
+    out3 = torch.empty_like(out)
+    ctx.rand_start_tensor(out3, seed=1235)
+    ctx.synchronize()
+    u = out.cpu().numpy()
+    assert torch.equal(out, out2) and not torch.equal(out, out3)
+    rows = {tuple(r) for r in lt.nuval}
+    jumps = nt // 10
+    hits = np.zeros(nt)
+    for k in range(K):
+        assert all(tuple(c) in rows for c in u[k])
+        changes = np.flatnonzero(np.any(u[k][1:] != u[k][:-1], axis=1)) + 1
+        assert changes.size <= jumps
+        if k < 3:
+            hu, S = _rand_start_host(lt, nt, jumps, 1234, k)
+            assert np.array_equal(u[k].T, hu) and len(S) == jumps and set(changes) <= S
+        hits[changes] += 1
+    if shape == "sos1":  # each step 1..nt-1 is a candidate with probability jumps/(nt-1); a change needs a new level
+        p = jumps / (nt - 1) * (2 / 3)
+        assert abs(hits[1:].mean() / K - p) < 0.1 * p
+    with pytest.raises(native.MiocNativeError):
+        ctx.rand_start_tensor(out, seed=1, jumps=nt)
+    ctx.close()
