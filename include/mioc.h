@@ -126,6 +126,11 @@ int32_t mioc_bellman_batch_device(mioc_ctx *ctx, int64_t K, const double *d_df, 
                                   int64_t nx, int64_t nt, int64_t B, double dt);
 int32_t mioc_backtrack_batch_device(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_star,
                                     int32_t *d_status);
+/* The same with one budget per subproblem: d_B_use[k] (device, K int32, each 0 <= B_use[k] <= B) -- the
+ * per-restart trust-region radii after halving (multi-trust.jl:108-110, B_new = floor(Δᵏ/Δt) per restart).
+ * Reads the K budgets back once to validate them. */
+int32_t mioc_backtrack_batch_budgets_device(mioc_ctx *ctx, const int32_t *d_B_use, double *d_u_out, double *d_phi_star,
+                                            int32_t *d_status);
 int32_t mioc_synchronize(mioc_ctx *ctx);
 
 /*

@@ -84,6 +84,7 @@ ProblemDev problem_dev(const mioc_ctx *ctx) {
   P.dt = ctx->dt;
   P.df = ctx->d_df;
   P.uold = ctx->d_uold;
+  P.Bvec = ctx->Bvec;
   return P;
 }
 
@@ -736,6 +737,24 @@ int32_t mioc_backtrack_batch_device(mioc_ctx *ctx, int64_t B_use, double *d_u_ou
   if (rc) return rc;
   if (!d_u_out) return fail(ctx, MIOC_EINVAL, "null output pointer");
   return run_backtrack(ctx, B_use, d_u_out, d_phi_star, d_status);
+}
+
+int32_t mioc_backtrack_batch_budgets_device(mioc_ctx *ctx, const int32_t *d_B_use, double *d_u_out, double *d_phi_star,
+                                            int32_t *d_status) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (!d_u_out || !d_B_use) return fail(ctx, MIOC_EINVAL, "null pointer");
+  if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "backtrack called before bellman");
+  // the per-subproblem budgets must lie in [0, B]; checked on the device copy (a few bytes per subproblem)
+  std::vector<int32_t> hb(ctx->K);
+  HIP_TRY(ctx, hipMemcpyAsync(hb.data(), d_B_use, ctx->K * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (int32_t b : hb)
+    if (b < 0 || b > ctx->B) return fail(ctx, MIOC_ESTATE, "every B_use[k] must satisfy 0 <= B_use[k] <= B");
+  ctx->Bvec = d_B_use;
+  rc = run_backtrack(ctx, ctx->B, d_u_out, d_phi_star, d_status);
+  ctx->Bvec = nullptr;
+  return rc;
 }
 
 int32_t mioc_backtrack(mioc_ctx *ctx, int64_t B_use, double *u_out, double *phi_star, uint8_t *switch_mask) {

@@ -311,6 +311,7 @@ __device__ ArgKey block_argmin(ArgKey mine) {
 __global__ __launch_bounds__(1024) void k_generic_argmin0(ProblemDev P, LevelsDev Lv, const double *front0,
                                                           size_t front_stride, int Bu, Start *start) {
   const int k = blockIdx.x;
+  if (P.Bvec) Bu = P.Bvec[k];
   const double *f = front0 + (size_t)k * front_stride;
   ArgKey best;
   best.v = ~0ull;
@@ -510,6 +511,7 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
 __global__ __launch_bounds__(1024) void k_stage_argmin0(ProblemDev P, LevelsDev Lv, const uint32_t *perm_all,
                                                         const double *S0_all, size_t s_stride, int Bu, Start *start) {
   const int k = blockIdx.x, L = Lv.L;
+  if (P.Bvec) Bu = P.Bvec[k];
   const double *S0 = S0_all + (size_t)k * s_stride;
   const uint32_t *perm = perm_all + (size_t)k * P.nt * L;  // sphere order of u_old(0): rank | b̃ << 16
   ArgKey best;

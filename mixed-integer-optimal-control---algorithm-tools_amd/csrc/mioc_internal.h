@@ -43,6 +43,7 @@ struct ProblemDev {
   double dt = 0.0;
   const double *df = nullptr;      // [K][nt][M]  (each subproblem nx x nt column-major)
   const double *uold = nullptr;    // [K][nt][M]
+  const int32_t *Bvec = nullptr;   // backtrack: per-subproblem budget B'_k (null: one B' for the batch)
 };
 
 // Product grid with consecutive integer levels per dimension (the L1-ball pyramid's domain).
@@ -199,6 +200,7 @@ struct mioc_ctx {
   bool pred_fma = false;           // MIOC_OPT_PRED_FMA
   double *d_pred_own = nullptr;    // mioc_pred staging: 4 doubles, then the TV error flag (int32)
   bool trm_pending = false;
+  const int32_t *Bvec = nullptr;   // per-subproblem B' of the running backtrack (mioc_backtrack_batch_budgets_device)
   double *d_ode_state = nullptr;   // [K][nt][2] forward states of mioc_ode_eval_device
   size_t ode_cap = 0;        // a device pred / TV launch whose error flag mioc_synchronize reads
   int64_t costlut_len = 0;

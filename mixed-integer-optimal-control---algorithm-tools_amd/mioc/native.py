@@ -37,7 +37,7 @@ EXPORTED = [
     "mioc_backtrack_batch_device", "mioc_synchronize", "mioc_stream", "mioc_kernel_stats",
     "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics", "mioc_get_argmin_table", "mioc_get_ranks_device",
     "mioc_pred", "mioc_pred_batch_device", "mioc_tv_device", "mioc_trm_decide_device", "mioc_batch_multi",
-    "mioc_ode_eval_device", "mioc_rand_start_device",
+    "mioc_ode_eval_device", "mioc_rand_start_device", "mioc_backtrack_batch_budgets_device",
 ]
 
 
@@ -100,6 +100,7 @@ def load_library(path=None):
         "mioc_batch_multi": (i32, [vp, i32, i64, vp, vp, i64, i64, i64, dbl, i64, vp, vp, vp]),
         "mioc_ode_eval_device": (i32, [vp, i32, i64, vp, i64, i64, dbl, dbl, vp, i32, vp, vp]),
         "mioc_rand_start_device": (i32, [vp, i64, i64, i64, ctypes.c_uint64, vp]),
+        "mioc_backtrack_batch_budgets_device": (i32, [vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -246,6 +247,22 @@ class Context:
                 raise ValueError(f"{name} must be a contiguous {dt_} tensor with K entries")
         self.backtrack_batch_device(B_use, u.data_ptr(), 0 if phi is None else phi.data_ptr(),
                                     0 if status is None else status.data_ptr())
+
+    def backtrack_batch_budgets_tensors(self, budgets, u, phi=None, status=None):
+        """eval_u_TRM! with one budget per subproblem: budgets (K,) int32 CUDA tensor (each <= B); u (K, nt, nx)
+        float64 CUDA tensor; phi, status optional (mioc_backtrack_batch_budgets_device)."""
+        if u.dim() != 3 or not u.is_contiguous() or not u.is_cuda or str(u.dtype) != "torch.float64":
+            raise ValueError("u must be a contiguous float64 CUDA tensor of shape (K, nt, nx)")
+        if not budgets.is_cuda or str(budgets.dtype) != "torch.int32" or not budgets.is_contiguous() or \
+                budgets.numel() != u.shape[0]:
+            raise ValueError("budgets must be a contiguous int32 CUDA tensor with K entries")
+        for name, t, dt_ in (("phi", phi, "torch.float64"), ("status", status, "torch.int32")):
+            if t is not None and (not t.is_contiguous() or str(t.dtype) != dt_ or t.numel() != u.shape[0]):
+                raise ValueError(f"{name} must be a contiguous {dt_} tensor with K entries")
+        self._check(self.lib.mioc_backtrack_batch_budgets_device(
+            self.h, ctypes.c_void_p(budgets.data_ptr()), ctypes.c_void_p(u.data_ptr()),
+            ctypes.c_void_p(phi.data_ptr()) if phi is not None else None,
+            ctypes.c_void_p(status.data_ptr()) if status is not None else None))
 
     def ranks_tensor(self, out):
         """Level ranks (iterator order) of the last backtrack into `out`, an int32 CUDA tensor (K, nt)."""

@@ -167,3 +167,59 @@ def test_rand_start_device(shape):
     with pytest.raises(native.MiocNativeError):
         ctx.rand_start_tensor(out, seed=1, jumps=nt)
     ctx.close()
+
+
+class _DeviceODE:
+    """Test double: an ODE example whose eval_f! / eval_df! run through mioc_ode_eval_device for one restart, so
+    the host TRM (multi-trust.jl mirror) and TRM_batch see bit-identical objective values and gradients."""
+
+    def __new__(cls, name, nt, ctx):
+        import torch
+        obj = _obj(name, nt)
+        prob = dict((c[0], c[1]) for c in CASES)[name]
+
+        def f_helper(x, cache):
+            X = torch.tensor(np.ascontiguousarray(np.asarray(x).T[None]), dtype=torch.float64, device="cuda")
+            J = torch.empty(1, dtype=torch.float64, device="cuda")
+            ctx.ode_eval_tensors(prob, X, obj.T0, obj.T1, J, None)
+            ctx.synchronize()
+            return J.item()
+
+        def df_helper():
+            X = torch.tensor(np.ascontiguousarray(obj.x.T[None]), dtype=torch.float64, device="cuda")
+            D = torch.empty_like(X)
+            ctx.ode_eval_tensors(prob, X, obj.T0, obj.T1, None, D)
+            ctx.synchronize()
+            obj.df[:, :] = D[0].cpu().numpy().T
+
+        obj.eval_f_helper = f_helper
+        obj.eval_df_helper = df_helper
+        return obj
+
+
+@pytest.mark.parametrize("name,p,nt", [("fishing", math.inf, 240), ("doubletank", math.inf, 240),
+                                       ("vanderpol", 1, 2000)])
+def test_trm_batch_equals_sequential_trm(name, p, nt):
+    """TRM_batch (every restart's data on the device, decisions per inner iteration) against the host TRM loop
+    (multi-trust.jl:53-170 mirror) run restart by restart with the same device kernels: identical returned values
+    J + β·TV_p(u) and identical controls obj.x, including restarts that halve Δ and that stop on pred <= 0."""
+    import torch
+    from mioc.trm_batch import TRM_batch
+    K = 12  # vanderpol: explicit Euler needs the example's own nt = 2000 over T = 20 to stay finite
+    par = mioc.TRM_parameters(beta=1e-3, Delta0=1.0, p=p, maxiter=6, kmax=5)
+    ctx = native.Context(0)
+    ctx.set_levels(LevelTable([[0, 1]] * 3, mioc.bounded_sum_iterator([[0, 1]] * 3, 1, 1)))
+    x0 = torch.empty(K, nt, 3, dtype=torch.float64, device="cuda")
+    ctx.rand_start_tensor(x0, seed=99)
+    ctx.synchronize()
+    log = []
+    vals, u, iters = TRM_batch(name, par, x0=x0, log=log)
+    ub = u.cpu().numpy()
+    halvings = sum(int(np.sum(d == 1)) for *_, d, _inner in log)
+    for k in range(K):
+        obj = _DeviceODE(name, nt, ctx)
+        J = mioc.TRM(obj, par, x0=x0[k].cpu().numpy().T.copy())
+        assert J == vals[k], (k, J, vals[k])
+        assert np.array_equal(obj.x, ub[k].T), k
+    print(f"{name}: iterations per restart {iters.tolist()}, halvings {halvings}")
+    ctx.close()
