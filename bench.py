@@ -40,6 +40,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md
 FP64_VALU_PEAK_TOPS = 39.3     # 256 CU x 64 FP64 lanes/clk x 2.4 GHz (78.6 TFLOP/s counts an FMA as 2)
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix, AMD spec (dense; the guide tabulates no FP64 MFMA row)
 METRIC = "bellman_TRM! subproblems/sec (nt=65536, 4096 levels, budget=256) + HBM GB/s"
 
 
@@ -57,6 +58,10 @@ def parse(argv=None):
     ap.add_argument("--batch-size", type=int, default=1024, help="batch line: subproblems per rank per step")
     ap.add_argument("--pinf-batch-config", default="C2",
                     help="the p=Inf batch line's config (the reference's main() runs C1-C3 at p=Inf; 'none' to skip)")
+    ap.add_argument("--heat-restarts", type=int, default=4096,
+                    help="PDE heat gradient line (SURVEY §8 f4): restarts per rank per step (0 to skip)")
+    ap.add_argument("--heat-n", type=int, default=17, help="heat line: P1 grid side (N = n^2 dofs)")
+    ap.add_argument("--heat-nt", type=int, default=500, help="heat line: time steps (example_heat.jl nt)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=5, help="recursion steps timed for the C4 CPU baseline")
     ap.add_argument("--solver", default="native", choices=["native", "oracle"],
@@ -424,6 +429,107 @@ def cpu_baseline(cfg_name, p_over, cpu_steps):
                       f"({per_step[threads]:.3f} s/step), extrapolated x{cfg.nt - 1}; {host}"}
 
 
+def heat_line(args, rank, world, device, dist, torch):
+    """The PDE heat objective's eval_f + eval_df (PDEObjective.jl:129-199) for K restarts per rank per step on the
+    device (mioc_heat_eval_device, one k_heat_run launch), timed like the DP lines; HIP events on the library's
+    stream give the kernel's own time for the MFMA roofline."""
+    from mioc import native
+    from mioc.heat import HeatProblem
+    K, nt = args.heat_restarts, args.heat_nt
+    steps = max(args.steps, 3)
+    hp = HeatProblem(n=args.heat_n, nt=nt)
+    ctx = native.Context(device)
+    hp.setup(ctx)
+    g = torch.Generator().manual_seed(1234 + rank)
+    xs = [torch.randint(0, 6, (K, nt, 2), generator=g).double().to(f"cuda:{device}") for _ in range(2)]
+    J = torch.empty(K, dtype=torch.float64, device=f"cuda:{device}")
+    df = torch.empty_like(xs[0])
+    st = torch.cuda.ExternalStream(ctx.stream(), device=f"cuda:{device}")
+    for w in range(max(1, args.warmup)):
+        ctx.heat_eval_tensors(xs[w % 2], J, df)
+    ctx.synchronize()
+    if world > 1:
+        dist.barrier()
+    ctx.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record(st)
+    for s in range(steps):
+        ctx.heat_eval_tensors(xs[s % 2], J, df)
+    ev[1].record(st)
+    ctx.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    kern_s = ev[0].elapsed_time(ev[1]) / 1e3 / steps
+    N, Np = hp.N, (hp.N + 15) // 16 * 16
+    flops = 3 * 2.0 * N * N * nt * K       # S^-1 z, M v (forward), S^-T r (adjoint): one N x N matvec each per step
+    hbm = K * nt * (2 * Np * 8 + 2 * 2 * 8)  # Gy scratch written + read, x in + df out
+    ach = flops / kern_s / 1e12
+    traffic, tsrc = pmc_traffic("k_heat_run", "HEAT")
+    line = {"config": {"workload": f"HEAT: example_heat.jl objective, N={N} dofs (P1 {args.heat_n}x{args.heat_n} "
+                                   f"stand-in mesh), nx=2, nt={nt}, {K} restart(s) per GPU per step: eval_f + eval_df",
+                       "parallelism": f"dp{world} (independent restarts)"},
+            "value": round(world * K * steps / elapsed, 3), "unit": "gradient evaluations/s", "n_gpus": world,
+            "scaling": "weak", "steps": steps, "ms_per_step": round(1e3 * elapsed / steps, 3),
+            "algorithm": {"implicit-Euler state + adjoint on FP64 MFMA, LDS-resident columns": "k_heat_run"},
+            "checksum": float(J.sum().item()) + float(df.sum().item()),
+            "roofline": {"bound": "mfma", "achieved": round(ach, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 6),
+                         "traffic": None if traffic is None else round(traffic), "traffic_source": tsrc,
+                         "kernel": "k_heat_run", "avg_launch_us": round(kern_s * 1e6, 3),
+                         "flops_per_launch": flops, "hbm_bytes_per_launch": hbm,
+                         "hbm_frac": round(hbm / kern_s / 1e9 / HBM_PEAK_GBS, 6)}}
+    ctx.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = heat_cpu_baseline(hp)
+    return line
+
+
+def heat_cpu_baseline(hp):
+    """The reference's heat gradient (LU restatement, oracle/heat_oracle.py) on the host: restarts over a pool of
+    single-threaded worker processes (spawned, BLAS at 1 thread each) for about 3 s."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+
+    from oracle.heat_oracle import HeatOracle, eval_batch
+    model, aff, threads = _cpu_info()
+    mats = (hp.M_invA, hp.M_invF, hp.M, hp.state0, hp.yd)
+    o = HeatOracle(*mats, hp.T0, hp.T1, hp.gamma)
+    rng = np.random.default_rng(7)
+    x0 = rng.integers(0, 6, size=(2, hp.nt)).astype(np.float64)
+    t0 = time.perf_counter()
+    o.eval(x0)
+    t1 = time.perf_counter() - t0
+    per = max(1, min(64, int(3.0 / max(t1, 1e-4))))  # restarts per worker: about 3 s each
+    saved = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    for k in saved:
+        os.environ[k] = "1"
+    try:
+        with ProcessPoolExecutor(threads, mp_context=mp.get_context("spawn")) as ex:
+            list(ex.map(eval_batch, [(mats, hp.T0, hp.T1, hp.gamma, [x0])] * threads))  # start-up, untimed
+            jobs = [(mats, hp.T0, hp.T1, hp.gamma, [x0] * per)] * threads
+            t0 = time.perf_counter()
+            list(ex.map(eval_batch, jobs))
+            tn = time.perf_counter() - t0
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return {"value": round(threads * per / tn, 3), "unit": "gradient evaluations/s", "cores": threads,
+            "kind": "port", "value_1thread": round(1.0 / t1, 3),
+            "sample": f"{threads * per} eval_f + eval_df of the heat objective (N={hp.N}, nt={hp.nt}; numpy/scipy "
+                      f"LU restatement, one LAPACK triangular-solve pair per step) over {threads} single-threaded "
+                      f"worker processes: {tn:.2f} s (matrix set-up per worker included); one alone {t1:.3f} s; "
+                      f"host: {model}, {aff} CPUs in the affinity mask"}
+
+
 def workload(res):
     lv = res["levels"]
     counts = "x".join(str(len(v)) for v in lv.nu)
@@ -488,7 +594,9 @@ def main():
             line["cpu_baseline"] = cpu_baseline(cfg_name, None, args.cpu_steps)
         return line
 
-    batch_pinf = None
+    batch_pinf = heat = None
+    if args.heat_restarts > 0 and args.nt is None and args.solver == "native" and args.backend == "nccl":
+        heat = heat_line(args, rank, world, device, dist, torch)
     if args.batch_config not in ("", "none") and args.nt is None:
         batch = batch_line(args.batch_config)
     if args.pinf_batch_config not in ("", "none") and args.nt is None:
@@ -525,6 +633,8 @@ def main():
             out["batch"] = batch
         if batch_pinf:
             out["batch_p_inf"] = batch_pinf
+        if heat:
+            out["batch_heat"] = heat
         if not args.no_cpu_baseline and world == 1 and args.nt is None and args.solver == "native":
             out["cpu_baseline"] = cpu_baseline(args.config, args.p, args.cpu_steps)
         print(json.dumps(out), flush=True)

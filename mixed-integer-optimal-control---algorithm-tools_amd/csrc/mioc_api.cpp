@@ -102,6 +102,8 @@ void free_all(mioc_ctx *ctx) {
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (ctx->h_flags) hipHostFree(ctx->h_flags);
+  heat_free(ctx->heat);
+  ctx->heat = nullptr;
   ev_collect(ctx);
   for (auto &pr : ctx->ev_pool) hipEventDestroy(pr.begin), hipEventDestroy(pr.end);
   if (ctx->stream) hipStreamDestroy(ctx->stream);

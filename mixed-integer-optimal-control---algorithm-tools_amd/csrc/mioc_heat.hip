@@ -1,0 +1,405 @@
+// mioc_heat.hip -- the PDE heat objective's value and gradient, batched over restarts on gfx950.
+//
+// Reference: julia_opt/PDEObjective.jl:129-139 (impleuler_state!: y_i = SMatLU \ (y_{i-1} + τ·M⁻¹F·x_{i-1})),
+// :142-156 (eval_f_helper: trapezoid over G + G_t, x extended by its last column), :159-172 (impleuler_adjoint!:
+// p_i = AMatLU \ (p_{i+1} + τ·Gy_i), AMatLU = lu(StateMat')), :174-199 (eval_df_helper: df_i = (M⁻¹F)ᵀ p_i, plus
+// Gu = γ for i ≥ 2 only), with the hooks of julia_opt/example_heat.jl:135-161 (G = ½ vᵀMv, v = y_i − yd_i;
+// G_t = γ·Σx; Gy = M·v; Gu = γ).  StateMat = I + τ·M⁻¹A (example_heat.jl:113-115).
+//
+// The matrices are the caller's: the Julia objective assembles A, M, F, state0 and yd with its FEM bundle
+// (FEMBundle, julia_fem/) and hands them over once (mioc_heat_setup); only the time loops run here.
+//
+// Design.  The system is linear and time-invariant, so both triangular solves per step become one product with a
+// precomputed inverse (S⁻¹ for the state, S⁻ᵀ for the adjoint), and the K restarts side by side turn every step
+// into a dense (N × N) · (N × 16) product on the FP64 matrix cores: one workgroup per 16 restarts (one MFMA column
+// tile), all nt forward and nt adjoint steps in one launch, the 16 state columns resident in LDS.  Per forward step
+// two products (S⁻¹·Z, then M·(y − yd) for G and Gy), per adjoint step one (S⁻ᵀ·R); Gy_i goes to an HBM scratch
+// between the sweeps (written once, read once) instead of a third product.  The operand matrices stream from L2
+// (each ≤ 1.3 MB, shared by every workgroup of an XCD) in the MFMA A-operand order, one 16-byte load per lane per
+// two MFMAs.  Results agree with the reference's LU solves to rounding (the inverse and the MFMA sum order are not
+// the reference's operation order): the tests hold them to 1e-9 relative.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mioc_internal.h"
+
+namespace mioc {
+
+struct HeatState {
+  int64_t N = 0, Np = 0, nx = 0, nt = 0;
+  double tau = 0.0, gamma = 0.0;
+  double *d_sinv = nullptr, *d_sinvT = nullptr, *d_mass = nullptr;  // A-operand order, [Np/16][Np/8][64] double2
+  double *d_minvF = nullptr;                                        // [Np][nx] row-major, zero-padded
+  double *d_state0 = nullptr;                                       // [Np]
+  double *d_yd = nullptr;                                           // [nt + 1][Np]
+  double *d_gy = nullptr;                                           // [tiles][nt][Np][16] Gy_i between the sweeps
+  size_t gy_cap = 0;
+};
+
+void heat_free(HeatState *h) {
+  if (!h) return;
+  for (double *p : {h->d_sinv, h->d_sinvT, h->d_mass, h->d_minvF, h->d_state0, h->d_yd, h->d_gy})
+    if (p) hipFree(p);
+  delete h;
+}
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+constexpr int HW = 4;           // waves per workgroup
+constexpr int HMAXNX = 4;       // controls per step
+constexpr int HMAXN = 400;      // 3 LDS column blocks of Np x 16 doubles fit 160 KB up to Np = 400
+
+struct HeatArgs {
+  const d2 *sinv, *sinvT, *mass;
+  const double *minvF, *state0, *yd;
+  const double *X;
+  double *J, *DF, *GY;
+  int K, nx, nt, Np;
+  double tau, gamma;
+};
+
+// acc[s] += A(tile w + HW·s) · Bs for this wave's row tiles; Bs is [Np][16] in LDS.  A-operand lanes hold
+// A[16t + (l & 15)][k + (l >> 4)] (MI355X_MICROARCH.md, v_mfma_f64_16x16x4_f64), two k-blocks per 16-byte load;
+// the loads of block kb + 1 are in flight while block kb's MFMAs issue.
+template <int TPW>
+__device__ __forceinline__ void heat_gemm(const d2 *__restrict__ A, const double *Bs, int Np, int w, int lane,
+                                          d4 (&acc)[TPW]) {
+  const int ntile = Np >> 4, KB = Np >> 3, bo = ((lane >> 4) << 4) + (lane & 15);
+#pragma unroll
+  for (int s = 0; s < TPW; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
+  const d2 *ap[TPW];
+#pragma unroll
+  for (int s = 0; s < TPW; ++s) ap[s] = A + (size_t)min(w + HW * s, ntile - 1) * KB * 64 + lane;
+  d2 an[TPW];
+#pragma unroll
+  for (int s = 0; s < TPW; ++s) an[s] = ap[s][0];
+  for (int kb = 0; kb < KB; ++kb) {
+    d2 a[TPW];
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) a[s] = an[s];
+    const int kn = min(kb + 1, KB - 1);
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) an[s] = ap[s][(size_t)kn * 64];
+    const double b0 = Bs[kb * 128 + bo], b1 = Bs[kb * 128 + 64 + bo];
+#pragma unroll
+    for (int s = 0; s < TPW; ++s)
+      if (w + HW * s < ntile) {
+        acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].x, b0, acc[s], 0, 0, 0);
+        acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].y, b1, acc[s], 0, 0, 0);
+      }
+  }
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int TPW>
+__global__ __launch_bounds__(256) void k_heat_run(HeatArgs H) {
+  extern __shared__ __attribute__((aligned(16))) double hsm[];
+  const int Np = H.Np, nx = H.nx, nt = H.nt, E = Np * 16;
+  double *Ys = hsm, *Zs = hsm + E, *Vs = hsm + 2 * E, *red = hsm + 3 * E;  // red: [HW][16], then [HW][HMAXNX][16]
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, c = lane & 15, tile = blockIdx.x;
+  const int ntile = Np >> 4;
+  const double tau = H.tau;
+  const size_t xs = (size_t)nt * nx;  // doubles per restart in X / DF
+  // this thread's restart column in phase A (every e it visits has e & 15 == tid & 15)
+  const int kcol = tile * 16 + (tid & 15);
+  const double *xk = kcol < H.K ? H.X + (size_t)kcol * xs : nullptr;
+  double *gyt = H.DF ? H.GY + (size_t)tile * nt * E : nullptr;
+
+  // state column 0 = state0 (PDEObjective.jl:130); V = y_0 − yd_0
+  for (int e = tid; e < E; e += 256) {
+    const double y = H.state0[e >> 4];
+    Ys[e] = y;
+    Vs[e] = y - H.yd[e >> 4];
+  }
+  __syncthreads();
+  double gacc = 0.0;  // Σ_j w_j · v_jᵀ M v_j for column c (trapezoid weights of PDEObjective.jl:148-153)
+  d4 acc[TPW];
+  for (int j = 0;; ++j) {
+    // Gy_j = M·v_j; G-partial v·Gy; Gy_j to HBM for the adjoint (j < nt, when df is wanted)
+    heat_gemm<TPW>(H.mass, Vs, Np, w, lane, acc);
+    const double wj = (j == 0 || j == nt) ? 0.5 : 1.0;
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      const int t = w + HW * s;
+      if (t < ntile) {
+        double part = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 16 * t + (lane >> 4) + 4 * q;
+          part += Vs[r * 16 + c] * acc[s][q];
+          if (H.DF && j < nt) gyt[(size_t)j * E + r * 16 + c] = acc[s][q];
+        }
+        gacc += wj * part;
+      }
+    }
+    if (j == nt) break;
+    // Z = y_j + τ·(M⁻¹F · x_j)  (PDEObjective.jl:136)
+    {
+      double xq[HMAXNX];
+#pragma unroll
+      for (int q = 0; q < HMAXNX; ++q) xq[q] = (xk && q < nx) ? xk[(size_t)j * nx + q] : 0.0;
+      for (int e = tid; e < E; e += 256) {
+        const double *f = H.minvF + (size_t)(e >> 4) * nx;
+        double sf = 0.0;
+#pragma unroll
+        for (int q = 0; q < HMAXNX; ++q)
+          if (q < nx) sf += f[q] * xq[q];
+        Zs[e] = Ys[e] + tau * sf;
+      }
+    }
+    lds_barrier();
+    // y_{j+1} = S⁻¹·Z; v_{j+1} = y_{j+1} − yd_{j+1}
+    heat_gemm<TPW>(H.sinv, Zs, Np, w, lane, acc);
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      const int t = w + HW * s;
+      if (t < ntile) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 16 * t + (lane >> 4) + 4 * q;
+          Ys[r * 16 + c] = acc[s][q];
+          Vs[r * 16 + c] = acc[s][q] - H.yd[(size_t)(j + 1) * Np + r];
+        }
+      }
+    }
+    lds_barrier();
+  }
+  // J = τ·(½·Σ w_j v_jᵀMv_j + Σ w_j γ·Σx_j), x extended by its last column (PDEObjective.jl:145-153)
+  gacc += __shfl_xor(gacc, 16);
+  gacc += __shfl_xor(gacc, 32);
+  if (lane < 16) red[w * 16 + lane] = gacc;
+  __syncthreads();
+  if (tid < 16 && H.J && kcol < H.K) {
+    const double g = ((red[tid] + red[16 + tid]) + red[32 + tid]) + red[48 + tid];
+    double gt = 0.0;
+    for (int i = 0; i <= nt; ++i) {
+      const int ic = i < nt ? i : nt - 1;
+      double sx = 0.0;
+      for (int q = 0; q < nx; ++q) sx += xk[(size_t)ic * nx + q];
+      gt += (i == 0 || i == nt ? 0.5 : 1.0) * (H.gamma * sx);
+    }
+    H.J[kcol] = tau * (0.5 * g + gt);
+  }
+  if (!H.DF) return;
+  // adjoint: p_nt = 0; p_i = S⁻ᵀ·(p_{i+1} + τ·Gy_i); df_i = (M⁻¹F)ᵀ p_i (+ γ for i ≥ 1)  (PDEObjective.jl:159-199)
+  for (int e = tid; e < E; e += 256) Ys[e] = 0.0;
+  __syncthreads();
+  double *redf = red + HW * 16;  // [HW][HMAXNX][16]
+  for (int i = nt - 1; i >= 0; --i) {
+    {
+      const double *g = gyt + (size_t)i * E;
+      for (int e = tid; e < E; e += 256) Zs[e] = Ys[e] + tau * g[e];
+    }
+    lds_barrier();
+    heat_gemm<TPW>(H.sinvT, Zs, Np, w, lane, acc);
+    double dq[HMAXNX] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+      const int t = w + HW * s;
+      if (t < ntile) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 16 * t + (lane >> 4) + 4 * q;
+          const double p = acc[s][q];
+          Ys[r * 16 + c] = p;
+#pragma unroll
+          for (int m = 0; m < HMAXNX; ++m)
+            if (m < nx) dq[m] += H.minvF[(size_t)r * nx + m] * p;
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < HMAXNX; ++m) {
+      double v = dq[m];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16 && m < nx) redf[(w * HMAXNX + m) * 16 + lane] = v;
+    }
+    lds_barrier();
+    if (tid < nx * 16) {
+      const int m = tid >> 4, cc = tid & 15, k = tile * 16 + cc;
+      if (k < H.K) {
+        const double v = ((redf[(0 * HMAXNX + m) * 16 + cc] + redf[(1 * HMAXNX + m) * 16 + cc]) +
+                          redf[(2 * HMAXNX + m) * 16 + cc]) + redf[(3 * HMAXNX + m) * 16 + cc];
+        H.DF[(size_t)k * xs + (size_t)i * nx + m] = (0.0 + v) + (i >= 1 ? H.gamma : 0.0);
+      }
+    }
+  }
+}
+
+template <int TPW>
+hipError_t launch_tpw(hipStream_t s, const HeatArgs &H, int tiles) {
+  const size_t lds = ((size_t)3 * H.Np * 16 + HW * 16 + HW * HMAXNX * 16) * sizeof(double);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_heat_run<TPW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_heat_run<TPW>, dim3(tiles), dim3(HW * 64), lds, s, H);
+  return hipGetLastError();
+}
+
+// A (N x N, element a(r, c)) into the MFMA A-operand order: [Np/16][Np/8][64] double2, lane l of block (t, kb)
+// holding {a(16t + (l&15), 8kb + (l>>4)), a(16t + (l&15), 8kb + 4 + (l>>4))}, zero outside N.
+template <class F>
+std::vector<double> swizzle(int64_t N, int64_t Np, F a) {
+  std::vector<double> out((size_t)Np * Np, 0.0);
+  const int64_t KB = Np / 8;
+  for (int64_t t = 0; t < Np / 16; ++t)
+    for (int64_t kb = 0; kb < KB; ++kb)
+      for (int l = 0; l < 64; ++l) {
+        const int64_t r = 16 * t + (l & 15), k0 = 8 * kb + (l >> 4), k1 = k0 + 4;
+        double *o = &out[(((size_t)t * KB + kb) * 64 + l) * 2];
+        o[0] = (r < N && k0 < N) ? a(r, k0) : 0.0;
+        o[1] = (r < N && k1 < N) ? a(r, k1) : 0.0;
+      }
+  return out;
+}
+
+// inverse of the dense N x N matrix S (column-major) by Gauss-Jordan with partial pivoting; false if singular
+bool invert(int64_t N, std::vector<double> S, std::vector<double> &inv) {
+  inv.assign((size_t)N * N, 0.0);
+  for (int64_t i = 0; i < N; ++i) inv[(size_t)i * N + i] = 1.0;
+  auto s = [&](int64_t r, int64_t c) -> double & { return S[(size_t)c * N + r]; };
+  auto v = [&](int64_t r, int64_t c) -> double & { return inv[(size_t)c * N + r]; };
+  for (int64_t col = 0; col < N; ++col) {
+    int64_t piv = col;
+    for (int64_t r = col + 1; r < N; ++r)
+      if (std::fabs(s(r, col)) > std::fabs(s(piv, col))) piv = r;
+    if (!(std::fabs(s(piv, col)) > 0.0)) return false;
+    if (piv != col)
+      for (int64_t c = 0; c < N; ++c) std::swap(s(piv, c), s(col, c)), std::swap(v(piv, c), v(col, c));
+    const double d = s(col, col);
+    for (int64_t c = 0; c < N; ++c) s(col, c) /= d, v(col, c) /= d;
+    for (int64_t r = 0; r < N; ++r) {
+      if (r == col) continue;
+      const double f = s(r, col);
+      if (f == 0.0) continue;
+      for (int64_t c = 0; c < N; ++c) s(r, c) -= f * s(col, c), v(r, c) -= f * v(col, c);
+    }
+  }
+  return true;
+}
+
+int heat_fail(mioc_ctx *ctx, int code, const std::string &msg) {
+  ctx->err = msg;
+  return code;
+}
+
+int upload(mioc_ctx *ctx, double **dst, const std::vector<double> &src, const char *what) {
+  if (*dst) hipFree(*dst), *dst = nullptr;
+  if (hipMalloc(reinterpret_cast<void **>(dst), src.size() * sizeof(double)) != hipSuccess) {
+    (void)hipGetLastError();
+    *dst = nullptr;
+    return heat_fail(ctx, MIOC_ENOMEM, std::string("cannot allocate the heat ") + what);
+  }
+  if (hipMemcpy(*dst, src.data(), src.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+    return heat_fail(ctx, MIOC_EHIP, std::string("heat upload failed: ") + what);
+  return MIOC_OK;
+}
+
+}  // namespace
+}  // namespace mioc
+
+using namespace mioc;
+
+extern "C" {
+
+int32_t mioc_heat_setup(mioc_ctx *ctx, int64_t N, int64_t nx, int64_t nt, double T0, double T1, double gamma,
+                        const double *M_invA, const double *M_invF, const double *mass, const double *state0,
+                        const double *yd) {
+  if (!ctx) return MIOC_EINVAL;
+  if (N < 1 || N > HMAXN) return heat_fail(ctx, MIOC_EINVAL, "heat: need 1 <= Nglobal_dofs <= 400 (LDS-resident state)");
+  if (nx < 1 || nx > HMAXNX) return heat_fail(ctx, MIOC_EINVAL, "heat: need 1 <= nx <= 4 controls");
+  if (nt < 1 || nt > (1 << 24)) return heat_fail(ctx, MIOC_EINVAL, "heat: bad nt");
+  if (!(T1 > T0)) return heat_fail(ctx, MIOC_EINVAL, "heat: need T1 > T0");
+  if (!M_invA || !M_invF || !mass || !state0 || !yd) return heat_fail(ctx, MIOC_EINVAL, "heat: null matrix");
+  if (!std::isfinite(gamma)) return heat_fail(ctx, MIOC_EINVAL, "heat: gamma must be finite");
+  const double tau = (T1 - T0) / (double)nt;  // example_heat.jl:90
+  // StateMat = spdiagm(ones(N)) + τ·M⁻¹A (example_heat.jl:113)
+  std::vector<double> S((size_t)N * N);
+  for (int64_t c = 0; c < N; ++c)
+    for (int64_t r = 0; r < N; ++r) {
+      const double a = M_invA[(size_t)c * N + r];
+      if (!std::isfinite(a)) return heat_fail(ctx, MIOC_EINVAL, "heat: M_invA has a non-finite entry");
+      S[(size_t)c * N + r] = (r == c ? 1.0 : 0.0) + tau * a;
+    }
+  std::vector<double> Si;
+  if (!invert(N, S, Si)) return heat_fail(ctx, MIOC_EINVAL, "heat: I + tau*M_invA is singular");
+  const int64_t Np = (N + 15) / 16 * 16;
+  HeatState *h = ctx->heat ? ctx->heat : new HeatState();
+  ctx->heat = h;
+  h->N = N, h->Np = Np, h->nx = nx, h->nt = nt, h->tau = tau, h->gamma = gamma;
+  if (hipSetDevice(ctx->device) != hipSuccess) return heat_fail(ctx, MIOC_EHIP, "hipSetDevice failed");
+  int rc;
+  if ((rc = upload(ctx, &h->d_sinv, swizzle(N, Np, [&](int64_t r, int64_t c) { return Si[(size_t)c * N + r]; }),
+                   "S^-1")))
+    return rc;
+  if ((rc = upload(ctx, &h->d_sinvT, swizzle(N, Np, [&](int64_t r, int64_t c) { return Si[(size_t)r * N + c]; }),
+                   "S^-T")))
+    return rc;
+  if ((rc = upload(ctx, &h->d_mass, swizzle(N, Np, [&](int64_t r, int64_t c) { return mass[(size_t)c * N + r]; }),
+                   "mass matrix")))
+    return rc;
+  std::vector<double> f((size_t)Np * nx, 0.0), y0(Np, 0.0), ydp((size_t)(nt + 1) * Np, 0.0);
+  for (int64_t r = 0; r < N; ++r) {
+    for (int64_t q = 0; q < nx; ++q) f[(size_t)r * nx + q] = M_invF[(size_t)q * N + r];
+    y0[r] = state0[r];
+  }
+  for (int64_t j = 0; j <= nt; ++j)
+    for (int64_t r = 0; r < N; ++r) ydp[(size_t)j * Np + r] = yd[(size_t)j * N + r];
+  if ((rc = upload(ctx, &h->d_minvF, f, "M_invF")) || (rc = upload(ctx, &h->d_state0, y0, "state0")) ||
+      (rc = upload(ctx, &h->d_yd, ydp, "yd")))
+    return rc;
+  return MIOC_OK;
+}
+
+int32_t mioc_heat_eval_device(mioc_ctx *ctx, int64_t K, const double *d_x, double *d_J, double *d_df) {
+  if (!ctx) return MIOC_EINVAL;
+  HeatState *h = ctx->heat;
+  if (!h || !h->d_sinv) return heat_fail(ctx, MIOC_ESTATE, "heat: mioc_heat_setup first");
+  if (K < 1 || K > INT32_MAX || !d_x) return heat_fail(ctx, MIOC_EINVAL, "heat: bad K / x");
+  if (hipSetDevice(ctx->device) != hipSuccess) return heat_fail(ctx, MIOC_EHIP, "hipSetDevice failed");
+  const int64_t tiles = (K + 15) / 16;
+  const size_t need = (size_t)tiles * h->nt * h->Np * 16 * sizeof(double);
+  if (d_df && h->gy_cap < need) {
+    if (h->d_gy) hipFree(h->d_gy), h->d_gy = nullptr, h->gy_cap = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&h->d_gy), need) != hipSuccess) {
+      (void)hipGetLastError();
+      h->d_gy = nullptr;
+      return heat_fail(ctx, MIOC_ENOMEM, "heat: cannot allocate the Gy scratch");
+    }
+    h->gy_cap = need;
+  }
+  HeatArgs A;
+  A.sinv = reinterpret_cast<const d2 *>(h->d_sinv);
+  A.sinvT = reinterpret_cast<const d2 *>(h->d_sinvT);
+  A.mass = reinterpret_cast<const d2 *>(h->d_mass);
+  A.minvF = h->d_minvF, A.state0 = h->d_state0, A.yd = h->d_yd;
+  A.X = d_x, A.J = d_J, A.DF = d_df;
+  A.GY = h->d_gy;
+  A.K = (int)K, A.nx = (int)h->nx, A.nt = (int)h->nt, A.Np = (int)h->Np;
+  A.tau = h->tau, A.gamma = h->gamma;
+  const int tpw = (int)((h->Np / 16 + HW - 1) / HW);
+  hipError_t e;
+  switch (tpw) {
+    case 1: e = launch_tpw<1>(ctx->stream, A, (int)tiles); break;
+    case 2: e = launch_tpw<2>(ctx->stream, A, (int)tiles); break;
+    case 3: e = launch_tpw<3>(ctx->stream, A, (int)tiles); break;
+    case 4: e = launch_tpw<4>(ctx->stream, A, (int)tiles); break;
+    case 5: e = launch_tpw<5>(ctx->stream, A, (int)tiles); break;
+    case 6: e = launch_tpw<6>(ctx->stream, A, (int)tiles); break;
+    default: e = launch_tpw<7>(ctx->stream, A, (int)tiles); break;
+  }
+  if (e != hipSuccess) return heat_fail(ctx, MIOC_EHIP, std::string("k_heat_run: ") + hipGetErrorString(e));
+  return MIOC_OK;
+}
+
+}  // extern "C"

@@ -163,6 +163,9 @@ hipError_t launch_rand_start(hipStream_t s, int K, int nt, int jumps, uint64_t s
 hipError_t launch_ode_eval(hipStream_t s, int problem, int K, int nt, double tau, const double *params, int y0off,
                            const double *X, double *J, double *DF, double *ST);
 
+struct HeatState;  // mioc_heat.hip: the PDE heat objective's device matrices (mioc_heat_setup)
+void heat_free(HeatState *h);
+
 }  // namespace mioc
 
 // ---- the context ----------------------------------------------------------------------------------
@@ -202,7 +205,8 @@ struct mioc_ctx {
   bool trm_pending = false;
   const int32_t *Bvec = nullptr;   // per-subproblem B' of the running backtrack (mioc_backtrack_batch_budgets_device)
   double *d_ode_state = nullptr;   // [K][nt][2] forward states of mioc_ode_eval_device
-  size_t ode_cap = 0;        // a device pred / TV launch whose error flag mioc_synchronize reads
+  size_t ode_cap = 0;
+  mioc::HeatState *heat = nullptr; // mioc_heat_setup / mioc_heat_eval_device
   int64_t costlut_len = 0;
 
   // owned problem inputs (device)

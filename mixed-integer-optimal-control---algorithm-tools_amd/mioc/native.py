@@ -38,6 +38,7 @@ EXPORTED = [
     "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics", "mioc_get_argmin_table", "mioc_get_ranks_device",
     "mioc_pred", "mioc_pred_batch_device", "mioc_tv_device", "mioc_trm_decide_device", "mioc_batch_multi",
     "mioc_ode_eval_device", "mioc_rand_start_device", "mioc_backtrack_batch_budgets_device",
+    "mioc_heat_setup", "mioc_heat_eval_device",
 ]
 
 
@@ -101,6 +102,8 @@ def load_library(path=None):
         "mioc_ode_eval_device": (i32, [vp, i32, i64, vp, i64, i64, dbl, dbl, vp, i32, vp, vp]),
         "mioc_rand_start_device": (i32, [vp, i64, i64, i64, ctypes.c_uint64, vp]),
         "mioc_backtrack_batch_budgets_device": (i32, [vp, vp, vp, vp, vp]),
+        "mioc_heat_setup": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, vp, vp, vp, vp, vp]),
+        "mioc_heat_eval_device": (i32, [vp, i64, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -324,6 +327,36 @@ class Context:
         self._check(self.lib.mioc_ode_eval_device(
             self.h, int(problem), K, ctypes.c_void_p(x.data_ptr()), nx, nt, float(T0), float(T1),
             None if par is None else _p(par), 0 if par is None else par.size,
+            ctypes.c_void_p(J.data_ptr()) if J is not None else None,
+            ctypes.c_void_p(df.data_ptr()) if df is not None else None))
+
+    def heat_setup(self, M_invA, M_invF, mass, state0, yd, T0, T1, gamma):
+        """Hand the heat objective's matrices to the device (mioc_heat_setup; example_heat.jl:101-115): M_invA, mass
+        (N, N), M_invF (N, nx), state0 (N,), yd (N, nt+1) as numpy arrays; nt = yd.shape[1] - 1."""
+        f = lambda a: np.asfortranarray(a, dtype=np.float64)  # noqa: E731  (column-major, Julia's layout)
+        A, F, Mm, y0, Yd = f(M_invA), f(M_invF), f(mass), f(state0), f(yd)
+        N, nx = F.shape
+        nt = Yd.shape[1] - 1
+        if A.shape != (N, N) or Mm.shape != (N, N) or y0.shape != (N,) or Yd.shape[0] != N:
+            raise ValueError("heat matrices: M_invA, mass (N, N); M_invF (N, nx); state0 (N,); yd (N, nt+1)")
+        self._check(self.lib.mioc_heat_setup(self.h, N, nx, nt, float(T0), float(T1), float(gamma),
+                                             _p(A), _p(F), _p(Mm), _p(y0), _p(Yd)))
+        self.heat_shape = (N, nx, nt)
+
+    def heat_eval_tensors(self, x, J=None, df=None):
+        """eval_f / eval_df of the heat objective for K controls x (K, nt, nx) float64 CUDA tensor into J (K,) and
+        df (K, nt, nx) float64 CUDA tensors (each optional); enqueued (mioc_heat_eval_device)."""
+        if x.dim() != 3 or not x.is_contiguous() or not x.is_cuda or str(x.dtype) != "torch.float64":
+            raise ValueError("x must be a contiguous float64 CUDA tensor of shape (K, nt, nx)")
+        K, nt, nx = x.shape
+        if getattr(self, "heat_shape", None) is None or self.heat_shape[1:] != (nx, nt):
+            raise ValueError("x does not match the (nx, nt) given to heat_setup")
+        for name, t, n in (("J", J, K), ("df", df, x.numel())):
+            if t is not None and (not t.is_cuda or not t.is_contiguous() or str(t.dtype) != "torch.float64" or
+                                  t.numel() != n):
+                raise ValueError(f"{name} must be a contiguous float64 CUDA tensor with {n} entries")
+        self._check(self.lib.mioc_heat_eval_device(
+            self.h, K, ctypes.c_void_p(x.data_ptr()),
             ctypes.c_void_p(J.data_ptr()) if J is not None else None,
             ctypes.c_void_p(df.data_ptr()) if df is not None else None))
 
