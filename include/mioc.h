@@ -217,6 +217,8 @@ int32_t mioc_heat_setup(mioc_ctx *ctx, int64_t N, int64_t nx, int64_t nt, double
                         const double *M_invA, const double *M_invF, const double *mass, const double *state0,
                         const double *yd);
 int32_t mioc_heat_eval_device(mioc_ctx *ctx, int64_t K, const double *d_x, double *d_J, double *d_df);
+/* The same from host arrays (the Julia objective's x / df, K x nx x nt column-major; J: K), synchronous. */
+int32_t mioc_heat_eval(mioc_ctx *ctx, int64_t K, const double *x, double *J, double *df);
 
 /* The HIP stream the context enqueues on (hipStream_t), for callers that order their own work. */
 void *mioc_stream(mioc_ctx *ctx);

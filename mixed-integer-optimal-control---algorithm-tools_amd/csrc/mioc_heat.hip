@@ -38,11 +38,13 @@ struct HeatState {
   double *d_yd = nullptr;                                           // [nt + 1][Np]
   double *d_gy = nullptr;                                           // [tiles][nt][Np][16] Gy_i between the sweeps
   size_t gy_cap = 0;
+  double *d_io = nullptr;                                           // host entry staging: x, df, J
+  size_t io_cap = 0;
 };
 
 void heat_free(HeatState *h) {
   if (!h) return;
-  for (double *p : {h->d_sinv, h->d_sinvT, h->d_mass, h->d_minvF, h->d_state0, h->d_yd, h->d_gy})
+  for (double *p : {h->d_sinv, h->d_sinvT, h->d_mass, h->d_minvF, h->d_state0, h->d_yd, h->d_gy, h->d_io})
     if (p) hipFree(p);
   delete h;
 }
@@ -52,9 +54,18 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-constexpr int HW = 4;           // waves per workgroup
+#ifndef HEAT_HW
+#define HEAT_HW 16  // measured at N = 289, K = 4096: 4 waves 39.4 ms, 8 waves 33.8 ms, 16 waves 28.9 ms per launch
+#endif
+#ifndef HEAT_PF
+#define HEAT_PF 1
+#endif
+
+constexpr int HW = HEAT_HW;     // waves per workgroup
+constexpr int PF = HEAT_PF;     // k-blocks of A loads in flight ahead of the MFMAs (1 or 2; 2 measured 3-5 % slower)
 constexpr int HMAXNX = 4;       // controls per step
 constexpr int HMAXN = 400;      // 3 LDS column blocks of Np x 16 doubles fit 160 KB up to Np = 400
+static_assert(HW * 64 <= 1024, "at most 16 waves per workgroup");
 
 struct HeatArgs {
   const d2 *sinv, *sinvT, *mass;
@@ -77,16 +88,26 @@ __device__ __forceinline__ void heat_gemm(const d2 *__restrict__ A, const double
   const d2 *ap[TPW];
 #pragma unroll
   for (int s = 0; s < TPW; ++s) ap[s] = A + (size_t)min(w + HW * s, ntile - 1) * KB * 64 + lane;
-  d2 an[TPW];
+  d2 an[TPW], an2[TPW];
 #pragma unroll
-  for (int s = 0; s < TPW; ++s) an[s] = ap[s][0];
+  for (int s = 0; s < TPW; ++s) {
+    an[s] = ap[s][0];
+    if (PF > 1) an2[s] = ap[s][(size_t)min(1, KB - 1) * 64];
+  }
   for (int kb = 0; kb < KB; ++kb) {
     d2 a[TPW];
 #pragma unroll
     for (int s = 0; s < TPW; ++s) a[s] = an[s];
-    const int kn = min(kb + 1, KB - 1);
+    const int kn = min(kb + PF, KB - 1);
 #pragma unroll
-    for (int s = 0; s < TPW; ++s) an[s] = ap[s][(size_t)kn * 64];
+    for (int s = 0; s < TPW; ++s) {
+      if (PF > 1) {
+        an[s] = an2[s];
+        an2[s] = ap[s][(size_t)kn * 64];
+      } else {
+        an[s] = ap[s][(size_t)kn * 64];
+      }
+    }
     const double b0 = Bs[kb * 128 + bo], b1 = Bs[kb * 128 + 64 + bo];
 #pragma unroll
     for (int s = 0; s < TPW; ++s)
@@ -102,7 +123,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 template <int TPW>
-__global__ __launch_bounds__(256) void k_heat_run(HeatArgs H) {
+__global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
   extern __shared__ __attribute__((aligned(16))) double hsm[];
   const int Np = H.Np, nx = H.nx, nt = H.nt, E = Np * 16;
   double *Ys = hsm, *Zs = hsm + E, *Vs = hsm + 2 * E, *red = hsm + 3 * E;  // red: [HW][16], then [HW][HMAXNX][16]
@@ -110,13 +131,13 @@ __global__ __launch_bounds__(256) void k_heat_run(HeatArgs H) {
   const int ntile = Np >> 4;
   const double tau = H.tau;
   const size_t xs = (size_t)nt * nx;  // doubles per restart in X / DF
-  // this thread's restart column in phase A (every e it visits has e & 15 == tid & 15)
+  // this thread's restart column in phase A (every e it visits has e & 15 == tid & 15: the stride is 16·HW)
   const int kcol = tile * 16 + (tid & 15);
   const double *xk = kcol < H.K ? H.X + (size_t)kcol * xs : nullptr;
   double *gyt = H.DF ? H.GY + (size_t)tile * nt * E : nullptr;
 
   // state column 0 = state0 (PDEObjective.jl:130); V = y_0 − yd_0
-  for (int e = tid; e < E; e += 256) {
+  for (int e = tid; e < E; e += HW * 64) {
     const double y = H.state0[e >> 4];
     Ys[e] = y;
     Vs[e] = y - H.yd[e >> 4];
@@ -148,7 +169,7 @@ __global__ __launch_bounds__(256) void k_heat_run(HeatArgs H) {
       double xq[HMAXNX];
 #pragma unroll
       for (int q = 0; q < HMAXNX; ++q) xq[q] = (xk && q < nx) ? xk[(size_t)j * nx + q] : 0.0;
-      for (int e = tid; e < E; e += 256) {
+      for (int e = tid; e < E; e += HW * 64) {
         const double *f = H.minvF + (size_t)(e >> 4) * nx;
         double sf = 0.0;
 #pragma unroll
@@ -180,7 +201,8 @@ __global__ __launch_bounds__(256) void k_heat_run(HeatArgs H) {
   if (lane < 16) red[w * 16 + lane] = gacc;
   __syncthreads();
   if (tid < 16 && H.J && kcol < H.K) {
-    const double g = ((red[tid] + red[16 + tid]) + red[32 + tid]) + red[48 + tid];
+    double g = 0.0;
+    for (int v = 0; v < HW; ++v) g += red[v * 16 + tid];
     double gt = 0.0;
     for (int i = 0; i <= nt; ++i) {
       const int ic = i < nt ? i : nt - 1;
@@ -192,13 +214,13 @@ __global__ __launch_bounds__(256) void k_heat_run(HeatArgs H) {
   }
   if (!H.DF) return;
   // adjoint: p_nt = 0; p_i = S⁻ᵀ·(p_{i+1} + τ·Gy_i); df_i = (M⁻¹F)ᵀ p_i (+ γ for i ≥ 1)  (PDEObjective.jl:159-199)
-  for (int e = tid; e < E; e += 256) Ys[e] = 0.0;
+  for (int e = tid; e < E; e += HW * 64) Ys[e] = 0.0;
   __syncthreads();
   double *redf = red + HW * 16;  // [HW][HMAXNX][16]
   for (int i = nt - 1; i >= 0; --i) {
     {
       const double *g = gyt + (size_t)i * E;
-      for (int e = tid; e < E; e += 256) Zs[e] = Ys[e] + tau * g[e];
+      for (int e = tid; e < E; e += HW * 64) Zs[e] = Ys[e] + tau * g[e];
     }
     lds_barrier();
     heat_gemm<TPW>(H.sinvT, Zs, Np, w, lane, acc);
@@ -229,8 +251,8 @@ __global__ __launch_bounds__(256) void k_heat_run(HeatArgs H) {
     if (tid < nx * 16) {
       const int m = tid >> 4, cc = tid & 15, k = tile * 16 + cc;
       if (k < H.K) {
-        const double v = ((redf[(0 * HMAXNX + m) * 16 + cc] + redf[(1 * HMAXNX + m) * 16 + cc]) +
-                          redf[(2 * HMAXNX + m) * 16 + cc]) + redf[(3 * HMAXNX + m) * 16 + cc];
+        double v = 0.0;
+        for (int u = 0; u < HW; ++u) v += redf[(u * HMAXNX + m) * 16 + cc];
         H.DF[(size_t)k * xs + (size_t)i * nx + m] = (0.0 + v) + (i >= 1 ? H.gamma : 0.0);
       }
     }
@@ -399,6 +421,35 @@ int32_t mioc_heat_eval_device(mioc_ctx *ctx, int64_t K, const double *d_x, doubl
     default: e = launch_tpw<7>(ctx->stream, A, (int)tiles); break;
   }
   if (e != hipSuccess) return heat_fail(ctx, MIOC_EHIP, std::string("k_heat_run: ") + hipGetErrorString(e));
+  return MIOC_OK;
+}
+
+int32_t mioc_heat_eval(mioc_ctx *ctx, int64_t K, const double *x, double *J, double *df) {
+  if (!ctx) return MIOC_EINVAL;
+  HeatState *h = ctx->heat;
+  if (!h || !h->d_sinv) return heat_fail(ctx, MIOC_ESTATE, "heat: mioc_heat_setup first");
+  if (K < 1 || K > INT32_MAX || !x || (!J && !df)) return heat_fail(ctx, MIOC_EINVAL, "heat: bad K / x / outputs");
+  if (hipSetDevice(ctx->device) != hipSuccess) return heat_fail(ctx, MIOC_EHIP, "hipSetDevice failed");
+  const size_t nxt = (size_t)K * h->nx * h->nt, need = (2 * nxt + K) * sizeof(double);
+  if (h->io_cap < need) {
+    if (h->d_io) hipFree(h->d_io), h->d_io = nullptr, h->io_cap = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&h->d_io), need) != hipSuccess) {
+      (void)hipGetLastError();
+      h->d_io = nullptr;
+      return heat_fail(ctx, MIOC_ENOMEM, "heat: cannot allocate the host-entry staging");
+    }
+    h->io_cap = need;
+  }
+  double *dx = h->d_io, *ddf = h->d_io + nxt, *dJ = h->d_io + 2 * nxt;
+  if (hipMemcpyAsync(dx, x, nxt * sizeof(double), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+    return heat_fail(ctx, MIOC_EHIP, "heat: x copy-in failed");
+  int rc = mioc_heat_eval_device(ctx, K, dx, J ? dJ : nullptr, df ? ddf : nullptr);
+  if (rc) return rc;
+  if (J && hipMemcpyAsync(J, dJ, K * sizeof(double), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    return heat_fail(ctx, MIOC_EHIP, "heat: J copy-out failed");
+  if (df && hipMemcpyAsync(df, ddf, nxt * sizeof(double), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    return heat_fail(ctx, MIOC_EHIP, "heat: df copy-out failed");
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return heat_fail(ctx, MIOC_EHIP, "hipStreamSynchronize failed");
   return MIOC_OK;
 }
 

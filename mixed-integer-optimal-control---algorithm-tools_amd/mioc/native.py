@@ -38,7 +38,7 @@ EXPORTED = [
     "mioc_reset_stats", "mioc_last_algo", "mioc_diagnostics", "mioc_get_argmin_table", "mioc_get_ranks_device",
     "mioc_pred", "mioc_pred_batch_device", "mioc_tv_device", "mioc_trm_decide_device", "mioc_batch_multi",
     "mioc_ode_eval_device", "mioc_rand_start_device", "mioc_backtrack_batch_budgets_device",
-    "mioc_heat_setup", "mioc_heat_eval_device",
+    "mioc_heat_setup", "mioc_heat_eval_device", "mioc_heat_eval",
 ]
 
 
@@ -104,6 +104,7 @@ def load_library(path=None):
         "mioc_backtrack_batch_budgets_device": (i32, [vp, vp, vp, vp, vp]),
         "mioc_heat_setup": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, vp, vp, vp, vp, vp]),
         "mioc_heat_eval_device": (i32, [vp, i64, vp, vp, vp]),
+        "mioc_heat_eval": (i32, [vp, i64, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -359,6 +360,18 @@ class Context:
             self.h, K, ctypes.c_void_p(x.data_ptr()),
             ctypes.c_void_p(J.data_ptr()) if J is not None else None,
             ctypes.c_void_p(df.data_ptr()) if df is not None else None))
+
+    def heat_eval(self, xs):
+        """Host entry (mioc_heat_eval): xs (K, nx, nt) numpy controls (Julia's per-restart layout) -> J (K,),
+        df (K, nx, nt)."""
+        x = np.ascontiguousarray(np.asarray(xs, dtype=np.float64).transpose(0, 2, 1))  # K x (nx x nt col-major)
+        K, nt, nx = x.shape
+        if getattr(self, "heat_shape", None) is None or self.heat_shape[1:] != (nx, nt):
+            raise ValueError("xs does not match the (nx, nt) given to heat_setup")
+        J = np.empty(K)
+        df = np.empty_like(x)
+        self._check(self.lib.mioc_heat_eval(self.h, K, _p(x), _p(J), _p(df)))
+        return J, df.transpose(0, 2, 1)
 
     def rand_start_tensor(self, out, seed, jumps=-1):
         """rand_func_int (HelpFunctions.jl:204-225) for K restarts into out, a (K, nt, M) float64 CUDA tensor;

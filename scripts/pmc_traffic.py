@@ -13,7 +13,7 @@ from collections import defaultdict
 
 
 def short(name):
-    n = name.split("(")[0].replace("void ", "").strip()
+    n = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
     return n.split("::")[-1].split("<")[0]
 
 

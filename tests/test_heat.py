@@ -137,6 +137,20 @@ def test_heat_batch_restart_independence():
 
 
 @pytest.mark.gpu
+def test_heat_host_entry_equals_device_entry():
+    """mioc_heat_eval (host arrays, what the Julia binding calls) gives the device entry's results bit for bit."""
+    from mioc import native
+    hp = HeatProblem(n=9, nt=60)
+    xs = _controls(hp, 21, seed=8)
+    J, df = _device_eval(hp, xs)
+    ctx = native.Context(0)
+    hp.setup(ctx)
+    Jh, dfh = ctx.heat_eval(np.stack(xs))
+    ctx.close()
+    assert np.array_equal(Jh, J) and np.array_equal(dfh.transpose(0, 2, 1), df)
+
+
+@pytest.mark.gpu
 def test_heat_errors():
     from mioc import native
     ctx = native.Context(0)
