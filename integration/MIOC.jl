@@ -145,4 +145,39 @@ function pred(ctx::Context)
     (iv[], to[], tn[], pr[])
 end
 
+"""
+    heat_setup!(ctx, obj)
+
+Hands the matrices a PDE objective (example_heat.jl's HeatObj, PDEObjective.jl) already holds to the device:
+M_invA, M_invF, M, state0, yd, T0, T1, γ (example_heat.jl:101-115).  StateMat = I + τ·M_invA is factored once
+there.  Call again whenever those matrices change.
+"""
+function heat_setup!(ctx::Context, obj)
+    M_invA = Matrix{Float64}(obj.M_invA)
+    M_invF = Matrix{Float64}(obj.M_invF)
+    M = Matrix{Float64}(obj.M)
+    N, nx = size(M_invF)
+    nt = size(obj.yd, 2) - 1
+    check(ctx, ccall((:mioc_heat_setup, libmioc), Int32,
+                     (Ptr{Cvoid}, Int64, Int64, Int64, Float64, Float64, Float64,
+                      Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                     ctx.ptr, N, nx, nt, obj.T0, obj.T1, obj.γ, M_invA, M_invF, M,
+                     Vector{Float64}(obj.state0), Matrix{Float64}(obj.yd)))
+    nothing
+end
+
+"""
+    heat_eval!(ctx, x, df) -> fval
+
+eval_f_helper + eval_df_helper of PDEObjective.jl:142-199 for the control x (nx × nt) in one device call: returns
+the objective value and writes the gradient into df (nx × nt), as the two Julia helpers would.
+"""
+function heat_eval!(ctx::Context, x::Matrix{Float64}, df::Matrix{Float64})
+    size(df) == size(x) || throw(DimensionMismatch("df and x differ in shape"))
+    J = Ref{Float64}(0.0)
+    check(ctx, ccall((:mioc_heat_eval, libmioc), Int32,
+                     (Ptr{Cvoid}, Int64, Ptr{Float64}, Ref{Float64}, Ptr{Float64}), ctx.ptr, 1, x, J, df))
+    J[]
+end
+
 end # module
