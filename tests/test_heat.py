@@ -105,8 +105,8 @@ def _check(hp, xs, J, df):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,nt,K", [(17, 500, 20), (5, 64, 33), (2, 7, 3), (20, 40, 16), (9, 1, 5), (12, 2, 17)],
-                         ids=["heat289_nt500", "N25_ragged", "N4", "N400_maxLDS", "nt1", "nt2"])
+@pytest.mark.parametrize("n,nt,K", [(17, 500, 20), (5, 64, 33), (2, 7, 3), (22, 40, 16), (9, 1, 5), (12, 2, 17)],
+                         ids=["heat289_nt500", "N25_ragged", "N4", "N484_maxLDS", "nt1", "nt2"])
 def test_heat_eval_device_vs_oracle(n, nt, K):
     hp = HeatProblem(n=n, nt=nt)
     xs = _controls(hp, K, seed=n * 1000 + nt)
@@ -155,7 +155,7 @@ def test_heat_errors():
     from mioc import native
     ctx = native.Context(0)
     with pytest.raises(native.MiocNativeError):
-        HeatProblem(n=21, nt=4).setup(ctx)  # N = 441 > 400
+        HeatProblem(n=23, nt=4).setup(ctx)  # N = 529 > 512
     import torch
     ctx.heat_shape = (4, 2, 4)
     with pytest.raises(native.MiocNativeError) as e:  # eval before a successful setup
