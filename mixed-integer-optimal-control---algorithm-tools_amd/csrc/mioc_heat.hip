@@ -32,7 +32,7 @@ namespace mioc {
 struct HeatState {
   int64_t N = 0, Np = 0, nx = 0, nt = 0;
   double tau = 0.0, gamma = 0.0;
-  double *d_sinv = nullptr, *d_sinvT = nullptr, *d_mass = nullptr;  // A-operand order, [Np/16][Np/8][64] double2
+  double *d_sinv = nullptr, *d_sinvT = nullptr;                    // A-operand order, [Np/16][Np/8][64] double2
   double *d_minvF = nullptr;                                        // [Np][nx] row-major, zero-padded
   double *d_state0 = nullptr;                                       // [Np]
   double *d_yd = nullptr;                                           // [nt + 1][Np]
@@ -40,11 +40,17 @@ struct HeatState {
   size_t gy_cap = 0;
   double *d_io = nullptr;                                           // host entry staging: x, df, J
   size_t io_cap = 0;
+  double *d_msinv = nullptr;                                        // M·S⁻¹ in the A-operand order
+  double *d_myd = nullptr;                                          // [nt + 1][Np] M·yd_j
+  double *d_gy0 = nullptr;                                          // [Np] M·(state0 − yd_0)
+  double g0 = 0.0;                                                  // (state0 − yd_0)ᵀ M (state0 − yd_0)
+  double *d_sc = nullptr;                                           // [tiles][2][Np][16] y, z for Np > 512
+  size_t sc_cap = 0;
 };
 
 void heat_free(HeatState *h) {
   if (!h) return;
-  for (double *p : {h->d_sinv, h->d_sinvT, h->d_mass, h->d_minvF, h->d_state0, h->d_yd, h->d_gy, h->d_io})
+  for (double *p : {h->d_sinv, h->d_sinvT, h->d_minvF, h->d_state0, h->d_yd, h->d_gy, h->d_io, h->d_msinv, h->d_myd, h->d_gy0, h->d_sc})
     if (p) hipFree(p);
   delete h;
 }
@@ -54,117 +60,102 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-#ifndef HEAT_HW
-#define HEAT_HW 16  // measured at N = 289, K = 4096: 4 waves 39.4 ms, 8 waves 33.8 ms, 16 waves 28.9 ms per launch
-#endif
-#ifndef HEAT_PF
-#define HEAT_PF 1
-#endif
-
-constexpr int HW = HEAT_HW;     // waves per workgroup
-constexpr int PF = HEAT_PF;     // k-blocks of A loads in flight ahead of the MFMAs (1 or 2; 2 measured 3-5 % slower)
+// Measured at N = 289, K = 4096 (scripts/probe_heat.py): 4 / 8 / 16 waves per workgroup 39.4 / 33.8 / 28.9 ms per
+// launch with separate forward products; one fused forward pass 25.1 ms; A prefetched two k-blocks ahead instead
+// of one 3-5 % slower; non-temporal Gy stores no change.
+constexpr int HW = 16;          // waves per workgroup
 constexpr int HMAXNX = 4;       // controls per step
-constexpr int HMAXN = 400;      // 3 LDS column blocks of Np x 16 doubles fit 160 KB up to Np = 400
-static_assert(HW * 64 <= 1024, "at most 16 waves per workgroup");
+constexpr int HMAXN_LDS = 512;  // y and z (2 x Np x 16 doubles) + the reduction scratch fit 160 KB of LDS
+constexpr int HMAXN = 2048;     // beyond HMAXN_LDS the 16 state columns live in a global scratch (L2-served)
 
 struct HeatArgs {
-  const d2 *sinv, *sinvT, *mass;
-  const double *minvF, *state0, *yd;
+  const d2 *sinv, *sinvT, *msinv;   // A-operand order: S⁻¹, S⁻ᵀ, M·S⁻¹
+  const double *minvF, *state0, *yd, *myd, *gy0;
+  double g0;
   const double *X;
   double *J, *DF, *GY;
+  double *SC;                       // [tiles][2][Np][16] y, z when they do not fit LDS
   int K, nx, nt, Np;
   double tau, gamma;
 };
 
-// acc[s] += A(tile w + HW·s) · Bs for this wave's row tiles; Bs is [Np][16] in LDS.  A-operand lanes hold
-// A[16t + (l & 15)][k + (l >> 4)] (MI355X_MICROARCH.md, v_mfma_f64_16x16x4_f64), two k-blocks per 16-byte load;
-// the loads of block kb + 1 are in flight while block kb's MFMAs issue.
-template <int TPW>
-__device__ __forceinline__ void heat_gemm(const d2 *__restrict__ A, const double *Bs, int Np, int w, int lane,
-                                          d4 (&acc)[TPW]) {
-  const int ntile = Np >> 4, KB = Np >> 3, bo = ((lane >> 4) << 4) + (lane & 15);
+// acc1 = A1(tile t) · Bs (and acc2 = A2(t) · Bs when A2) for the two row tiles t0, t1 of this wave (a tile
+// >= ntile is skipped); Bs is [Np][16].  A-operand lanes hold A[16t + (l & 15)][k + (l >> 4)] (MI355X_MICROARCH.md,
+// v_mfma_f64_16x16x4_f64), two k-blocks per 16-byte load; the loads of block kb + 1 are in flight while block kb's
+// MFMAs issue, and both products share the B reads.
+template <bool TWO>
+__device__ __forceinline__ void heat_gemm(const d2 *__restrict__ A1, const d2 *__restrict__ A2, const double *Bs,
+                                          int Np, int t0, int t1, int lane, d4 (&acc1)[2], d4 (&acc2)[2]) {
+  const int ntile = Np >> 4, KB = Np >> 3;
+  const bool on[2] = {t0 < ntile, t1 < ntile};
+  size_t off[2];
+  off[0] = (size_t)min(t0, ntile - 1) * KB * 64 + lane;
+  off[1] = (size_t)min(t1, ntile - 1) * KB * 64 + lane;
 #pragma unroll
-  for (int s = 0; s < TPW; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
-  const d2 *ap[TPW];
+  for (int s = 0; s < 2; ++s) acc1[s] = acc2[s] = d4{0.0, 0.0, 0.0, 0.0};
+  d2 n1[2], n2[2];
 #pragma unroll
-  for (int s = 0; s < TPW; ++s) ap[s] = A + (size_t)min(w + HW * s, ntile - 1) * KB * 64 + lane;
-  d2 an[TPW], an2[TPW];
-#pragma unroll
-  for (int s = 0; s < TPW; ++s) {
-    an[s] = ap[s][0];
-    if (PF > 1) an2[s] = ap[s][(size_t)min(1, KB - 1) * 64];
+  for (int s = 0; s < 2; ++s) {
+    n1[s] = A1[off[s]];
+    if (TWO) n2[s] = A2[off[s]];
   }
   for (int kb = 0; kb < KB; ++kb) {
-    d2 a[TPW];
+    d2 a1[2], a2[2];
 #pragma unroll
-    for (int s = 0; s < TPW; ++s) a[s] = an[s];
-    const int kn = min(kb + PF, KB - 1);
+    for (int s = 0; s < 2; ++s) a1[s] = n1[s], a2[s] = n2[s];
+    const size_t kn = (size_t)min(kb + 1, KB - 1) * 64;
 #pragma unroll
-    for (int s = 0; s < TPW; ++s) {
-      if (PF > 1) {
-        an[s] = an2[s];
-        an2[s] = ap[s][(size_t)kn * 64];
-      } else {
-        an[s] = ap[s][(size_t)kn * 64];
-      }
+    for (int s = 0; s < 2; ++s) {
+      n1[s] = A1[off[s] + kn];
+      if (TWO) n2[s] = A2[off[s] + kn];
     }
-    const double b0 = Bs[kb * 128 + bo], b1 = Bs[kb * 128 + 64 + bo];
+    const double b0 = Bs[kb * 128 + lane], b1 = Bs[kb * 128 + 64 + lane];
 #pragma unroll
-    for (int s = 0; s < TPW; ++s)
-      if (w + HW * s < ntile) {
-        acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].x, b0, acc[s], 0, 0, 0);
-        acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].y, b1, acc[s], 0, 0, 0);
+    for (int s = 0; s < 2; ++s)
+      if (on[s]) {
+        acc1[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s].x, b0, acc1[s], 0, 0, 0);
+        if (TWO) acc2[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s].x, b0, acc2[s], 0, 0, 0);
+        acc1[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s].y, b1, acc1[s], 0, 0, 0);
+        if (TWO) acc2[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s].y, b1, acc2[s], 0, 0, 0);
       }
   }
 }
 
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+// y / z in LDS: LDS traffic only, so the barrier waits for LDS operations alone (the Gy stores to HBM stay in
+// flight); in the global scratch the barrier must also drain the vector-memory stores
+template <bool GM>
+__device__ __forceinline__ void heat_barrier() {
+  if (GM)
+    __syncthreads();
+  else
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int TPW>
+template <bool GM>
 __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
   extern __shared__ __attribute__((aligned(16))) double hsm[];
   const int Np = H.Np, nx = H.nx, nt = H.nt, E = Np * 16;
-  double *Ys = hsm, *Zs = hsm + E, *Vs = hsm + 2 * E, *red = hsm + 3 * E;  // red: [HW][16], then [HW][HMAXNX][16]
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, c = lane & 15, tile = blockIdx.x;
   const int ntile = Np >> 4;
+  double *Ys = GM ? H.SC + (size_t)tile * 2 * E : hsm, *Zs = Ys + E;
+  double *red = GM ? hsm : hsm + 2 * E;  // [HW][16], then [HW][HMAXNX][16]
   const double tau = H.tau;
   const size_t xs = (size_t)nt * nx;  // doubles per restart in X / DF
-  // this thread's restart column in phase A (every e it visits has e & 15 == tid & 15: the stride is 16·HW)
+  // this thread's restart column in the elementwise phases (every e it visits has e & 15 == tid & 15)
   const int kcol = tile * 16 + (tid & 15);
   const double *xk = kcol < H.K ? H.X + (size_t)kcol * xs : nullptr;
   double *gyt = H.DF ? H.GY + (size_t)tile * nt * E : nullptr;
+  d4 acc[2], acc2[2];
 
-  // state column 0 = state0 (PDEObjective.jl:130); V = y_0 − yd_0
+  // state column 0 = state0 (PDEObjective.jl:130); Gy_0 and v_0ᵀMv_0 do not depend on the control (setup)
   for (int e = tid; e < E; e += HW * 64) {
-    const double y = H.state0[e >> 4];
-    Ys[e] = y;
-    Vs[e] = y - H.yd[e >> 4];
+    Ys[e] = H.state0[e >> 4];
+    if (gyt) gyt[e] = H.gy0[e >> 4];
   }
   __syncthreads();
   double gacc = 0.0;  // Σ_j w_j · v_jᵀ M v_j for column c (trapezoid weights of PDEObjective.jl:148-153)
-  d4 acc[TPW];
-  for (int j = 0;; ++j) {
-    // Gy_j = M·v_j; G-partial v·Gy; Gy_j to HBM for the adjoint (j < nt, when df is wanted)
-    heat_gemm<TPW>(H.mass, Vs, Np, w, lane, acc);
-    const double wj = (j == 0 || j == nt) ? 0.5 : 1.0;
-#pragma unroll
-    for (int s = 0; s < TPW; ++s) {
-      const int t = w + HW * s;
-      if (t < ntile) {
-        double part = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = 16 * t + (lane >> 4) + 4 * q;
-          part += Vs[r * 16 + c] * acc[s][q];
-          if (H.DF && j < nt) gyt[(size_t)j * E + r * 16 + c] = acc[s][q];
-        }
-        gacc += wj * part;
-      }
-    }
-    if (j == nt) break;
-    // Z = y_j + τ·(M⁻¹F · x_j)  (PDEObjective.jl:136)
+  for (int j = 0; j < nt; ++j) {
+    // z = y_j + τ·(M⁻¹F · x_j)  (PDEObjective.jl:136)
     {
       double xq[HMAXNX];
 #pragma unroll
@@ -178,22 +169,30 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
         Zs[e] = Ys[e] + tau * sf;
       }
     }
-    lds_barrier();
-    // y_{j+1} = S⁻¹·Z; v_{j+1} = y_{j+1} − yd_{j+1}
-    heat_gemm<TPW>(H.sinv, Zs, Np, w, lane, acc);
+    heat_barrier<GM>();
+    // y_{j+1} = S⁻¹·z; Gy_{j+1} = M·(y_{j+1} − yd_{j+1}) = (M·S⁻¹)·z − M·yd_{j+1}; G partial v·Gy
+    const double wj = (j + 1 == nt) ? 0.5 : 1.0;
+    const double *ydj = H.yd + (size_t)(j + 1) * Np, *mydj = H.myd + (size_t)(j + 1) * Np;
+    for (int t0 = w; t0 < ntile; t0 += 2 * HW) {
+      heat_gemm<true>(H.sinv, H.msinv, Zs, Np, t0, t0 + HW, lane, acc, acc2);
 #pragma unroll
-    for (int s = 0; s < TPW; ++s) {
-      const int t = w + HW * s;
-      if (t < ntile) {
+      for (int s = 0; s < 2; ++s) {
+        const int t = t0 + HW * s;
+        if (t < ntile) {
+          double part = 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = 16 * t + (lane >> 4) + 4 * q;
-          Ys[r * 16 + c] = acc[s][q];
-          Vs[r * 16 + c] = acc[s][q] - H.yd[(size_t)(j + 1) * Np + r];
+          for (int q = 0; q < 4; ++q) {
+            const int r = 16 * t + (lane >> 4) + 4 * q;
+            const double y = acc[s][q], gy = acc2[s][q] - mydj[r];
+            Ys[r * 16 + c] = y;
+            part += (y - ydj[r]) * gy;
+            if (gyt && j + 1 < nt) gyt[(size_t)(j + 1) * E + r * 16 + c] = gy;
+          }
+          gacc += wj * part;
         }
       }
     }
-    lds_barrier();
+    heat_barrier<GM>();
   }
   // J = τ·(½·Σ w_j v_jᵀMv_j + Σ w_j γ·Σx_j), x extended by its last column (PDEObjective.jl:145-153)
   gacc += __shfl_xor(gacc, 16);
@@ -201,7 +200,7 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
   if (lane < 16) red[w * 16 + lane] = gacc;
   __syncthreads();
   if (tid < 16 && H.J && kcol < H.K) {
-    double g = 0.0;
+    double g = 0.5 * H.g0;  // the j = 0 term (weight ½)
     for (int v = 0; v < HW; ++v) g += red[v * 16 + tid];
     double gt = 0.0;
     for (int i = 0; i <= nt; ++i) {
@@ -222,21 +221,23 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
       const double *g = gyt + (size_t)i * E;
       for (int e = tid; e < E; e += HW * 64) Zs[e] = Ys[e] + tau * g[e];
     }
-    lds_barrier();
-    heat_gemm<TPW>(H.sinvT, Zs, Np, w, lane, acc);
+    heat_barrier<GM>();
     double dq[HMAXNX] = {0.0, 0.0, 0.0, 0.0};
+    for (int t0 = w; t0 < ntile; t0 += 2 * HW) {
+      heat_gemm<false>(H.sinvT, nullptr, Zs, Np, t0, t0 + HW, lane, acc, acc2);
 #pragma unroll
-    for (int s = 0; s < TPW; ++s) {
-      const int t = w + HW * s;
-      if (t < ntile) {
+      for (int s = 0; s < 2; ++s) {
+        const int t = t0 + HW * s;
+        if (t < ntile) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = 16 * t + (lane >> 4) + 4 * q;
-          const double p = acc[s][q];
-          Ys[r * 16 + c] = p;
+          for (int q = 0; q < 4; ++q) {
+            const int r = 16 * t + (lane >> 4) + 4 * q;
+            const double p = acc[s][q];
+            Ys[r * 16 + c] = p;
 #pragma unroll
-          for (int m = 0; m < HMAXNX; ++m)
-            if (m < nx) dq[m] += H.minvF[(size_t)r * nx + m] * p;
+            for (int m = 0; m < HMAXNX; ++m)
+              if (m < nx) dq[m] += H.minvF[(size_t)r * nx + m] * p;
+          }
         }
       }
     }
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
       v += __shfl_xor(v, 32);
       if (lane < 16 && m < nx) redf[(w * HMAXNX + m) * 16 + lane] = v;
     }
-    lds_barrier();
+    heat_barrier<GM>();
     if (tid < nx * 16) {
       const int m = tid >> 4, cc = tid & 15, k = tile * 16 + cc;
       if (k < H.K) {
@@ -259,12 +260,16 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
   }
 }
 
-template <int TPW>
-hipError_t launch_tpw(hipStream_t s, const HeatArgs &H, int tiles) {
-  const size_t lds = ((size_t)3 * H.Np * 16 + HW * 16 + HW * HMAXNX * 16) * sizeof(double);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_heat_run<TPW>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_heat_run<TPW>, dim3(tiles), dim3(HW * 64), lds, s, H);
+hipError_t launch_heat(hipStream_t s, const HeatArgs &H, int tiles) {
+  const bool gm = H.Np > HMAXN_LDS;
+  const size_t lds = ((gm ? 0 : (size_t)2 * H.Np * 16) + HW * 16 + HW * HMAXNX * 16) * sizeof(double);
+  const void *fn = gm ? reinterpret_cast<const void *>(&k_heat_run<true>)
+                      : reinterpret_cast<const void *>(&k_heat_run<false>);
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (gm)
+    hipLaunchKernelGGL(k_heat_run<true>, dim3(tiles), dim3(HW * 64), lds, s, H);
+  else
+    hipLaunchKernelGGL(k_heat_run<false>, dim3(tiles), dim3(HW * 64), lds, s, H);
   return hipGetLastError();
 }
 
@@ -291,6 +296,7 @@ bool invert(int64_t N, std::vector<double> S, std::vector<double> &inv) {
   for (int64_t i = 0; i < N; ++i) inv[(size_t)i * N + i] = 1.0;
   auto s = [&](int64_t r, int64_t c) -> double & { return S[(size_t)c * N + r]; };
   auto v = [&](int64_t r, int64_t c) -> double & { return inv[(size_t)c * N + r]; };
+  std::vector<double> f(N);
   for (int64_t col = 0; col < N; ++col) {
     int64_t piv = col;
     for (int64_t r = col + 1; r < N; ++r)
@@ -300,11 +306,18 @@ bool invert(int64_t N, std::vector<double> S, std::vector<double> &inv) {
       for (int64_t c = 0; c < N; ++c) std::swap(s(piv, c), s(col, c)), std::swap(v(piv, c), v(col, c));
     const double d = s(col, col);
     for (int64_t c = 0; c < N; ++c) s(col, c) /= d, v(col, c) /= d;
-    for (int64_t r = 0; r < N; ++r) {
-      if (r == col) continue;
-      const double f = s(r, col);
-      if (f == 0.0) continue;
-      for (int64_t c = 0; c < N; ++c) s(r, c) -= f * s(col, c), v(r, c) -= f * v(col, c);
+    for (int64_t r = 0; r < N; ++r) f[r] = r == col ? 0.0 : s(r, col);
+    // column by column (contiguous in r): row r -= f[r] * pivot row
+    for (int64_t c = 0; c < N; ++c) {
+      const double ps = s(col, c), pv = v(col, c);
+      if (ps != 0.0) {
+        double *sc = &s(0, c);
+        for (int64_t r = 0; r < N; ++r) sc[r] -= f[r] * ps;
+      }
+      if (pv != 0.0) {
+        double *vc = &v(0, c);
+        for (int64_t r = 0; r < N; ++r) vc[r] -= f[r] * pv;
+      }
     }
   }
   return true;
@@ -338,7 +351,8 @@ int32_t mioc_heat_setup(mioc_ctx *ctx, int64_t N, int64_t nx, int64_t nt, double
                         const double *M_invA, const double *M_invF, const double *mass, const double *state0,
                         const double *yd) {
   if (!ctx) return MIOC_EINVAL;
-  if (N < 1 || N > HMAXN) return heat_fail(ctx, MIOC_EINVAL, "heat: need 1 <= Nglobal_dofs <= 400 (LDS-resident state)");
+  if (N < 1 || N > HMAXN)
+    return heat_fail(ctx, MIOC_EINVAL, "heat: need 1 <= Nglobal_dofs <= " + std::to_string(HMAXN));
   if (nx < 1 || nx > HMAXNX) return heat_fail(ctx, MIOC_EINVAL, "heat: need 1 <= nx <= 4 controls");
   if (nt < 1 || nt > (1 << 24)) return heat_fail(ctx, MIOC_EINVAL, "heat: bad nt");
   if (!(T1 > T0)) return heat_fail(ctx, MIOC_EINVAL, "heat: need T1 > T0");
@@ -367,8 +381,30 @@ int32_t mioc_heat_setup(mioc_ctx *ctx, int64_t N, int64_t nx, int64_t nt, double
   if ((rc = upload(ctx, &h->d_sinvT, swizzle(N, Np, [&](int64_t r, int64_t c) { return Si[(size_t)r * N + c]; }),
                    "S^-T")))
     return rc;
-  if ((rc = upload(ctx, &h->d_mass, swizzle(N, Np, [&](int64_t r, int64_t c) { return mass[(size_t)c * N + r]; }),
-                   "mass matrix")))
+  // M·S⁻¹ (column-major), M·yd_j, Gy_0 = M·(state0 − yd_0) and g0 = (state0 − yd_0)ᵀ Gy_0 for the fused step
+  std::vector<double> MS((size_t)N * N, 0.0), myd((size_t)(nt + 1) * Np, 0.0), gy0(Np, 0.0);
+  for (int64_t c = 0; c < N; ++c)
+    for (int64_t k = 0; k < N; ++k) {
+      const double b = Si[(size_t)c * N + k];
+      if (b == 0.0) continue;
+      for (int64_t r = 0; r < N; ++r) MS[(size_t)c * N + r] += mass[(size_t)k * N + r] * b;
+    }
+  for (int64_t j = 0; j <= nt; ++j)
+    for (int64_t k = 0; k < N; ++k) {
+      const double y = yd[(size_t)j * N + k];
+      if (y == 0.0) continue;
+      for (int64_t r = 0; r < N; ++r) myd[(size_t)j * Np + r] += mass[(size_t)k * N + r] * y;
+    }
+  double g0 = 0.0;
+  for (int64_t k = 0; k < N; ++k) {
+    const double v0 = state0[k] - yd[k];
+    for (int64_t r = 0; r < N; ++r) gy0[r] += mass[(size_t)k * N + r] * v0;
+  }
+  for (int64_t r = 0; r < N; ++r) g0 += (state0[r] - yd[r]) * gy0[r];
+  h->g0 = g0;
+  if ((rc = upload(ctx, &h->d_msinv, swizzle(N, Np, [&](int64_t r, int64_t c) { return MS[(size_t)c * N + r]; }),
+                   "M S^-1")) ||
+      (rc = upload(ctx, &h->d_myd, myd, "M yd")) || (rc = upload(ctx, &h->d_gy0, gy0, "Gy_0")))
     return rc;
   std::vector<double> f((size_t)Np * nx, 0.0), y0(Np, 0.0), ydp((size_t)(nt + 1) * Np, 0.0);
   for (int64_t r = 0; r < N; ++r) {
@@ -403,23 +439,27 @@ int32_t mioc_heat_eval_device(mioc_ctx *ctx, int64_t K, const double *d_x, doubl
   HeatArgs A;
   A.sinv = reinterpret_cast<const d2 *>(h->d_sinv);
   A.sinvT = reinterpret_cast<const d2 *>(h->d_sinvT);
-  A.mass = reinterpret_cast<const d2 *>(h->d_mass);
-  A.minvF = h->d_minvF, A.state0 = h->d_state0, A.yd = h->d_yd;
+  A.msinv = reinterpret_cast<const d2 *>(h->d_msinv);
+  A.minvF = h->d_minvF, A.state0 = h->d_state0, A.yd = h->d_yd, A.myd = h->d_myd, A.gy0 = h->d_gy0, A.g0 = h->g0;
   A.X = d_x, A.J = d_J, A.DF = d_df;
   A.GY = h->d_gy;
   A.K = (int)K, A.nx = (int)h->nx, A.nt = (int)h->nt, A.Np = (int)h->Np;
   A.tau = h->tau, A.gamma = h->gamma;
-  const int tpw = (int)((h->Np / 16 + HW - 1) / HW);
-  hipError_t e;
-  switch (tpw) {
-    case 1: e = launch_tpw<1>(ctx->stream, A, (int)tiles); break;
-    case 2: e = launch_tpw<2>(ctx->stream, A, (int)tiles); break;
-    case 3: e = launch_tpw<3>(ctx->stream, A, (int)tiles); break;
-    case 4: e = launch_tpw<4>(ctx->stream, A, (int)tiles); break;
-    case 5: e = launch_tpw<5>(ctx->stream, A, (int)tiles); break;
-    case 6: e = launch_tpw<6>(ctx->stream, A, (int)tiles); break;
-    default: e = launch_tpw<7>(ctx->stream, A, (int)tiles); break;
+  A.SC = nullptr;
+  if (h->Np > HMAXN_LDS) {
+    const size_t sneed = (size_t)tiles * 2 * h->Np * 16 * sizeof(double);
+    if (h->sc_cap < sneed) {
+      if (h->d_sc) hipFree(h->d_sc), h->d_sc = nullptr, h->sc_cap = 0;
+      if (hipMalloc(reinterpret_cast<void **>(&h->d_sc), sneed) != hipSuccess) {
+        (void)hipGetLastError();
+        h->d_sc = nullptr;
+        return heat_fail(ctx, MIOC_ENOMEM, "heat: cannot allocate the state scratch");
+      }
+      h->sc_cap = sneed;
+    }
+    A.SC = h->d_sc;
   }
+  const hipError_t e = launch_heat(ctx->stream, A, (int)tiles);
   if (e != hipSuccess) return heat_fail(ctx, MIOC_EHIP, std::string("k_heat_run: ") + hipGetErrorString(e));
   return MIOC_OK;
 }

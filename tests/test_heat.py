@@ -9,6 +9,7 @@ invariants (mass of the square = 4, constant state0).
 GPU tier: mioc_heat_eval_device against the oracle on the same matrices.  Bar: |J − J_oracle| ≤ 1e-9·|J_oracle| and
 max|df − df_oracle| ≤ 1e-9·max|df_oracle| (the device multiplies by the precomputed inverse of StateMat on the FP64
 matrix cores; the reference solves with its LU factors, so the results agree to rounding, not bit for bit).
+N <= 512 keeps the 16 state columns in LDS, larger N (up to 2048) in a global scratch: both are covered.
 """
 import numpy as np
 import pytest
@@ -105,8 +106,10 @@ def _check(hp, xs, J, df):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,nt,K", [(17, 500, 20), (5, 64, 33), (2, 7, 3), (22, 40, 16), (9, 1, 5), (12, 2, 17)],
-                         ids=["heat289_nt500", "N25_ragged", "N4", "N484_maxLDS", "nt1", "nt2"])
+@pytest.mark.parametrize("n,nt,K", [(17, 500, 20), (5, 64, 33), (2, 7, 3), (22, 40, 16), (9, 1, 5), (12, 2, 17),
+                                    (23, 12, 18), (33, 20, 9)],
+                         ids=["heat289_nt500", "N25_ragged", "N4", "N484_maxLDS", "nt1", "nt2", "N529_global",
+                              "N1089_global"])
 def test_heat_eval_device_vs_oracle(n, nt, K):
     hp = HeatProblem(n=n, nt=nt)
     xs = _controls(hp, K, seed=n * 1000 + nt)
@@ -155,7 +158,7 @@ def test_heat_errors():
     from mioc import native
     ctx = native.Context(0)
     with pytest.raises(native.MiocNativeError):
-        HeatProblem(n=23, nt=4).setup(ctx)  # N = 529 > 512
+        HeatProblem(n=46, nt=2).setup(ctx)  # N = 2116 > 2048
     import torch
     ctx.heat_shape = (4, 2, 4)
     with pytest.raises(native.MiocNativeError) as e:  # eval before a successful setup
