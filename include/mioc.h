@@ -210,7 +210,7 @@ int32_t mioc_rand_start_device(mioc_ctx *ctx, int64_t K, int64_t nt, int64_t jum
  * AMatLU = lu(StateMat'), df_i = (M⁻¹F)ᵀ p_i + Gu) with the hooks of example_heat.jl:135-161 (G = ½(y−yd)ᵀM(y−yd),
  * G_t = γ·Σx, Gu = γ).  mioc_heat_setup takes the matrices the Julia objective already holds (example_heat.jl:101-115;
  * all column-major): M_invA (N x N), M_invF (N x nx), mass = M (N x N), state0 (N), yd (N x (nt+1)); τ = (T1−T0)/nt,
- * StateMat = I + τ·M_invA is factored once on the host.  1 <= N <= 400, 1 <= nx <= 4.  mioc_heat_eval_device:
+ * StateMat = I + τ·M_invA is factored once on the host.  1 <= N <= 2048, 1 <= nx <= 4.  mioc_heat_eval_device:
  * d_x = K x nx x nt controls (the DP's input layout), d_J (K, nullable), d_df (K x nx x nt, nullable).  Enqueued.
  */
 int32_t mioc_heat_setup(mioc_ctx *ctx, int64_t N, int64_t nx, int64_t nt, double T0, double T1, double gamma,

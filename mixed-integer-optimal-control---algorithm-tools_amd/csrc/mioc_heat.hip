@@ -11,13 +11,14 @@
 //
 // Design.  The system is linear and time-invariant, so both triangular solves per step become one product with a
 // precomputed inverse (S⁻¹ for the state, S⁻ᵀ for the adjoint), and the K restarts side by side turn every step
-// into a dense (N × N) · (N × 16) product on the FP64 matrix cores: one workgroup per 16 restarts (one MFMA column
-// tile), all nt forward and nt adjoint steps in one launch, the 16 state columns resident in LDS.  Per forward step
-// two products (S⁻¹·Z, then M·(y − yd) for G and Gy), per adjoint step one (S⁻ᵀ·R); Gy_i goes to an HBM scratch
-// between the sweeps (written once, read once) instead of a third product.  The operand matrices stream from L2
-// (each ≤ 1.3 MB, shared by every workgroup of an XCD) in the MFMA A-operand order, one 16-byte load per lane per
-// two MFMAs.  Results agree with the reference's LU solves to rounding (the inverse and the MFMA sum order are not
-// the reference's operation order): the tests hold them to 1e-9 relative.
+// into a dense (N × N) · (N × 16) product on the FP64 matrix cores: one workgroup (16 waves) per 16 restarts (one
+// MFMA column tile), all nt forward and nt adjoint steps in one launch, the 16 state columns in LDS (N ≤ 512) or in
+// a per-workgroup global scratch (N ≤ 2048).  A forward step is one pass over its right-hand side z computing
+// y' = S⁻¹z and Gy' = (M·S⁻¹)z − M·yd' with two accumulators that share the B reads; an adjoint step one product
+// with S⁻ᵀ.  Gy goes to an HBM scratch between the sweeps (written once, read once).  The operand matrices stream
+// from L2 in the MFMA A-operand order, one 16-byte load per lane per two MFMAs.  Results agree with the
+// reference's LU solves to rounding (the inverse and the MFMA sum order are not the reference's operation order):
+// the tests hold them to 1e-9 relative.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
