@@ -66,7 +66,7 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 // of one 3-5 % slower; non-temporal Gy stores no change.
 constexpr int HW = 16;          // waves per workgroup
 constexpr int HMAXNX = 4;       // controls per step
-constexpr int HMAXN_LDS = 512;  // y and z (2 x Np x 16 doubles) + the reduction scratch fit 160 KB of LDS
+constexpr int HMAXN_LDS = 496;  // y and z (2 x Np x 16 doubles), yd / M·yd rows and the reductions fit 160 KB of LDS
 constexpr int HMAXN = 2048;     // beyond HMAXN_LDS the 16 state columns live in a global scratch (L2-served)
 
 struct HeatArgs {
@@ -139,7 +139,8 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, c = lane & 15, tile = blockIdx.x;
   const int ntile = Np >> 4;
   double *Ys = GM ? H.SC + (size_t)tile * 2 * E : hsm, *Zs = Ys + E;
-  double *red = GM ? hsm : hsm + 2 * E;  // [HW][16], then [HW][HMAXNX][16]
+  double *ydl = GM ? hsm : hsm + 2 * E, *mydl = ydl + Np;  // yd_{j+1}, M·yd_{j+1} of the running step
+  double *red = mydl + Np;                                   // [HW][16], then [HW][HMAXNX][16]
   const double tau = H.tau;
   const size_t xs = (size_t)nt * nx;  // doubles per restart in X / DF
   // this thread's restart column in the elementwise phases (every e it visits has e & 15 == tid & 15)
@@ -169,11 +170,15 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
           if (q < nx) sf += f[q] * xq[q];
         Zs[e] = Ys[e] + tau * sf;
       }
+      // the epilogue's yd_{j+1} / M·yd_{j+1} through LDS: their global round trip overlaps this phase's
+      for (int r = tid; r < Np; r += HW * 64) {
+        ydl[r] = H.yd[(size_t)(j + 1) * Np + r];
+        mydl[r] = H.myd[(size_t)(j + 1) * Np + r];
+      }
     }
     heat_barrier<GM>();
     // y_{j+1} = S⁻¹·z; Gy_{j+1} = M·(y_{j+1} − yd_{j+1}) = (M·S⁻¹)·z − M·yd_{j+1}; G partial v·Gy
     const double wj = (j + 1 == nt) ? 0.5 : 1.0;
-    const double *ydj = H.yd + (size_t)(j + 1) * Np, *mydj = H.myd + (size_t)(j + 1) * Np;
     for (int t0 = w; t0 < ntile; t0 += 2 * HW) {
       heat_gemm<true>(H.sinv, H.msinv, Zs, Np, t0, t0 + HW, lane, acc, acc2);
 #pragma unroll
@@ -184,9 +189,9 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int r = 16 * t + (lane >> 4) + 4 * q;
-            const double y = acc[s][q], gy = acc2[s][q] - mydj[r];
+            const double y = acc[s][q], gy = acc2[s][q] - mydl[r];
             Ys[r * 16 + c] = y;
-            part += (y - ydj[r]) * gy;
+            part += (y - ydl[r]) * gy;
             if (gyt && j + 1 < nt) gyt[(size_t)(j + 1) * E + r * 16 + c] = gy;
           }
           gacc += wj * part;
@@ -217,10 +222,30 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
   for (int e = tid; e < E; e += HW * 64) Ys[e] = 0.0;
   __syncthreads();
   double *redf = red + HW * 16;  // [HW][HMAXNX][16]
+  // Gy_i of this thread's first GPF elements is loaded one step ahead, in flight across the barrier and the product
+  constexpr int GPF = GM ? 2 : 8;  // the global-scratch variant has no registers to spare
+  double gn[GPF];
+#pragma unroll
+  for (int u = 0; u < GPF; ++u) {
+    const int e = tid + u * HW * 64;
+    gn[u] = e < E ? gyt[(size_t)(nt - 1) * E + e] : 0.0;
+  }
   for (int i = nt - 1; i >= 0; --i) {
     {
+#pragma unroll
+      for (int u = 0; u < GPF; ++u) {
+        const int e = tid + u * HW * 64;
+        if (e < E) Zs[e] = Ys[e] + tau * gn[u];
+      }
       const double *g = gyt + (size_t)i * E;
-      for (int e = tid; e < E; e += HW * 64) Zs[e] = Ys[e] + tau * g[e];
+      for (int e = tid + GPF * HW * 64; e < E; e += HW * 64) Zs[e] = Ys[e] + tau * g[e];
+      if (i > 0) {
+#pragma unroll
+        for (int u = 0; u < GPF; ++u) {
+          const int e = tid + u * HW * 64;
+          if (e < E) gn[u] = g[e - E];
+        }
+      }
     }
     heat_barrier<GM>();
     double dq[HMAXNX] = {0.0, 0.0, 0.0, 0.0};
@@ -263,7 +288,7 @@ __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
 
 hipError_t launch_heat(hipStream_t s, const HeatArgs &H, int tiles) {
   const bool gm = H.Np > HMAXN_LDS;
-  const size_t lds = ((gm ? 0 : (size_t)2 * H.Np * 16) + HW * 16 + HW * HMAXNX * 16) * sizeof(double);
+  const size_t lds = ((gm ? 0 : (size_t)2 * H.Np * 16) + 2 * (size_t)H.Np + HW * 16 + HW * HMAXNX * 16) * sizeof(double);
   const void *fn = gm ? reinterpret_cast<const void *>(&k_heat_run<true>)
                       : reinterpret_cast<const void *>(&k_heat_run<false>);
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
