@@ -16,6 +16,9 @@ from __future__ import annotations
 
 import numpy as np
 
+from .iterators import product_iterator
+from .objective import AbstractObjectiveLazy
+
 
 class HeatProblem:
     """Assembled data of example_heat.jl:23-116 on a structured P1 mesh (a stand-in for FEMBundle's P2 mesh)."""
@@ -77,3 +80,35 @@ class HeatProblem:
     def setup(self, ctx):
         """Hand the matrices to a native.Context (mioc_heat_setup)."""
         ctx.heat_setup(self.M_invA, self.M_invF, self.M, self.state0, self.yd, self.T0, self.T1, self.gamma)
+
+
+class HeatObj(AbstractObjectiveLazy):
+    """The reference's HeatObj (example_heat.jl:23-116) as a lazy objective for TRM: eval_f_helper and
+    eval_df_helper (PDEObjective.jl:142-199) run on the device through mioc_heat_eval (no CPU path).  One
+    device call computes both; the gradient of the last eval_f at obj.x is kept and handed out by eval_df."""
+
+    def __init__(self, problem=None, ctx=None, device=0, **kw):
+        from .native import Context
+        self.problem = HeatProblem(**kw) if problem is None else problem
+        hp = self.problem
+        self.T0, self.T1, self.nt, self.tau, self.gamma = hp.T0, hp.T1, hp.nt, hp.tau, hp.gamma
+        self.V = [list(v) for v in hp.levels]
+        self.iterator = product_iterator(self.V)  # no restrictions on the integer controls (example_heat.jl:44)
+        self.nu, self.nv = 0, len(self.V)
+        self.nx = self.nu + self.nv
+        self._init_fields(self.nx, self.nt)
+        self.ctx = Context(device) if ctx is None else ctx
+        hp.setup(self.ctx)
+        self._df_at = None
+
+    def eval_f_helper(self, x, cache):
+        J, df = self.ctx.heat_eval(np.asarray(x, dtype=np.float64)[None])
+        if cache:
+            self._df_at = (np.array(x, copy=True), df[0])
+        return float(J[0])
+
+    def eval_df_helper(self):
+        if self._df_at is None or not np.array_equal(self._df_at[0], self.x):
+            _, df = self.ctx.heat_eval(np.asarray(self.x, dtype=np.float64)[None])
+            self._df_at = (np.array(self.x, copy=True), df[0])
+        self.df[:, :] = self._df_at[1]

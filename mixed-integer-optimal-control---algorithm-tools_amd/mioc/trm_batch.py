@@ -9,7 +9,8 @@ The control flow is multi-trust.jl:53-170 per restart, run for K restarts in loc
   return            J + β·TV_p(u)                                            :169
 
 Device kernels do all O(nt) work: the random starts (mioc_rand_start_device, HelpFunctions.jl:204-225), the ODE
-objective and adjoint gradient (mioc_ode_eval_device, ODEObjective.jl:125-184), the DP and backtrack with one budget
+objective and adjoint gradient (mioc_ode_eval_device, ODEObjective.jl:125-184) or the PDE heat objective's
+(mioc_heat_eval_device, PDEObjective.jl:129-199), the DP and backtrack with one budget
 per restart after halving (mioc_backtrack_batch_budgets_device), pred and TV_p, and the decision.  Per inner
 iteration the host reads back K decision codes and keeps K small counters (Δᵏ, k, flags); the controls never leave
 HBM.  The context enqueues on its own stream and the few torch element-wise updates (masks, where) run on
@@ -39,16 +40,32 @@ def sos1_levels():
 
 
 def TRM_batch(problem, par, K=None, x0=None, seed=0, nt=None, device=0, log=None):  # noqa: C901
-    """Run TRM (multi-trust.jl:53-170) for K restarts of an ODE example on the device.
+    """Run TRM (multi-trust.jl:53-170) for K restarts of an ODE example, or of the PDE heat example, on the device.
 
-    x0: a (K, nt, 3) float64 CUDA tensor of starts, or None for K device random starts (rand_func_int with `seed`).
-    Returns (values (K,) numpy: J + β·TV_p(u) per restart, u (K, nt, 3) CUDA tensor: obj.x of each restart,
+    problem: "fishing" / "doubletank" / "vanderpol", or a mioc.heat.HeatProblem (example_heat.jl: 6 x 6 product
+    levels, gradient from mioc_heat_eval_device; its nt is the problem's).
+    x0: a (K, nt, nx) float64 CUDA tensor of starts, or None for K device random starts (rand_func_int with `seed`).
+    Returns (values (K,) numpy: J + β·TV_p(u) per restart, u (K, nt, nx) CUDA tensor: obj.x of each restart,
     iterations (K,) numpy)."""
     import torch
 
-    prob, nt_def, T0, T1 = PROBLEMS[problem]
-    lt = sos1_levels()
     ctx = Context(device)
+    if isinstance(problem, str):
+        prob, nt_def, T0, T1 = PROBLEMS[problem]
+        lt = sos1_levels()
+
+        def evalf(x, J, df):
+            ctx.ode_eval_tensors(prob, x, T0, T1, J, df)
+    else:  # the PDE heat objective (PDEObjective.jl:129-199, example_heat.jl)
+        hp = problem
+        nt_def, T0, T1 = hp.nt, hp.T0, hp.T1
+        if nt is not None and int(nt) != hp.nt:
+            raise ValueError("the heat problem fixes nt")
+        lt = LevelTable(hp.levels)
+        hp.setup(ctx)
+
+        def evalf(x, J, df):
+            ctx.heat_eval_tensors(x, J, df)
 
     def _to_torch():  # the context's results are read by torch ops
         ctx.synchronize()
@@ -75,7 +92,7 @@ def TRM_batch(problem, par, K=None, x0=None, seed=0, nt=None, device=0, log=None
     u_old = u.clone()
     J_old = torch.empty(K, **f64)
     _to_ctx()
-    ctx.ode_eval_tensors(prob, u, T0, T1, J_old, None)
+    evalf(u, J_old, None)
     tv_u = torch.empty(K, **f64)
     ctx.tv_tensors(u, tv_u)               # TV of the current u; afterwards every trial's TV_new
     J = torch.full((K,), math.inf, **f64)
@@ -95,7 +112,7 @@ def TRM_batch(problem, par, K=None, x0=None, seed=0, nt=None, device=0, log=None
         _to_torch()
         TV_old = tv_u.clone()                                    # TV_p(u, p), multi-trust.jl:99
         _to_ctx()
-        ctx.ode_eval_tensors(prob, u, T0, T1, None, df)          # ∇f at obj.x = u, :102-103
+        evalf(u, None, df)                                       # ∇f at obj.x = u, :102-103
         ctx.bellman_batch_tensors(df, u_old, B, tau)
         Dk = np.full(K, D0)
         k = np.ones(K, dtype=np.int64)
@@ -112,7 +129,7 @@ def TRM_batch(problem, par, K=None, x0=None, seed=0, nt=None, device=0, log=None
             # after an inner loop that ran out of kmax, where u is a rejected trial)
             pred_ref = int_val + beta * (TV_old - tv_new)
             _to_ctx()
-            ctx.ode_eval_tensors(prob, trial, T0, T1, J_new, None)
+            evalf(trial, J_new, None)
             ctx.trm_decide_tensors(J_old, J_new, TV_old, tv_new, pred_ref, sigma, dec)
             ctx.synchronize()
             d = dec.cpu().numpy()
@@ -142,7 +159,7 @@ def TRM_batch(problem, par, K=None, x0=None, seed=0, nt=None, device=0, log=None
         iters[active] += 1
         it += 1
     _to_ctx()
-    ctx.ode_eval_tensors(prob, u, T0, T1, None, df)              # final derivative, :166-167
+    evalf(u, None, df)                                           # final derivative, :166-167
     _to_torch()
     values = (J + beta * tv_u).cpu().numpy()                     # J + β·TV_p(u, p), :169
     ctx.close()
