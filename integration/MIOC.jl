@@ -170,13 +170,14 @@ end
     heat_eval!(ctx, x, df) -> fval
 
 eval_f_helper + eval_df_helper of PDEObjective.jl:142-199 for the control x (nx × nt) in one device call: returns
-the objective value and writes the gradient into df (nx × nt), as the two Julia helpers would.
+the objective value and, unless `df` is `nothing`, writes the gradient at x into df (nx × nt).
 """
-function heat_eval!(ctx::Context, x::Matrix{Float64}, df::Matrix{Float64})
-    size(df) == size(x) || throw(DimensionMismatch("df and x differ in shape"))
+function heat_eval!(ctx::Context, x::Matrix{Float64}, df::Union{Matrix{Float64},Nothing})
+    df === nothing || size(df) == size(x) || throw(DimensionMismatch("df and x differ in shape"))
     J = Ref{Float64}(0.0)
     check(ctx, ccall((:mioc_heat_eval, libmioc), Int32,
-                     (Ptr{Cvoid}, Int64, Ptr{Float64}, Ref{Float64}, Ptr{Float64}), ctx.ptr, 1, x, J, df))
+                     (Ptr{Cvoid}, Int64, Ptr{Float64}, Ref{Float64}, Ptr{Float64}), ctx.ptr, 1, x, J,
+                     df === nothing ? Ptr{Float64}(C_NULL) : df))
     J[]
 end
 

@@ -118,6 +118,18 @@ def test_heat_eval_device_vs_oracle(n, nt, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nh", [1, 3, 4], ids=["nx1", "nx3", "nx4"])
+def test_heat_control_counts_vs_oracle(nh):
+    """1 to 4 heaters (nx, the controls per step; mioc_heat_setup accepts up to 4)."""
+    spots = ((-1.0, 0.0), (1.0, 0.0), (0.0, 1.0), (0.0, -1.0))[:nh]
+    hp = HeatProblem(n=7, nt=30, c1=(10.0,) * nh, c2=(20.0,) * nh, heaters=spots)
+    rng = np.random.default_rng(nh)
+    xs = [rng.integers(0, 6, size=(nh, hp.nt)).astype(np.float64) for _ in range(5)]
+    J, df = _device_eval(hp, xs)
+    _check(hp, xs, J, df)
+
+
+@pytest.mark.gpu
 def test_heat_J_only_equals_J_with_gradient():
     hp = HeatProblem(n=9, nt=50)
     xs = _controls(hp, 19, seed=3)
@@ -159,6 +171,10 @@ def test_heat_errors():
     ctx = native.Context(0)
     with pytest.raises(native.MiocNativeError):
         HeatProblem(n=46, nt=2).setup(ctx)  # N = 2116 > 2048
+    with pytest.raises(native.MiocNativeError):  # nx = 5 > 4
+        ctx.heat_setup(np.eye(4), np.zeros((4, 5)), np.eye(4), np.ones(4), np.ones((4, 3)), 0.0, 1.0, 1.0)
+    with pytest.raises(native.MiocNativeError):  # T1 <= T0
+        ctx.heat_setup(np.eye(4), np.zeros((4, 2)), np.eye(4), np.ones(4), np.ones((4, 3)), 1.0, 1.0, 1.0)
     import torch
     ctx.heat_shape = (4, 2, 4)
     with pytest.raises(native.MiocNativeError) as e:  # eval before a successful setup
