@@ -11,6 +11,8 @@ max|df − df_oracle| ≤ 1e-9·max|df_oracle| (the device multiplies by the pre
 matrix cores; the reference solves with its LU factors, so the results agree to rounding, not bit for bit).
 N <= 512 keeps the 16 state columns in LDS, larger N (up to 2048) in a global scratch: both are covered.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -20,6 +22,27 @@ from oracle.heat_oracle import HeatOracle
 
 def _oracle(hp):
     return HeatOracle(hp.M_invA, hp.M_invF, hp.M, hp.state0, hp.yd, hp.T0, hp.T1, hp.gamma)
+
+
+HEAT_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "heat", "heat_n5_nt24.npz")
+
+
+def _golden():
+    z = np.load(HEAT_GOLDEN, allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def test_oracle_reproduces_heat_golden():
+    """The committed fixture (tests/golden/heat/make_heat_golden.py): the oracle on its stored matrices reproduces
+    J and df to 1e-12 relative (a regression anchor for the restatement; bit-equal on the machine that wrote it,
+    LAPACK builds elsewhere may round the triangular solves differently)."""
+    g = _golden()
+    T0, T1, gamma = g["scalars"]
+    o = HeatOracle(g["M_invA"], g["M_invF"], g["M"], g["state0"], g["yd"], T0, T1, gamma)
+    for k in range(len(g["x"])):
+        f, df, _ = o.eval(g["x"][k])
+        assert abs(f - g["J"][k]) <= 1e-12 * abs(g["J"][k]), k
+        assert np.max(np.abs(df - g["df"][k])) <= 1e-12 * np.max(np.abs(g["df"][k])), k
 
 
 def test_standin_assembly_invariants():
@@ -127,6 +150,27 @@ def test_heat_control_counts_vs_oracle(nh):
     xs = [rng.integers(0, 6, size=(nh, hp.nt)).astype(np.float64) for _ in range(5)]
     J, df = _device_eval(hp, xs)
     _check(hp, xs, J, df)
+
+
+@pytest.mark.gpu
+def test_heat_device_vs_golden():
+    """The device on the committed fixture's matrices and controls against its stored J / df (1e-9 relative)."""
+    import torch
+    from mioc import native
+    g = _golden()
+    T0, T1, gamma = g["scalars"]
+    ctx = native.Context(0)
+    ctx.heat_setup(g["M_invA"], g["M_invF"], g["M"], g["state0"], g["yd"], T0, T1, gamma)
+    dx = torch.tensor(np.ascontiguousarray(g["x"].transpose(0, 2, 1)), dtype=torch.float64, device="cuda")
+    J = torch.empty(len(g["x"]), dtype=torch.float64, device="cuda")
+    df = torch.empty_like(dx)
+    ctx.heat_eval_tensors(dx, J, df)
+    ctx.synchronize()
+    J, df = J.cpu().numpy(), df.cpu().numpy()
+    ctx.close()
+    for k in range(len(g["x"])):
+        assert abs(J[k] - g["J"][k]) <= 1e-9 * abs(g["J"][k]), k
+        assert np.max(np.abs(df[k].T - g["df"][k])) <= 1e-9 * np.max(np.abs(g["df"][k])), k
 
 
 @pytest.mark.gpu
