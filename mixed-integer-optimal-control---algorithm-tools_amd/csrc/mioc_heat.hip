@@ -31,6 +31,7 @@
 namespace mioc {
 
 struct HeatState {
+  bool ready = false;  // every device table matches N / Np / nx / nt (false after a failed setup)
   int64_t N = 0, Np = 0, nx = 0, nt = 0;
   double tau = 0.0, gamma = 0.0;
   double *d_sinv = nullptr, *d_sinvT = nullptr;                    // A-operand order, [Np/16][Np/8][64] double2
@@ -398,6 +399,7 @@ int32_t mioc_heat_setup(mioc_ctx *ctx, int64_t N, int64_t nx, int64_t nt, double
   const int64_t Np = (N + 15) / 16 * 16;
   HeatState *h = ctx->heat ? ctx->heat : new HeatState();
   ctx->heat = h;
+  h->ready = false;  // until every table below is uploaded for the new sizes
   h->N = N, h->Np = Np, h->nx = nx, h->nt = nt, h->tau = tau, h->gamma = gamma;
   if (hipSetDevice(ctx->device) != hipSuccess) return heat_fail(ctx, MIOC_EHIP, "hipSetDevice failed");
   int rc;
@@ -442,13 +444,14 @@ int32_t mioc_heat_setup(mioc_ctx *ctx, int64_t N, int64_t nx, int64_t nt, double
   if ((rc = upload(ctx, &h->d_minvF, f, "M_invF")) || (rc = upload(ctx, &h->d_state0, y0, "state0")) ||
       (rc = upload(ctx, &h->d_yd, ydp, "yd")))
     return rc;
+  h->ready = true;
   return MIOC_OK;
 }
 
 int32_t mioc_heat_eval_device(mioc_ctx *ctx, int64_t K, const double *d_x, double *d_J, double *d_df) {
   if (!ctx) return MIOC_EINVAL;
   HeatState *h = ctx->heat;
-  if (!h || !h->d_sinv) return heat_fail(ctx, MIOC_ESTATE, "heat: mioc_heat_setup first");
+  if (!h || !h->ready) return heat_fail(ctx, MIOC_ESTATE, "heat: no successful mioc_heat_setup");
   if (K < 1 || K > INT32_MAX || !d_x) return heat_fail(ctx, MIOC_EINVAL, "heat: bad K / x");
   if (hipSetDevice(ctx->device) != hipSuccess) return heat_fail(ctx, MIOC_EHIP, "hipSetDevice failed");
   const int64_t tiles = (K + 15) / 16;
@@ -493,7 +496,7 @@ int32_t mioc_heat_eval_device(mioc_ctx *ctx, int64_t K, const double *d_x, doubl
 int32_t mioc_heat_eval(mioc_ctx *ctx, int64_t K, const double *x, double *J, double *df) {
   if (!ctx) return MIOC_EINVAL;
   HeatState *h = ctx->heat;
-  if (!h || !h->d_sinv) return heat_fail(ctx, MIOC_ESTATE, "heat: mioc_heat_setup first");
+  if (!h || !h->ready) return heat_fail(ctx, MIOC_ESTATE, "heat: no successful mioc_heat_setup");
   if (K < 1 || K > INT32_MAX || !x || (!J && !df)) return heat_fail(ctx, MIOC_EINVAL, "heat: bad K / x / outputs");
   if (hipSetDevice(ctx->device) != hipSuccess) return heat_fail(ctx, MIOC_EHIP, "hipSetDevice failed");
   const size_t nxt = (size_t)K * h->nx * h->nt, need = (2 * nxt + K) * sizeof(double);
