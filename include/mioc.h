@@ -67,6 +67,11 @@ extern "C" {
                                whose workgroups hand rows to each other; 0: one launch per step */
 #define MIOC_OPT_PRED_FMA 4 /* mioc_pred*: 1 accumulates each ∇f[:,j]'(u_old[:,j] - u[:,j]) with fma, as an
                                FMA-contracted BLAS ddot does; 0 (default): products rounded, then added */
+#define MIOC_OPT_SPIN_LIMIT 5 /* separable transform, persistent launch: polls a dependency wait may take
+                                 before the launch is abandoned and the DP redone with per-step launches
+                                 (default 2^24; a tiny value forces that fallback, for tests) */
+#define MIOC_OPT_SDT_BUFFERS 6 /* persistent separable transform: staging buffers (4..64, default 64; more
+                                  buffers let rows run further apart, which hides the row hand-off) */
 
 typedef struct mioc_ctx mioc_ctx;
 
@@ -243,8 +248,9 @@ int32_t mioc_last_algo(mioc_ctx *ctx);
  * targets of rows sent straight to the exact scan: few targets, or a value scale outside its binade), [2] backtrack: p=Inf walk steps resolved
  * by the exact scan, or for the U-table walks (generic, pyramid) the run-ahead rounds taken (each round
  * settles up to 64 steps), [3] internal consistency failures (must be 0); [4..7] pyramid internals: rows whose
- * value hash overflowed, targets whose value was not found, values flagged as colliding; [7] fused DP: resident
- * workgroups per CU (occupancy query).
+ * value hash overflowed, targets whose value was not found, values flagged as colliding (after a separable-transform
+ * DP, [6] instead counts this context's persistent DPs redone with per-step launches: cooperative launch refused, or
+ * a dependency wait timed out -- 0 on a healthy run); [7] fused DP: resident workgroups per CU (occupancy query).
  */
 int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n);
 

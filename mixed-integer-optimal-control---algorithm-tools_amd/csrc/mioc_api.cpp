@@ -92,6 +92,7 @@ void ev_collect(mioc_ctx *ctx);
 
 void free_all(mioc_ctx *ctx) {
   if (ctx->d_runflags) hipFree(ctx->d_runflags);
+  if (ctx->d_chain) hipFree(ctx->d_chain);
   if (ctx->h_run_err) hipHostFree(ctx->h_run_err);
   void *ptrs[] = {ctx->d_nuval, ctx->d_nuint,  ctx->d_gidx,      ctx->d_numin,       ctx->d_numax,
                   ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
@@ -270,61 +271,61 @@ int run_bellman(mioc_ctx *ctx) {
 
   if (algo == MIOC_ALGO_PYRAMID || algo == MIOC_ALGO_SEPARABLE) {
     const size_t s_stride = (size_t)(ctx->B + 1) * L;
-    // persistent separable transform: every workgroup resident, one per CU (96 KB of LDS keeps a second one
-    // off the CU: its register file would not hold it), kSdtBuffers staging buffers; B + 1 rows on B
-    // workgroups, workgroup 0 taking rows 0 and B (k_sdt_run)
-    // 96 KB keeps the workgroups one per CU (the register file holds one: k_sdt_run needs 256 VGPRs per lane)
-    const size_t run_lds = std::max<size_t>(sdt_lds_bytes(ctx->pyr), 96 * 1024);
-    int nwg = 0, kint = 1;
+    // persistent separable transform: rows 1..B of every subproblem in contiguous chunks over resident workgroups
+    // (one per CU: the row body needs 2 waves per SIMD of registers and ~106 KB of LDS), row 0 of every step
+    // precomputed (k_sdt_chain, k_sdt_row0), NB staging buffers
+    const size_t run_lds = sdt_lds_bytes(ctx->pyr);
+    int nwg = 0;
     bool persist = false;
     // (B + 1)·L·8 < 2^31: the persistent kernel addresses a staging block with 32-bit buffer offsets
     // ... and every b̃ within the kernel's dependency window (7 per dimension: u_old on the level grid); a u_old
     // off the grid reaches rows further back than the window waits for, so those problems take per-step launches
-    if (algo == MIOC_ALGO_SEPARABLE && ctx->opt_persist && nt >= 2 && s_stride * sizeof(double) < (1ull << 31) &&
-        bmax <= 7 * ctx->pyr.M && !ctx->force_steps) {
+    if (algo == MIOC_ALGO_SEPARABLE && ctx->opt_persist && nt >= 2 && ctx->B >= 1 &&
+        s_stride * sizeof(double) < (1ull << 31) && bmax <= 7 * ctx->pyr.M && !ctx->force_steps) {
       int ncu = 0;
       HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-      const int bpc = sdt_run_blocks_per_cu(ctx->pyr, run_lds);
+      const int bpc = std::min(sdt_run_blocks_per_cu(ctx->pyr, run_lds), 1);  // one row workgroup per CU
       const size_t slots = (size_t)ncu * (size_t)std::max(bpc, 0);
-      const size_t Bw = (size_t)std::max<int64_t>(ctx->B, 1);  // one row per workgroup: B (rows 0, B share one)
-      if (K * Bw <= slots || K > 8 || Bw > slots) {
-        // contiguous row chunks, nwg / K workgroups per subproblem
-        const size_t per_k = std::min<size_t>(Bw, K ? slots / K : 0);
-        nwg = (int)(per_k * K);
-        kint = 1;
-      } else {
-        // more subproblems than the CUs hold one row each of: every workgroup keeps one row of all K, interleaved
-        nwg = (int)Bw;
-        kint = (int)K;
-      }
-      persist = nwg > 0;
+      const size_t per_k = std::min<size_t>((size_t)ctx->B, K ? slots / K : 0);  // workgroups per subproblem
+      nwg = (int)(per_k * K);
+      persist = per_k >= 1;
     }
+    // persistent layout: per subproblem NB staging buffers of (B+1)·L, then row 0 of every step (nt·L), one region
+    // addressed by one buffer resource (< 4 GiB); per-step layout: two buffers of K blocks of (B+1)·L
+    const int nbuf = persist ? ctx->opt_nb : 2;
+    const size_t kstride = persist ? (size_t)nbuf * s_stride + nt * L : s_stride;
+    if (persist && kstride * sizeof(double) >= (1ull << 32)) persist = false;  // (then also kstride = s_stride)
+    const size_t ks = persist ? kstride : s_stride;
     const size_t runflag_bytes = ((2 * K * (size_t)(ctx->B + 1) + 1) * sizeof(int32_t) + 15) / 16 * 16;
     if (persist) {
       int rcf = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, runflag_bytes, "persistent row flags");
+      if (!rcf) rcf = grow(ctx, &ctx->d_chain, &ctx->chain_cap, K * nt * sizeof(double), "row 0 chain");
       if (rcf) return rcf;
       if (!ctx->h_run_err) HIP_TRY(ctx, hipHostMalloc(&ctx->h_run_err, 16, 0));
       *ctx->h_run_err = 0;
     }
-    const int nbuf = persist ? kSdtBuffers : 2;
-    int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, nbuf * K * s_stride * sizeof(double), "staging fronts");
+    const size_t stage_doubles = persist ? K * ks : 2 * K * s_stride;
+    int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, stage_doubles * sizeof(double), "staging fronts");
     if (rc) return rc;
+    ctx->stage_kstride = ks;
     const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
     rc = grow(ctx, &ctx->d_U, &ctx->U_cap, K * uu_stride_k * sizeof(uint16_t), "argmin table U");
     if (rc) return rc;
     rc = grow(ctx, &ctx->d_perm, &ctx->perm_cap, K * nt * L * sizeof(uint32_t), "sphere orders");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
-    double *term = persist ? ctx->d_stage + ((nt - 1) % kSdtBuffers) * K * s_stride : st[(nt - 1) & 1];
+    double *term = persist ? ctx->d_stage + ((nt - 1) % nbuf) * s_stride : st[(nt - 1) & 1];
     HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm));
-    HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, term, s_stride));
+    HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, term, ks));
     if (algo == MIOC_ALGO_SEPARABLE && persist) {
       // the whole DP as one persistent launch: rows handed between resident workgroups by flags
+      HIP_TRY(ctx, launch_sdt_prep(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_chain, ctx->d_stage, ks,
+                                   (size_t)nbuf * s_stride, (uint16_t *)ctx->d_U, uu_stride_k));
       HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, runflag_bytes, ctx->stream));
       ev_begin(ctx, 0, "k_sdt_run");
-      const hipError_t le = launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_stage, K * s_stride,
-                                           (uint16_t *)ctx->d_U, s_stride, uu_stride_k, ctx->d_counters,
-                                           ctx->d_runflags, nwg, kint, run_lds);
+      const hipError_t le = launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_stage, ks, nbuf,
+                                           (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags, nwg,
+                                           ctx->spin_limit, run_lds);
       if (le == hipErrorCooperativeLaunchTooLarge) {  // not every workgroup can be resident: one launch per step
         (void)hipGetLastError();
         ev_end(ctx, 0, 0);
@@ -411,7 +412,16 @@ int run_bellman(mioc_ctx *ctx) {
   return MIOC_OK;
 }
 
+int check_run(mioc_ctx *ctx);
+
 int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_star, int32_t *d_status) {
+  // a persistent DP still in flight: learn whether its dependency waits timed out BEFORE anything reads its
+  // tables, so that a redone DP (check_run) is what the backtrack walks
+  if (ctx->run_pending) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const int rcr = check_run(ctx);
+    if (rcr) return rcr;
+  }
   if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "backtrack called before bellman");
   if (B_use < 0 || B_use > ctx->B)
     return fail(ctx, MIOC_ESTATE, "B_use must satisfy 0 <= B_use <= B of the last bellman call");
@@ -432,7 +442,8 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
   if (ctx->algo == MIOC_ALGO_PYRAMID || ctx->algo == MIOC_ALGO_SEPARABLE) {
     const size_t s_stride = (size_t)(ctx->B + 1) * ctx->L;
     const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
-    HIP_TRY(ctx, launch_stage_argmin0(ctx->stream, P, Lv, ctx->d_perm, ctx->d_stage, s_stride, (int)B_use, ctx->d_start));
+    HIP_TRY(ctx, launch_stage_argmin0(ctx->stream, P, Lv, ctx->d_perm, ctx->d_stage, ctx->stage_kstride, (int)B_use,
+                                      ctx->d_start));
     ev_begin(ctx, 1, "k_stage_walk");
     HIP_TRY(ctx, launch_stage_walk(ctx->stream, P, Lv, (const uint16_t *)ctx->d_U, uu_stride_k, ctx->d_start,
                                    d_urank, ctx->d_ranks, ctx->d_flags + 2));
@@ -563,6 +574,16 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   }
   if (option == MIOC_OPT_PRED_FMA) {
     ctx->pred_fma = value != 0;
+    return MIOC_OK;
+  }
+  if (option == MIOC_OPT_SPIN_LIMIT) {
+    if (value < 1 || value > (1ll << 30)) return fail(ctx, MIOC_EINVAL, "spin limit must be in [1, 2^30]");
+    ctx->spin_limit = (unsigned)value;
+    return MIOC_OK;
+  }
+  if (option == MIOC_OPT_SDT_BUFFERS) {
+    if (value < 4 || value > kSdtMaxBuffers) return fail(ctx, MIOC_EINVAL, "staging buffers must be in [4, 64]");
+    ctx->opt_nb = (int)value;
     return MIOC_OK;
   }
   return fail(ctx, MIOC_EINVAL, "unknown option");
@@ -846,10 +867,7 @@ int32_t mioc_ode_eval_device(mioc_ctx *ctx, int32_t problem, int64_t K, const do
   double par[14] = {};
   for (int q = 0; q < np; ++q) par[q] = params ? params[q] : def[q];
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  if (d_df) {
-    int rc = grow(ctx, &ctx->d_ode_state, &ctx->ode_cap, (size_t)K * nt * 2 * sizeof(double), "ODE states");
-    if (rc) return rc;
-  } else if (!ctx->d_ode_state) {
+  {  // k_ode_eval stores every restart's forward states, J-only calls included
     int rc = grow(ctx, &ctx->d_ode_state, &ctx->ode_cap, (size_t)K * nt * 2 * sizeof(double), "ODE states");
     if (rc) return rc;
   }
@@ -988,7 +1006,8 @@ int32_t mioc_pred(mioc_ctx *ctx, double *int_val, double *tv_old, double *tv_new
   double *o = ctx->d_pred_own;
   TrmDev T = trm_dev(ctx, 7, 1, ctx->nt);
   T.out_int = o, T.out_told = o + 1, T.out_tnew = o + 2, T.out_pred = o + 3;
-  HIP_TRY(ctx, hipMemsetAsync(o + 4, 0, sizeof(double), ctx->stream));
+  if (!ctx->trm_pending) HIP_TRY(ctx, hipMemsetAsync(o + 4, 0, sizeof(double), ctx->stream));
+  ctx->trm_pending = false;  // checked below, with this call's own flag
   HIP_TRY(ctx, launch_trm_pred(ctx->stream, T));
   double h[5];
   HIP_TRY(ctx, hipMemcpyAsync(h, o, 5 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
@@ -1010,7 +1029,9 @@ int32_t mioc_pred_batch_device(mioc_ctx *ctx, double *d_int_val, double *d_tv_ol
     return fail(ctx, MIOC_ESTATE, "pred needs a backtrack result");
   TrmDev T = trm_dev(ctx, 7, ctx->K, ctx->nt);
   T.out_int = d_int_val, T.out_told = d_tv_old, T.out_tnew = d_tv_new, T.out_pred = d_pred;
-  HIP_TRY(ctx, hipMemsetAsync(ctx->d_pred_own + 4, 0, sizeof(double), ctx->stream));
+  // the error flag is cleared by the first enqueue after a check only: an error of an earlier, not yet synchronised
+  // TV / pred call stays visible to the next mioc_synchronize
+  if (!ctx->trm_pending) HIP_TRY(ctx, hipMemsetAsync(ctx->d_pred_own + 4, 0, sizeof(double), ctx->stream));
   HIP_TRY(ctx, launch_trm_pred(ctx->stream, T));
   ctx->trm_pending = true;
   return MIOC_OK;
@@ -1025,7 +1046,9 @@ int32_t mioc_tv_device(mioc_ctx *ctx, int64_t K, const double *d_u, int64_t nx, 
   TrmDev T = trm_dev(ctx, 4, K, nt);
   T.u = d_u;
   T.out_tnew = d_tv;
-  HIP_TRY(ctx, hipMemsetAsync(ctx->d_pred_own + 4, 0, sizeof(double), ctx->stream));
+  // the error flag is cleared by the first enqueue after a check only: an error of an earlier, not yet synchronised
+  // TV / pred call stays visible to the next mioc_synchronize
+  if (!ctx->trm_pending) HIP_TRY(ctx, hipMemsetAsync(ctx->d_pred_own + 4, 0, sizeof(double), ctx->stream));
   HIP_TRY(ctx, launch_trm_pred(ctx->stream, T));
   ctx->trm_pending = true;
   return MIOC_OK;
@@ -1069,7 +1092,10 @@ int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->d_counters) HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
   HIP_TRY(ctx, hipMemcpy(f, ctx->d_flags, sizeof f, hipMemcpyDeviceToHost));
-  const int64_t all[8] = {c[0], c[1], f[2], f[3], c[4], c[5], c[6], ctx->occupancy};
+  // slot 6: the separable transform's persistent DPs redone with per-step launches (cooperative launch refused or a
+  // dependency wait timed out) -- its kernels write no c[6]; the pyramid's value-collision count otherwise
+  const int64_t c6 = ctx->algo == MIOC_ALGO_SEPARABLE ? ctx->n_persist_fallbacks : c[6];
+  const int64_t all[8] = {c[0], c[1], f[2], f[3], c[4], c[5], c6, ctx->occupancy};
   for (int32_t q = 0; q < n && q < 8; ++q) counters[q] = all[q];
   return MIOC_OK;
 }
@@ -1083,6 +1109,10 @@ int32_t mioc_get_argmin_table(mioc_ctx *ctx, int64_t k, int64_t step, int32_t *U
     return fail(ctx, MIOC_EINVAL, "the p=Inf collapse keeps per-budget class tables, not U");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  {
+    const int rcr = check_run(ctx);  // a timed-out persistent DP is redone before its table is read
+    if (rcr) return rcr;
+  }
   const int64_t R = ctx->B + 1, L = ctx->L, M = ctx->M, nt = ctx->nt;
   std::vector<double> uo(M);
   HIP_TRY(ctx, hipMemcpy(uo.data(), ctx->d_uold + ((size_t)k * nt + step) * M, M * sizeof(double),

@@ -92,13 +92,18 @@ size_t pyr_lds_bytes(const PyrGeom &G);
 // separable L1 transform (mioc_sdt.hip): same staging layout, 8^M grids (M = 3, 4), beta > 0
 bool sdt_supported(const PyrGeom &G);
 size_t sdt_lds_bytes(const PyrGeom &G);
-constexpr int kSdtBuffers = 4;  // persistent separable transform: staging buffers S_i, step i in buffer i % 4
+constexpr int kSdtMaxBuffers = 64;  // persistent separable transform: staging buffers S_i, step i in buffer i % NB
 hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
                            const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
                            size_t uu_stride_k, int32_t *counters);
+// persistent driver: per subproblem one region of kstride doubles = NB staging buffers of (B+1)·L, then row 0 of
+// every step (nt·L, at r0off); k_sdt_chain + k_sdt_row0 fill row 0, its U rows and S_0 row 0, then k_sdt_run
+hipError_t launch_sdt_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
+                           const uint32_t *perm, double *V, double *S, size_t kstride, size_t r0off, uint16_t *UU,
+                           size_t uu_stride_k);
 hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
-                          const uint32_t *perm, double *S, size_t buf_stride, uint16_t *UU, size_t s_stride,
-                          size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, int kint, size_t lds);
+                          const uint32_t *perm, double *S, size_t kstride, int NB, uint16_t *UU, size_t uu_stride_k,
+                          int32_t *counters, int32_t *flags, int nwg, unsigned spin_limit, size_t lds);
 int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds);
 hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
                                 const double *S0, size_t s_stride, int Bu, Start *start);
@@ -229,8 +234,13 @@ struct mioc_ctx {
   size_t perm_cap = 0;
   bool opt_persist = true;         // separable transform: one persistent launch (MIOC_OPT_PERSIST)
   bool force_steps = false;        // redo of a persistent DP whose waits timed out: per-step launches
-  int64_t n_persist_fallbacks = 0; // persistent DPs redone with per-step launches (diagnostics [6] of the sdt)
+  int64_t n_persist_fallbacks = 0; // persistent DPs redone with per-step launches (mioc_diagnostics slot 6 after a separable DP)
   int32_t *d_runflags = nullptr;   // persistent DP: [K][B+1] done, [K][B+1] loaded, err
+  double *d_chain = nullptr;       // persistent DP: V[k][i] = Φ_i[j0(i), 0], the row-0 chain (k_sdt_chain)
+  size_t chain_cap = 0;
+  unsigned spin_limit = 1u << 24;  // persistent DP: polls before a dependency wait gives up (MIOC_OPT_SPIN_LIMIT)
+  size_t stage_kstride = 0;        // doubles between two subproblems' staging blocks in the last pyramid / sdt DP
+  int opt_nb = mioc::kSdtMaxBuffers;    // staging buffers of a persistent separable DP (MIOC_OPT_SDT_BUFFERS)
   size_t runflag_cap = 0;
   int32_t *h_run_err = nullptr;    // pinned copy of err
   bool run_pending = false;

@@ -44,7 +44,6 @@ constexpr int SD_COOP = 8;               // listed targets up to this many: whol
 constexpr int SD_FEW = 4;                // rows with at most this many targets go straight to the exact scan
 constexpr int SD_SPARSE = 4;             // rows with at most this many finite sources: direct minimum over them
 constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, the scan sweeps every rank
-constexpr int SD_BLAG = 2;               // persistent kernel: row B runs this many steps behind row 0
 #ifndef SDT_RUN_MINW
 #define SDT_RUN_MINW 2                   // persistent kernel: waves per SIMD the registers must allow (4: two workgroups per CU, but the row code then spills)
 #endif
@@ -73,14 +72,21 @@ __device__ unsigned long long g_sdt_stamps[4096][16];
 #define SD_TL(k) \
   do {           \
   } while (0)
-#elif defined(MIOC_STAMPS)
-// persistent-kernel timeline (diagnostic build, make stamps_tl): per row, for steps i < 64: wait begin, wait
-// end (after the barrier), row body end, done published -- s_memrealtime (100 MHz); no in-row stamps
-__device__ unsigned long long g_sdt_tl[4096][64][4];
-#define SD_TL(k)                                                                                          \
-  do {                                                                                                    \
-    if (threadIdx.x == 0 && g < 4096 && (unsigned)i < 64u) g_sdt_tl[g][i][k] = __builtin_amdgcn_s_memrealtime();    \
+#define SD_TL_AT(gg, ii, ntt, k) \
+  do {                           \
   } while (0)
+#elif defined(MIOC_STAMPS)
+// persistent-kernel timeline (diagnostic build, make stamps_tl): per row g and for the 64 steps from nt/2 down,
+// s_memrealtime (100 MHz) at 8 points of a row: 0 start, 1 its loads consumed (after the first barrier), 2 mid
+// point reached, 3 previous row drained, 4 next row's inputs ready (poll done), 5 next row's loads issued, 6 stores
+// issued
+__device__ unsigned long long g_sdt_tl[4096][64][8];
+#define SD_TL_AT(gg, ii, ntt, k)                                                                          \
+  do {                                                                                                    \
+    if (threadIdx.x == 0 && (gg) < 4096 && (unsigned)((ii) - ((ntt) >> 1)) < 64u)                          \
+      g_sdt_tl[gg][(ii) - ((ntt) >> 1)][k] = __builtin_amdgcn_s_memrealtime();                             \
+  } while (0)
+#define SD_TL(k) SD_TL_AT(g, i, P.nt, k)
 #define SD_STAMP(k) \
   do {              \
   } while (0)
@@ -93,6 +99,9 @@ __device__ unsigned long long g_sdt_tl[4096][64][4];
 #else
 #define SD_TL(k) \
   do {           \
+  } while (0)
+#define SD_TL_AT(gg, ii, ntt, k) \
+  do {                           \
   } while (0)
 #define SD_STAMP(k) \
   do {              \
@@ -111,6 +120,20 @@ __device__ __forceinline__ double sd_min(double a, double b) {
   asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+
+// The thread index as a value the compiler cannot hoist out of the persistent driver's row loop: everything the
+// row body derives from it (LDS addresses of the passes, swizzles, store offsets) is recomputed per row instead of
+// being kept live in VGPRs across the whole loop, which would leave the body no registers (spills to scratch join
+// the vector-memory queue the driver keeps busy).
+__device__ __forceinline__ int sd_tid() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+// LDS-only workgroup barrier: __syncthreads() would also wait for every outstanding global load and store of
+// the wave, which the persistent driver keeps in flight across the row body on purpose
+__device__ __forceinline__ void sd_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // merge two disjoint candidate sets (their minima a, b): the smaller keeps its payload; a near tie sets
 // the flag.  |a - b| is exact (one binade), +Inf - +Inf is NaN and never flags.
@@ -147,7 +170,7 @@ __device__ __forceinline__ void sd_scan(const uint16_t *list, int nl, const doub
                                         const int *base, double beta, uint16_t *UU, double *outnat, double *redv,
                                         int *redj) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = sd_tid(), lane = tid & 63, w = tid >> 6;
   auto target = [&](int r, int *xl) {
     double t1 = 0.0;
 #pragma unroll
@@ -191,7 +214,7 @@ __device__ __forceinline__ void sd_scan(const uint16_t *list, int nl, const doub
         redj[e * NW + w] = bj;
       }
     }
-    __syncthreads();
+    sd_bar();
     if (tid < nl) {
       double bv = INFINITY;
       int bj = -1;
@@ -292,6 +315,7 @@ struct SdtShared {
   int nsp;   // sparse rows: the finite sources (rank, Ψ)
   int spj[SD_SPARSE];
   double spv[SD_SPARSE];
+  int cnt[2];  // targets sent to the exact scan (near ties, direct rows), flushed to the global counters once
 };
 
 // The sphere orders a step reads (step i+1, for the sources) and writes (step i, for the output row), as the
@@ -318,48 +342,44 @@ __device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restr
   pm.hout = pout[0];
 }
 
-// One source row c' of step i for subproblem k: reads S_{i+1} (Sin), writes row c' of S_i (Sout) and of
-// UU_i.  `loaded` (persistent kernel): flag stored once this row's reads of S_{i+1} are complete.
-template <int M, bool PERSIST>
-__device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int k, int cp,
-                                        int i, const SdPerm &pm, const double *Sin_all,
-                                        double *Sout_all, uint16_t *__restrict__ UU_all, size_t s_stride,
-                                        size_t uu_stride_k, int32_t *__restrict__ counters,
-                                        SdtShared<(1 << (3 * M - 3)) / 64> &sh, unsigned char *sds, int32_t *loaded,
-                                        int token) {
+// One source row c' of step i for subproblem k (the row body shared by both drivers).
+//   v      : Ψ at this thread's eight positions 2(tid + T·q) + {0, 1} of the sphere order of u_old(i+1), i.e.
+//            S_{i+1}[c' - b̃_j(i+1)][pos_{i+1}(j)] (+Inf where that row is below 0); loaded by the caller (the
+//            persistent driver issues these loads one row ahead, so they may still be in flight on entry).
+//   pin    : LDS copy of the sphere order of step i+1 (rank | b̃ << 16 by position), pout: of step i.
+//   mid    : mid.early() once every wave has consumed `v` (the driver publishes `loaded` and issues its dependency
+//            polls without waiting for them); mid() at a uniform point after the last use of `v` and of `pin`,
+//            before the passes: the driver drains the previous row's stores, publishes them, checks the polls and
+//            issues the next row's loads (both no-ops for one launch per step).  mid() returns false when the
+//            launch is being abandoned (a dependency wait timed out).
+// Returns -1 (abandoned), 1 (the row is all +Inf: no target in the trust region or no finite source) or 0.
+// Writes row c' of S_i (sphere order of u_old(i)) and of UU_i: exactly five 16-byte vector-memory stores per
+// thread on every path, the last vector-memory instructions of the row (the persistent driver's counted wait
+// for the next row's loads relies on it).  Every barrier is LDS-only (sd_bar): nothing here waits for the
+// caller's outstanding loads or stores.
+template <int M, bool PERSIST, class Mid>
+__device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int k, int cp,
+                                         int i, double (&v)[8], const uint32_t *pin, const uint32_t *pout,
+                                         double *Sout, uint16_t *UU, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
+                                         unsigned char *sds, Mid &&mid, const double *__restrict__ df_all,
+                                         const double *__restrict__ uo_all) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
   double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
   double *dtv = psi + L;                                // [L] transform values (swizzled), then outputs (natural)
   uint16_t *uu = reinterpret_cast<uint16_t *>(dtv + L);  // [L] the U row (natural order)
   uint16_t *list = uu + L;                              // [SD_LCAP] targets for the exact scan
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = sd_tid(), lane = tid & 63, w = tid >> 6;
   const int B = P.B;
   const double beta = Lv.beta;
-  const double *Sin = Sin_all + (size_t)k * s_stride;
-  double *Sout = Sout_all + (size_t)k * s_stride + (size_t)cp * L;
-  uint16_t *UU = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L) + (size_t)cp * L;
-  const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
-  const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
-  const uint2 *ein = pm.in, *eout = pm.out;
+  // df / u_old of this step (kernel arguments marked __restrict__: uniform scalar loads, which do not join the vector
+  // memory queue the persistent driver keeps busy)
+  const double *dfi = df_all + ((size_t)k * P.nt + i) * M;
+  const double *uoi = uo_all + ((size_t)k * P.nt + i) * M;
   SD_RSTAMP(13);
   SD_STAMP(0);
-
-  // ---- sources: Ψ_j = Φ_{i+1}[j, c'] = S_{i+1}[c' - b̃_j(i+1)][pos_{i+1}(j)]; thread: position pairs
-  // 2(tid + T·q) + {0, 1}, so each wave instruction covers 512 contiguous bytes ----------------------
-  // all loads issue back to back: a row below 0 (no such budget) reads row 0 and is masked after
-  const int sbytes = (B + 1) * L * (int)sizeof(double);
-  double v[8];
+  uint2 ein[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int p2 = 2 * (tid + T * q);
-    const int ra = max(cp - (int)(ein[q].x >> 16), 0), rb = max(cp - (int)(ein[q].y >> 16), 0);
-    sd_load_pair<PERSIST>(Sin, sbytes, ra * L + p2, rb * L + p2 + 1, v[2 * q], v[2 * q + 1]);
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      if ((int)((h ? ein[q].y : ein[q].x) >> 16) > cp) v[2 * q + h] = INFINITY;
+  for (int q = 0; q < 4; ++q) ein[q] = *reinterpret_cast<const uint2 *>(pin + 2 * (tid + T * q));
   // ---- this thread's targets: ranks tid | x << 3(M-1) (the lines of the last pass) -----------------
   double a[M];
   int lb[M], uo[M];
@@ -371,11 +391,9 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
   }
   double pre = 0.0;
   int bpre = 0;
-  int xt[M];
 #pragma unroll
   for (int m = 0; m < M - 1; ++m) {
-    xt[m] = (tid >> (3 * m)) & 7;
-    const int nu = lb[m] + xt[m];
+    const int nu = lb[m] + ((tid >> (3 * m)) & 7);
     pre = pre + a[m] * (double)nu;  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
     bpre += abs(nu - uo[m]);
   }
@@ -411,8 +429,8 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
     sh.rmx[w] = pmx;
     sh.rnv[w] = nv;
   }
-  __syncthreads();  // every load of S_{i+1} has returned (its value is in LDS)
-  if (PERSIST && tid == 0) __hip_atomic_store(loaded, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  sd_bar();  // every wave has consumed its loads of S_{i+1} (their values are in LDS)
+  mid.early();
 #pragma unroll
   for (int q = 0; q < NW; ++q) {
     pmn = fmin(pmn, sh.rmn[q]);
@@ -424,14 +442,8 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
   const int nf = nv >> 16;
   nv &= 0xFFFF;
   SD_STAMP(1);
-  if (nv == 0 || !(pmn < INFINITY)) {  // no target in the trust region, or nothing reachable
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      sd_store16<PERSIST>(Sout, L * 8, 2 * (tid + T * q), 0x7FF0000000000000ull, 0x7FF0000000000000ull);
-    // and the U row: no cell written (0xFFFF), as in the reference, where U keeps nothing for Φ_i = +Inf
-    *reinterpret_cast<ulonglong2 *>(UU + 8 * tid) = make_ulonglong2(~0ull, ~0ull);
-    return;
-  }
+  // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
+  const bool empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || !(pmn < INFINITY))) != 0;  // uniform
 
   // ---- the binade: values base + (Ψ - Ψmin)/β + d lie in [base, 2·base), grid g = 2^13 ulp ----------
   const double inv = Lv.inv_beta;                      // fl(1/β), host-computed
@@ -445,15 +457,15 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
   // 2 × stamping error (< g) + 2 × the reference's rounding (<= 4u·qmax per candidate), in units of β
   const double tol = 3.0 * g + 0x1p-49 * qmax * inv;
   // few finite sources (rows near c' = 0): every target's minimum over them, directly
-  const bool sparse = nf <= SD_SPARSE;
-  const bool direct = !sparse && (nv <= SD_FEW || !scale_ok || !(tol < base * 0x1p-20));
+  const bool sparse = !empty && nf <= SD_SPARSE;
+  const bool direct = !empty && !sparse && (nv <= SD_FEW || !scale_ok || !(tol < base * 0x1p-20));
 
   double o[8];
   int spj[SD_SPARSE];
   double spv[SD_SPARSE];
   if (sparse) {
     if (tid == 0) sh.nsp = 0;
-    __syncthreads();
+    sd_bar();
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -463,13 +475,15 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
           sh.spj[e] = (int)((h ? ein[q].y : ein[q].x) & 0xFFFFu);
           sh.spv[e] = v[2 * q + h];
         }
-    __syncthreads();
+    sd_bar();
 #pragma unroll
     for (int e = 0; e < SD_SPARSE; ++e) {  // uniform: broadcast reads into registers
       spj[e] = sh.spj[e];
       spv[e] = sh.spv[e];
     }
-  } else if (!direct) {
+  }
+  const bool transform = !direct && !empty && !sparse;  // uniform
+  if (transform) {
     // ---- stamp: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) | j --------------------------------------------
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -484,8 +498,12 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
         }
         dtv[sd_swz(j)] = V;
       }
-    __syncthreads();
+    sd_bar();
     SD_STAMP(2);
+  }
+  // `v` and `pin` are dead from here on: the driver may reuse the latter
+  if (!mid()) return -1;
+  if (transform) {
     // ---- M passes: forward and backward sweep along the 8 levels of one dimension, unit step 1.0 -----
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -506,100 +524,143 @@ __device__ __forceinline__ void sdt_row(const ProblemDev &P, const LevelsDev &Lv
 #pragma unroll
         for (int x = 0; x < 8; ++x) dtv[pos[x]] = o[x];
       }
-      __syncthreads();  // last pass: every read of dtv is done before it becomes the output buffer
+      sd_bar();  // last pass: every read of dtv is done before it becomes the output buffer
       SD_STAMP(3 + m);
     }
   }
 
-  // ---- targets: R(l, j*) for a certified winner; the others are listed for the exact scan (their
-  // output slot holds NaN until the scan fills it) ----------------------------------------------------
-  unsigned listed = 0;
-  if (!direct && !sparse) {  // branch-free: the eight winners' Ψ reads issue together
-    int jx[8];
-    double pv[8];
+  if (!empty) {
+    // ---- targets: R(l, j*) for a certified winner; the others are listed for the exact scan (their
+    // output slot holds NaN until the scan fills it) ----------------------------------------------------
+    unsigned listed = 0;
+    if (!direct && !sparse) {  // branch-free: the eight winners' Ψ reads issue together
+      int jx[8];
+      double pv[8];
 #pragma unroll
-    for (int x = 0; x < 8; ++x) jx[x] = __double2loint(o[x]) & (SD_FLAG - 1);  // +Inf carries payload 0
+      for (int x = 0; x < 8; ++x) jx[x] = __double2loint(o[x]) & (SD_FLAG - 1);  // +Inf carries payload 0
 #pragma unroll
-    for (int x = 0; x < 8; ++x) pv[x] = psi[jx[x]];
+      for (int x = 0; x < 8; ++x) pv[x] = psi[jx[x]];
 #pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      const int r = tid | (x << (3 * (M - 1))), j = jx[x];
-      const bool fin = (valid >> x & 1) && o[x] < INFINITY;
-      const bool flg = (__double2loint(o[x]) & SD_FLAG) != 0;
-      const unsigned d = sd_l1(sd_bytes(j), ptid | (unsigned)x << (8 * (M - 1)));
-      const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
-      const double val = (t1 + beta * (double)d) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
-      listed |= (unsigned)(fin && flg) << x;
-      uu[r] = (uint16_t)(fin && !flg ? j : 0xFFFF);  // 0xFFFF: unwritten (Φ = +Inf) or not yet known (listed)
-      dtv[r] = fin ? (flg ? __longlong_as_double(0x7FF8000000000000ll) : val) : INFINITY;
-    }
-  } else {
+      for (int x = 0; x < 8; ++x) {
+        const int r = tid | (x << (3 * (M - 1))), j = jx[x];
+        const bool fin = (valid >> x & 1) && o[x] < INFINITY;
+        const bool flg = (__double2loint(o[x]) & SD_FLAG) != 0;
+        const unsigned d = sd_l1(sd_bytes(j), ptid | (unsigned)x << (8 * (M - 1)));
+        const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
+        const double val = (t1 + beta * (double)d) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
+        listed |= (unsigned)(fin && flg) << x;
+        uu[r] = (uint16_t)(fin && !flg ? j : 0xFFFF);  // 0xFFFF: unwritten (Φ = +Inf) or not yet known (listed)
+        dtv[r] = fin ? (flg ? __longlong_as_double(0x7FF8000000000000ll) : val) : INFINITY;
+      }
+    } else {
 #pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      const int r = tid | (x << (3 * (M - 1)));
-      double ov = INFINITY;
-      int uj = 0xFFFF;  // U cell not written by the reference (Φ = +Inf) or not yet known (listed)
-      if (direct) {
-        listed |= valid & (1u << x);
-      } else if (sparse) {
-        if (valid >> x & 1) {  // the reference loop over the finite sources, ties to the lower rank
-          const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
-          double bv = INFINITY;
-          int bj = 0xFFFF;
+      for (int x = 0; x < 8; ++x) {
+        const int r = tid | (x << (3 * (M - 1)));
+        double ov = INFINITY;
+        int uj = 0xFFFF;  // U cell not written by the reference (Φ = +Inf) or not yet known (listed)
+        if (direct) {
+          listed |= valid & (1u << x);
+        } else {  // sparse: the reference loop over the finite sources, ties to the lower rank
+          if (valid >> x & 1) {
+            const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
+            double bv = INFINITY;
+            int bj = 0xFFFF;
 #pragma unroll
-          for (int e = 0; e < SD_SPARSE; ++e) {
-            if (e < nf) {
-              const int j = spj[e];
-              const unsigned d = sd_l1(sd_bytes(j), ptid | (unsigned)x << (8 * (M - 1)));
-              const double val = (t1 + beta * (double)d) + spv[e];
-              if (val < bv || (val == bv && j < bj)) {
-                bv = val;
-                bj = j;
+            for (int e = 0; e < SD_SPARSE; ++e) {
+              if (e < nf) {
+                const int j = spj[e];
+                const unsigned d = sd_l1(sd_bytes(j), ptid | (unsigned)x << (8 * (M - 1)));
+                const double val = (t1 + beta * (double)d) + spv[e];
+                if (val < bv || (val == bv && j < bj)) {
+                  bv = val;
+                  bj = j;
+                }
               }
             }
+            ov = bv;
+            uj = bj;
           }
-          ov = bv;
-          uj = bj;
         }
+        uu[r] = (uint16_t)uj;
+        dtv[r] = (listed >> x & 1) ? __longlong_as_double(0x7FF8000000000000ll) : ov;
       }
-      uu[r] = (uint16_t)uj;
-      dtv[r] = (listed >> x & 1) ? __longlong_as_double(0x7FF8000000000000ll) : ov;
+    }
+    if (listed) {
+      int e = atomicAdd(&sh.nlist, __popc(listed));
+#pragma unroll
+      for (int x = 0; x < 8; ++x)
+        if (listed >> x & 1) {
+          if (e < SD_LCAP) list[e] = (uint16_t)(tid | (x << (3 * (M - 1))));
+          ++e;
+        }
+    }
+    sd_bar();
+    SD_STAMP(7);
+    const int nl = sh.nlist;
+    if (nl) {
+      if (nl <= SD_COOP)
+        sd_scan<M, true>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
+      else if (nl <= SD_LCAP)
+        sd_scan<M, false>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
+      else
+        sd_scan<M, false>(nullptr, L, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);  // every NaN-marked rank
+      sd_bar();
+      if (tid == 0) sh.cnt[direct ? 1 : 0] += nl;
     }
   }
-  if (listed) {
-    int e = atomicAdd(&sh.nlist, __popc(listed));
+  if (empty) {  // uniform: the row is +Inf, U unwritten -- through LDS, so that the stores below take one path
 #pragma unroll
-    for (int x = 0; x < 8; ++x)
-      if (listed >> x & 1) {
-        if (e < SD_LCAP) list[e] = (uint16_t)(tid | (x << (3 * (M - 1))));
-        ++e;
-      }
-  }
-  __syncthreads();
-  SD_STAMP(7);
-  const int nl = sh.nlist;
-  if (nl) {
-    if (nl <= SD_COOP)
-      sd_scan<M, true>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
-    else if (nl <= SD_LCAP)
-      sd_scan<M, false>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
-    else
-      sd_scan<M, false>(nullptr, L, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);  // every NaN-marked rank
-    __syncthreads();
-    if (tid == 0) atomicAdd(&counters[direct ? 1 : 0], nl);
+    for (int x = 0; x < 8; ++x) dtv[tid | (x << (3 * (M - 1)))] = INFINITY;
+    reinterpret_cast<ulonglong2 *>(uu)[tid] = make_ulonglong2(~0ull, ~0ull);
+    sd_bar();
   }
   SD_STAMP(8);
   // ---- Φ_i row c' in the sphere order of u_old(i), and the U row, both 16 bytes per lane ------------
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    sd_store16<PERSIST>(Sout, L * 8, 2 * (tid + T * q), __double_as_longlong(dtv[eout[q].x & 0xFFFFu]),
-                        __double_as_longlong(dtv[eout[q].y & 0xFFFFu]));
+  for (int q = 0; q < 4; ++q) {
+    const uint2 e = *reinterpret_cast<const uint2 *>(pout + 2 * (tid + T * q));
+    sd_store16<PERSIST>(Sout, L * 8, 2 * (tid + T * q), __double_as_longlong(dtv[e.x & 0xFFFFu]),
+                        __double_as_longlong(dtv[e.y & 0xFFFFu]));
+  }
   {
     const ulonglong2 t = reinterpret_cast<const ulonglong2 *>(uu)[tid];
     *reinterpret_cast<ulonglong2 *>(UU + 8 * tid) = t;  // read by later launches only (backtrack)
   }
   SD_STAMP(9);
   SD_RSTAMP(14);
+  return empty ? 1 : 0;
+}
+
+// Ψ of row c' at step i: S_{i+1}[c' - b̃_j(i+1)][pos] for this thread's eight positions (sphere order `pin` of step
+// i+1, in LDS), +Inf where that row is below 0.  Row 0 comes from `r0` (the persistent driver keeps row 0 of every
+// step in its own array, written before the launch) or, when r0 is null, from the staging block itself.
+// SC1: the persistent driver's hand-off loads (`sc1` buffer loads to registers, MI355X_MICROARCH.md Valid forms).
+template <int M, bool SC1>
+__device__ __forceinline__ void sd_issue_loads(double (&v)[8], const uint32_t *pin, int cp, const double *Sin,
+                                               int sbytes, const double *r0) {
+  constexpr int L = 1 << (3 * M), T = L / 8;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p2 = 2 * (tid + T * q);
+    const uint2 e = *reinterpret_cast<const uint2 *>(pin + 2 * (tid + T * q));
+    const int ra = cp - (int)(e.x >> 16), rb = cp - (int)(e.y >> 16);
+    double va = INFINITY, vb = INFINITY;
+    if (ra == rb && (ra >= 1 || (ra == 0 && !r0))) {  // one 16-byte load (the common case)
+      sd_load_pair<SC1>(Sin, sbytes, ra * L + p2, ra * L + p2 + 1, va, vb);
+    } else {
+      if (ra >= 1 || (ra == 0 && !r0))
+        va = sd_load8<SC1>(Sin, sbytes, ra * L + p2);
+      else if (ra == 0)
+        va = r0[p2];
+      if (rb >= 1 || (rb == 0 && !r0))
+        vb = sd_load8<SC1>(Sin, sbytes, rb * L + p2 + 1);
+      else if (rb == 0)
+        vb = r0[p2 + 1];
+    }
+    v[2 * q] = va;
+    v[2 * q + 1] = vb;
+  }
 }
 
 // The two rows that need no transform (B >= 1):
@@ -767,6 +828,57 @@ __device__ __forceinline__ void sdt_rowB(const ProblemDev &P, const LevelsDev &L
   *reinterpret_cast<ulonglong2 *>(UB + 8 * tid) = make_ulonglong2(sd_pack4(ub), sd_pack4(ub + 4));
 }
 
+// per-step driver: no pipeline hooks
+struct SdMidNone {
+  __device__ __forceinline__ void early() const {}
+  __device__ __forceinline__ bool operator()() const { return true; }
+};
+
+// LDS bytes of the row body: Ψ by rank, the transform / output values, the U row, the scan list, and two
+// sphere-order slots (steps i+1 and i)
+template <int M>
+__host__ __device__ constexpr size_t sd_slot_offset() {  // the two sphere-order slots follow the row body's arrays
+  return ((size_t)1 << (3 * M)) * (2 * sizeof(double) + sizeof(uint16_t)) + SD_LCAP * sizeof(uint16_t);
+}
+size_t sdt_lds_bytes(const PyrGeom &G) {
+  const size_t L = (size_t)1 << (3 * G.M);
+  return (G.M == 4 ? sd_slot_offset<4>() : sd_slot_offset<3>()) + 2 * L * sizeof(uint32_t);
+}
+
+// copy one step's sphere order (L uint32) into an LDS slot with LDS-DMA (1 KiB per wave-instruction, no VGPRs);
+// lands asynchronously (vmcnt), visible to the other waves after their wait and a barrier
+template <int M>
+__device__ __forceinline__ void sd_perm_dma(const uint32_t *src, uint32_t *slot) {
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = wave; c < L * 4 / 1024; c += NW)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void *)((const char *)src + c * 1024 + lane * 16),
+        (__attribute__((address_space(3))) void *)((char *)slot + c * 1024), 16, 0, 0);
+}
+
+// The same copy for the persistent driver, as inline asm: the compiler then does not know these instructions
+// write LDS, and does not make every later LDS atomic wait (vmcnt(0)) for them -- and for the row loads queued
+// behind.  The driver orders them itself: they are issued before the next row's loads and complete under the
+// counted wait at that row's start, and every reader of the slot reads it after a later vmcnt(0) and a barrier.
+template <int M>
+__device__ __forceinline__ void sd_perm_dma_asm(const uint32_t *src, uint32_t *slot) {
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)slot);
+#pragma unroll
+  for (int c = wave; c < L * 4 / 1024; c += NW) {
+    const char *g = (const char *)src + c * 1024 + lane * 16;
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)c * 1024u);
+    unsigned keep;  // M0 is reserved to the compiler: saved and restored around the copy
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(m0)
+                 : "memory");
+  }
+}
+
 // One launch per step: one workgroup per (source row c', subproblem k).
 template <int M>
 __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i,
@@ -775,158 +887,369 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
                                                            double *__restrict__ Sout_all,
                                                            uint16_t *__restrict__ UU_all, size_t s_stride,
                                                            size_t uu_stride_k, int32_t *__restrict__ counters) {
+  constexpr int L = 1 << (3 * M);
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
-  SdPerm pm;
-  sd_perm_load<M>(pm, perm_all, P.nt, (int)blockIdx.y, i);
+  const int k = (int)blockIdx.y, tid = threadIdx.x;
+  if (tid == 0) sh.cnt[0] = sh.cnt[1] = 0;
   // B >= 1: block 0 takes rows 0 and B together, block x the row x (B workgroups, one per CU at B = 256)
   if (blockIdx.x == 0 && P.B >= 1) {
-    sdt_row0<M, false>(P, Lv, (int)blockIdx.y, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k, G.base,
+    SdPerm pm;
+    sd_perm_load<M>(pm, perm_all, P.nt, k, i);
+    sdt_row0<M, false>(P, Lv, k, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k, G.base, nullptr, 0);
+    sdt_rowB<M, false>(P, Lv, k, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k, G.base, counters, sh,
                        nullptr, 0);
-    sdt_rowB<M, false>(P, Lv, (int)blockIdx.y, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k, G.base,
-                       counters, sh, nullptr, 0);
-  } else
-    sdt_row<M, false>(P, Lv, G, (int)blockIdx.y, (int)blockIdx.x, i, pm, Sin_all, Sout_all, UU_all,
-                      s_stride, uu_stride_k, counters, sh, sds, nullptr, 0);
+  } else {
+    const int cp = (int)blockIdx.x;
+    uint32_t *slot = reinterpret_cast<uint32_t *>(sds + sd_slot_offset<M>());
+    sd_perm_dma<M>(perm_all + ((size_t)k * P.nt + i + 1) * L, slot);
+    sd_perm_dma<M>(perm_all + ((size_t)k * P.nt + i) * L, slot + L);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sd_bar();
+    double v[8];
+    sd_issue_loads<M, false>(v, slot, cp, Sin_all + (size_t)k * s_stride, (P.B + 1) * L * (int)sizeof(double),
+                             nullptr);
+    sdt_body<M, false>(P, Lv, G, k, cp, i, v, slot, slot + L, Sout_all + (size_t)k * s_stride + (size_t)cp * L,
+                       UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(P.B + 1) * L) + (size_t)cp * L, sh,
+                       sds, SdMidNone{}, P.df, P.uold);
+    if (tid == 0) {
+      if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
+      if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
+    }
+  }
   SD_FLUSH();
 }
 
-// Persistent: the whole DP in one launch.  Each subproblem's rows 0..B are split into chunks, one per resident
-// workgroup (nwg / K workgroups per subproblem, one per CU; chunks differ by at most one row).  With W = B
-// workgroups (257 rows on 256 CUs), workgroup w >= 1 takes row w and workgroup 0 the two rows that need no
-// transform: row 0 of step i and row B of step i + SD_BLAG.  Row B lags because it reads rows B - Smax .. B
-// of the step before: run in lockstep with row 0 it would close a dependency cycle through every row
-// (row 0 -> row 1 -> ... -> row B -> row 0 of the next step) and hold the whole DP to the hand-off latency
-// of every step; a lag of SD_BLAG steps leaves each row bound by its own body.
-//
-// Row c' of step i reads rows c' - s (s <= Smax) of S_{i+1} and overwrites row c' of the staging buffer
-// i % NB, which held S_{i+NB}, read by rows c' .. c' + Smax at step i+NB-1.  So before a chunk [lo, hi)
-// starts a step, one wave polls (relaxed agent loads, s_sleep)
-//   done[k][lo - s]        >= token(i+1)      for 1 <= s <= min(lo, Smax)           (its inputs are published)
-//   loaded[k][hi - 1 + s]  >= token(i+NB-1)   for 1 <= s <= min(B + 1 - hi, Smax)   (nobody still reads S_{i+NB})
-// with token(i) = nt - 1 - i (0 = nothing yet; the terminal row comes from the previous launch); rows inside
-// the chunk are the workgroup's own, already done in order.  Every wait points at a strictly earlier item in
-// the order (step descending, row ascending; workgroup 0's iteration i between steps i + 1 and i), so with
-// every workgroup resident there is no deadlock; a wait that exceeds its spin bound sets *err and every
-// workgroup leaves.
+// ---- the persistent driver's row 0 ---------------------------------------------------------------------------
+// Row 0 of every step has at most one finite source, j0(i+1) = the level at L1 distance 0 from u_old(i+1), so
+//   S_i[0][pos_i(l)] = Φ_i[l, b̃_l(i)] = fl(fl(T1(l, i) + β·d(l, j0(i+1))) + V(i+1))   (+Inf where b̃_l(i) > B),
+//   V(i) = S_i[0][0] = Φ_i[j0(i), 0], V(nt-1) = T1(j0(nt-1), nt-1), U_i[l, b̃_l(i)] = j0(i+1),
+// (HelpFunctions.jl:29-43, 45-77 restricted to budget row 0).  V is a scalar chain in time: k_sdt_chain folds it
+// once (its additions in the reference's order), k_sdt_row0 expands every step's row 0 into R0[k][i][pos] and its
+// U row, and the persistent kernel's rows 1..28 read row 0 from there instead of waiting for a workgroup.
 template <int M>
-__global__ __launch_bounds__(1 << (3 * M - 3), SDT_RUN_MINW) void k_sdt_run(ProblemDev P, LevelsDev Lv, PyrGeom G,
-                                                          const uint32_t *__restrict__ perm_all, double *S_all,
-                                                          size_t buf_stride, uint16_t *__restrict__ UU_all,
-                                                          size_t s_stride, size_t uu_stride_k,
-                                                          int32_t *__restrict__ counters, int32_t *flags, int nwg,
-                                                          int kint) {
-  constexpr int Smax = 7 * M, NB = kSdtBuffers;
-  extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
-  __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
-  const int R = P.B + 1, nrows = P.K * R, tid = threadIdx.x;
-  int32_t *done = flags, *loaded = flags + nrows, *err = flags + 2 * nrows;
-  // this workgroup's chunk of rows, in every one of its group's kint subproblems (interleaved: while one
-  // subproblem's row hand-off is in flight, the workgroup computes the same row of the next one)
-  const int W = nwg / (P.K / kint);  // workgroups per group of kint subproblems (the host guarantees >= 1)
-  const int kg = (int)blockIdx.x / W, wl = (int)blockIdx.x - kg * W;
-  if (kg * kint >= P.K) return;
-  const int base = R / W, extra = R - base * W;
-  const bool split = W == R - 1 && R >= 2, edges = split && wl == 0;
-  int lo, hi;  // rows [lo, hi), contiguous, the longer chunks highest
-  if (split) {
-    lo = wl;
-    hi = lo + 1;
-  } else {
-    lo = wl * base + max(0, wl - (W - extra));
-    hi = lo + base + (wl >= W - extra ? 1 : 0);
-  }
-  if (tid == 0) sh.stop = 0;
-  auto tok_of = [&](int step) { return P.nt - 1 - step; };
-  auto buf = [&](int step) { return S_all + (size_t)(step % NB) * buf_stride; };
-#pragma nounroll
-  for (int i = P.nt - 2; i >= (edges ? -SD_BLAG : 0); --i) {
-#pragma nounroll
-    for (int kk = 0; kk < kint; ++kk) {
-      const int k = kg * kint + kk;
-      const int iB = i + SD_BLAG;                   // workgroup 0: the step of its row B
-      const bool do0 = i >= 0, doB = edges && iB <= P.nt - 2;
-      const int g = k * R + lo;  // timeline stamps: the chunk's first row
-      (void)g;
-      SdPerm pm, pmB;  // static; SDT_PREFETCH: in flight during the wait (costs VGPRs)
-#if SDT_PREFETCH
-      if (do0) sd_perm_load<M>(pm, perm_all, P.nt, k, i);
-      if (doB) sd_perm_load<M>(pmB, perm_all, P.nt, k, iB);
-#endif
-      SD_TL(0);
-      if (tid < 64) {  // wave 0: dependency wait
-        const int lane = tid;
-        const int s = lane < 32 ? lane + 1 : lane - 31;
-        int32_t *fp = nullptr;
-        int need = 0;
-        // RAW: inputs of row lo at step i (workgroup 0: of row B at step iB)
-        const int rlo = edges ? R - 1 : lo, sraw = edges ? iB : i;
-        // WAR: readers of the buffer row lo .. hi-1 overwrites at step i (workgroup 0: row 0 at step i)
-        const int whi = edges ? 1 : hi;
-        if (lane < 32 && s <= Smax && s <= rlo && (!edges || doB)) {
-          fp = done + k * R + rlo - s;
-          need = tok_of(sraw + 1);
-        } else if (lane >= 32 && s <= Smax && whi - 1 + s < R && do0) {
-          fp = loaded + k * R + whi - 1 + s;
-          need = tok_of(i + NB - 1);
-        }
-        unsigned spins = 0;
-        for (;;) {
-          const bool ok =
-              !fp || need <= 0 || __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
-          if (__all(ok)) break;
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > (1u << 24)) {
-            if (lane == 0) {
-              __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              sh.stop = 1;
-            }
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
+__global__ __launch_bounds__(256) void k_sdt_chain(ProblemDev P, PyrGeom G, double beta,
+                                                  const uint32_t *__restrict__ perm_all, double *__restrict__ V) {
+  constexpr int L = 1 << (3 * M), CH = 2048;
+  __shared__ double av[CH];
+  const int k = (int)blockIdx.x, tid = threadIdx.x, nt = P.nt;
+  const uint32_t *pk = perm_all + (size_t)k * nt * L;
+  double *Vk = V + (size_t)k * nt;
+  auto j0 = [&](int i) { return (int)(pk[(size_t)i * L] & 0xFFFFu); };
+  auto t1 = [&](int r, int i) {  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
+    const double *dfi = P.df + ((size_t)k * nt + i) * M;
+    double t = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) t = t + (P.dt * dfi[m]) * (double)(G.base[m] + ((r >> (3 * m)) & 7));
+    return t;
+  };
+  double run = t1(j0(nt - 1), nt - 1);  // the terminal row (no switching term)
+  if (tid == 0) Vk[nt - 1] = run;
+  for (int hi = nt - 2; hi >= 0; hi -= CH) {  // steps hi, hi-1, ..., lo
+    const int lo = max(0, hi - CH + 1), n = hi - lo + 1;
+    for (int q = tid; q < n; q += blockDim.x) {
+      const int i = hi - q, r = j0(i);
+      const unsigned d = sd_l1(sd_bytes((unsigned)r), sd_bytes((unsigned)j0(i + 1)));
+      av[q] = t1(r, i) + beta * (double)d;  // temp_val_2, HelpFunctions.jl:67
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int q = 0;
+      for (; q + 8 <= n; q += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = av[q + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          run = x[u] + run;  // val = temp_val_2 + Φ_{i+1}, HelpFunctions.jl:71
+          av[q + u] = run;
         }
       }
-      __syncthreads();
-      SD_TL(1);
-      if (sh.stop) return;
-#if !SDT_PREFETCH
-      if (do0) sd_perm_load<M>(pm, perm_all, P.nt, k, i);
-      if (doB) sd_perm_load<M>(pmB, perm_all, P.nt, k, iB);
-#endif
-      if (edges) {
-        if (do0)
-          sdt_row0<M, true>(P, Lv, k, i, pm, buf(i + 1), buf(i), UU_all, s_stride, uu_stride_k, G.base,
-                            loaded + k * R, tok_of(i));
-        if (doB)
-          sdt_rowB<M, true>(P, Lv, k, iB, pmB, buf(iB + 1), buf(iB), UU_all, s_stride, uu_stride_k, G.base,
-                            counters, sh, loaded + k * R + R - 1, tok_of(iB));
-        SD_TL(2);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
-        __syncthreads();
-        if (tid == 0) {
-          if (do0) __hip_atomic_store(done + k * R, tok_of(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (doB)
-            __hip_atomic_store(done + k * R + R - 1, tok_of(iB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        SD_TL(3);
-      }
-#pragma nounroll
-      for (int cp = lo; cp < hi && !edges; ++cp) {
-        sdt_row<M, true>(P, Lv, G, k, cp, i, pm, buf(i + 1), buf(i), UU_all, s_stride, uu_stride_k, counters,
-                         sh, sds, loaded + k * R + cp, tok_of(i));
-        SD_TL(2);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores have landed
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(done + k * R + cp, tok_of(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        SD_TL(3);
+      for (; q < n; ++q) {
+        run = av[q] + run;
+        av[q] = run;
       }
     }
-    if (i == 0) SD_FLUSH();
+    __syncthreads();
+    for (int q = tid; q < n; q += blockDim.x) Vk[hi - q] = av[q];
+    __syncthreads();
   }
 }
 
-size_t sdt_lds_bytes(const PyrGeom &G) {
-  const size_t L = (size_t)1 << (3 * G.M);
-  return L * (2 * sizeof(double) + sizeof(uint16_t)) + SD_LCAP * sizeof(uint16_t);
+template <int M>
+__global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_row0(ProblemDev P, LevelsDev Lv, PyrGeom G,
+                                                            const uint32_t *__restrict__ perm_all,
+                                                            const double *__restrict__ V, double *__restrict__ S_all,
+                                                            size_t kstride, size_t r0off, uint16_t *__restrict__ UU_all,
+                                                            size_t uu_stride_k) {
+  constexpr int L = 1 << (3 * M), T = L / 8;
+  const int i = (int)blockIdx.x, k = (int)blockIdx.y, tid = threadIdx.x, nt = P.nt, B = P.B;
+  const uint32_t *pi = perm_all + ((size_t)k * nt + i) * L;
+  const bool term = i == nt - 1;
+  const int jn = term ? 0 : (int)(perm_all[((size_t)k * nt + i + 1) * L] & 0xFFFFu);  // j0(i+1)
+  const double vn = term ? 0.0 : V[(size_t)k * nt + i + 1];
+  const SdEdge<M> E(P, G.base, k, i);
+  double *reg = S_all + (size_t)k * kstride;
+  double *r0 = reg + r0off + (size_t)i * L;
+  auto val = [&](int r) {
+    const double t = E.t1(r);
+    return term ? t : (t + Lv.beta * (double)SdEdge<M>::dist(r, jn)) + vn;
+  };
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint2 e = *reinterpret_cast<const uint2 *>(pi + 2 * (tid + T * q));
+    const double o0 = (int)(e.x >> 16) > B ? INFINITY : val((int)(e.x & 0xFFFFu));
+    const double o1 = (int)(e.y >> 16) > B ? INFINITY : val((int)(e.y & 0xFFFFu));
+    *reinterpret_cast<double2 *>(r0 + 2 * (tid + T * q)) = make_double2(o0, o1);
+    if (i == 0) *reinterpret_cast<double2 *>(reg + 2 * (tid + T * q)) = make_double2(o0, o1);  // S_0 row 0 (buffer 0)
+  }
+  if (!term) {  // U row 0 of step i, natural order: ranks 8·tid .. 8·tid + 7 (written where Φ_i is finite)
+    unsigned short u0[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const int r = 8 * tid + x;
+      u0[x] = E.bt(r) <= B && val(r) < INFINITY ? (unsigned short)jn : (unsigned short)0xFFFF;
+    }
+    uint16_t *U0 = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L);
+    *reinterpret_cast<ulonglong2 *>(U0 + 8 * tid) = make_ulonglong2(sd_pack4(u0), sd_pack4(u0 + 4));
+  }
+}
+
+// The persistent driver's hand-off loads, branch-free (a divergent load makes the compiler wait for it before
+// the branches join): per position pair one 16-byte `sc1` load at the row of its first element and one 8-byte
+// `sc1` load at the row of its second where the pair straddles a sphere boundary, both through ONE buffer
+// resource spanning the subproblem's staging buffers and its row-0 array; out-of-range offsets (dropped by the
+// hardware) where a row is below 0 or no second load is needed.  `sd_take` selects once the data is in (at the
+// next row's start).
+struct SdRaw {
+  sd_u32x4 a[4];
+  sd_u32x2 b[4];
+  unsigned mask;  // per pair q: bit 3q the first element has no source row, 3q+1 the second, 3q+2 it straddles
+};
+template <int M>
+__device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t rs, const uint32_t *pin, int cp,
+                                              unsigned boff, unsigned r0, const unsigned rowb) {
+  constexpr int L = 1 << (3 * M), T = L / 8;
+  const int tid = sd_tid();
+  unsigned mask = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p2 = 2 * (tid + T * q);
+    const uint2 e = *reinterpret_cast<const uint2 *>(pin + p2);
+    const int ra = cp - (int)(e.x >> 16), rb = cp - (int)(e.y >> 16);
+    // an offset beyond the resource's range drops the access (the load returns 0 without touching memory): rows
+    // below 0, and the second element wherever the pair does not straddle (it came with the first)
+    constexpr unsigned OOB = 0xFFFFFFF0u;
+    const unsigned oa = ra >= 1 ? boff + (unsigned)ra * rowb + (unsigned)p2 * 8u : ra == 0 ? r0 + (unsigned)p2 * 8u : OOB;
+    const unsigned ob = rb == ra ? OOB
+                        : rb >= 1 ? boff + (unsigned)rb * rowb + (unsigned)(p2 + 1) * 8u
+                        : rb == 0 ? r0 + (unsigned)(p2 + 1) * 8u
+                                  : OOB;
+    w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa, 0, 16);
+    w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob, 0, 16);
+    mask |= ((unsigned)(ra < 0) | (unsigned)(rb < 0) << 1 | (unsigned)(ra != rb) << 2) << (3 * q);
+  }
+  w.mask = mask;
+}
+__device__ __forceinline__ void sd_take(double (&v)[8], const SdRaw &w) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const unsigned m = w.mask >> (3 * q);
+    const double a0 = __hiloint2double((int)w.a[q].y, (int)w.a[q].x);
+    const double a1 = __hiloint2double((int)w.a[q].w, (int)w.a[q].z);
+    const double b1 = __hiloint2double((int)w.b[q].y, (int)w.b[q].x);
+    v[2 * q] = (m & 1) ? INFINITY : a0;
+    v[2 * q + 1] = (m & 2) ? INFINITY : (m & 4) ? b1 : a1;
+  }
+}
+
+// ---- the persistent driver --------------------------------------------------------------------------------
+// The whole DP in one launch.  Rows 1..B of subproblem k are split into contiguous chunks [lo, hi), one per
+// resident workgroup (nwg / K per subproblem, one per CU); row 0 comes from R0 (k_sdt_row0).  A workgroup works
+// through its items (row, step) in the order step descending, row ascending, and runs one item ahead:
+//   item n:  wait for its Ψ (issued during item n-1) -> reductions, `loaded` published -> stamp, passes
+//            -> MID: drain item n-1's stores, publish item n-1 `done`; wait until item n+1's inputs are
+//               published (RAW) and nobody still reads what item n overwrites (WAR); issue item n+1's Ψ loads
+//               (and the next step's sphere order, LDS-DMA)
+//            -> certified winners, exact scans -> item n's five stores.
+// So the load latency of a row hides behind the second half of the previous row, the store drain behind the
+// first half of the next, and the row hand-off latency becomes pipeline skew: a row runs behind the rows below
+// it, by about half a step per row, which the NB staging buffers absorb (step i lives in buffer i % NB).
+//
+// Flags (relaxed agent-scope atomics, the measured-valid hand-off of MI355X_MICROARCH.md, Valid forms, row 1 of
+// its table: sc1 stores drained by every storing wave, then ONE lane's sc1 flag store behind a workgroup barrier;
+// one polling wave, sc1 loads of the bytes after the poll matched and a barrier):
+//   done[k][r]   = token(i): row r's stores of step i have landed   (token(i) = nt - 1 - i; 0 = nothing yet)
+//   loaded[k][r] = token(i): row r's loads of S_{i+1} have returned (its WAR guard)
+// Item (r, i) needs done[k][r - s] >= token(i+1) for 1 <= s <= 28, r - s >= 1, outside the chunk, and before
+// writing buffer i % NB, loaded[k][r + s] >= token(i + NB - 1) for 1 <= s <= 28, r + s <= B, outside the chunk.
+// Every wait points at an item of an earlier step, or of the same step and a lower row, so with every workgroup
+// resident nothing deadlocks; a wait beyond spin_limit polls sets *err and every workgroup leaves (the host then
+// redoes the DP with per-step launches: check_run).
+template <int M>
+__global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, LevelsDev Lv, PyrGeom G,
+                                                              const uint32_t *__restrict__ perm_all, double *S_all,
+                                                              size_t kstride, int NB, uint16_t *__restrict__ UU_all,
+                                                              size_t uu_stride_k, int32_t *__restrict__ counters,
+                                                              int32_t *flags, int nwg, unsigned spin_limit,
+                                                              const double *__restrict__ df_all,
+                                                              const double *__restrict__ uo_all) {
+  constexpr int L = 1 << (3 * M);
+  extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
+  __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
+  const int B = P.B, R = B + 1, nt = P.nt, tid = threadIdx.x;
+  int32_t *done = flags, *loaded = flags + P.K * R, *err = flags + 2 * P.K * R;
+  const int W = nwg / P.K;  // workgroups per subproblem (the host guarantees 1 <= W <= B)
+  const int k = (int)blockIdx.x / W, wl = (int)blockIdx.x - k * W;
+  if (k >= P.K) return;
+  const int base = B / W, extra = B - base * W;  // rows 1..B, the longer chunks highest
+  const int lo = 1 + wl * base + max(0, wl - (W - extra)), hi = lo + base + (wl >= W - extra ? 1 : 0);
+  uint32_t *slot = reinterpret_cast<uint32_t *>(sds + sd_slot_offset<M>());
+  double *dtv = reinterpret_cast<double *>(sds) + L;  // the row body's outputs (natural order) after a row
+  auto pslot = [&](int step) { return slot + (step & 1) * L; };  // sphere order of `step`
+  // this subproblem's region: NB staging buffers of R rows, then row 0 of every step (k_sdt_row0); one buffer
+  // resource over all of it (the host checks it is below 4 GiB)
+  double *reg = S_all + (size_t)k * kstride;
+  const unsigned rowb = (unsigned)L * 8u, bufb = (unsigned)R * rowb, r0b = (unsigned)NB * bufb;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(r0b + (unsigned)nt * rowb), 0x00020000);
+  auto boff = [&](int step) { return (unsigned)(step % NB) * bufb; };
+  const uint32_t *pk = perm_all + (size_t)k * nt * L;
+  int32_t *dk = done + k * R, *lk = loaded + k * R;
+  if (tid == 0) {
+    sh.stop = 0;
+    sh.cnt[0] = sh.cnt[1] = 0;
+  }
+  // prologue: both sphere orders of the first step, and the first row's loads (the terminal row was written by an
+  // earlier launch)
+  sd_perm_dma_asm<M>(pk + (size_t)(nt - 1) * L, pslot(nt - 1));
+  sd_perm_dma_asm<M>(pk + (size_t)(nt - 2) * L, pslot(nt - 2));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  sd_bar();
+  SdRaw raw;
+  sd_issue_pipe<M>(raw, rs, pslot(nt - 1), lo, boff(nt - 1), r0b + (unsigned)(nt - 1) * rowb, rowb);
+  // a wait the compiler sees (vmcnt(0), other counters untouched): entering the loop with these loads pending would
+  // make it assume, at the loop head, that nothing younger can be outstanding, and wait for every store there
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  int pcp = -1, pi = 0;  // the previous row, whose `done` is published at this row's mid point
+  int32_t *pfp;           // wave 0's dependency polls (Mid::early / Mid::operator())
+  int pneed, pval;
+  int status = 0;         // the previous row's sdt_body result: 1 = its outputs are all +Inf
+#pragma nounroll
+  for (int i = nt - 2; i >= 0 && status >= 0; --i) {
+#pragma nounroll
+    for (int cp = lo; cp < hi && status >= 0; ++cp) {
+      const bool last_row = cp + 1 == hi;
+      const int ncp = last_row ? lo : cp + 1, ni = last_row ? i - 1 : i;  // the next row
+      const bool has_next = ni >= 0;
+      const int g = k * R + cp;  // timeline stamps
+      (void)g;
+      SD_TL(0);
+      double v[8];
+      sd_take(v, raw);
+      // one row per workgroup: its sphere-0 source (position 0, the level at distance 0 from u_old(i+1)) is this
+      // workgroup's own output of the previous row, still in LDS (the loaded copy predates it)
+      if (hi - lo == 1 && pcp >= 0 && tid == 0)
+        v[0] = status == 1 ? INFINITY : dtv[pslot(i + 1)[0] & 0xFFFFu];
+      struct Mid {
+        int &pcp, &pi;
+        SdRaw &raw;
+        int32_t *dk, *lk, *err;
+        int cp, i, ncp, ni, lo, hi, B, NB, nt;
+        unsigned spin_limit, rowb, bufb, r0b;
+        bool has_next;
+        SdtShared<(1 << (3 * M - 3)) / 64> &sh;
+        const uint32_t *pk;
+        uint32_t *slot;
+        __amdgpu_buffer_rsrc_t rs;
+        int g;
+        // wave 0: this lane's dependency flag (a flag that always passes where it has none), the token it needs and
+        // the polled value -- kernel-scope variables, never re-initialised in the loop: a fresh value here would be
+        // a write to the register the last poll loaded into, and the compiler would wait for every store first
+        int32_t *&fp;
+        int &need, &val;
+        // loads of this row consumed: publish `loaded`; wave 0 issues its dependency polls (lanes 0-31 RAW for the
+        // next row, 32-63 WAR for this row's stores), results checked at the mid point
+        __device__ __forceinline__ void early() {
+          SD_TL_AT(g, i, nt, 1);
+          const int tid = threadIdx.x;
+          if (tid == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (tid < 64) {
+            const int lane = tid, s = lane < 32 ? lane + 1 : lane - 31;
+            fp = lk + cp;  // no dependency: any value passes
+            need = INT32_MIN;
+            if (lane < 32) {
+              const int r = ncp - s;
+              if (has_next && s <= 7 * M && r >= 1 && r < lo && nt - 2 - ni > 0) {
+                fp = dk + r;
+                need = nt - 2 - ni;  // token(ni + 1)
+              }
+            } else {
+              const int r = cp + s;
+              if (s <= 7 * M && r <= B && r >= hi && nt - i - NB > 0) {
+                fp = lk + r;
+                need = nt - i - NB;  // token(i + NB - 1)
+              }
+            }
+            val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every lane: no branch
+          }
+        }
+        __device__ __forceinline__ bool operator()() {
+          const int tid = threadIdx.x;
+          SD_TL_AT(g, i, nt, 2);
+          // the previous row's stores (every wave's) have landed: publish them
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          sd_bar();
+          SD_TL_AT(g, i, nt, 3);
+          if (tid < 64) {
+            const int lane = tid;
+            // evaluated before the flag store below: the compiler's wait for `val` would otherwise cover that store
+            bool ready = __all(val >= need);
+            if (lane == 0 && pcp >= 0)
+              __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned spins = 0;
+            for (;;) {
+              if (ready) break;
+              if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
+                if (lane == 0) {
+                  __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  sh.stop = 1;
+                }
+                break;
+              }
+              __builtin_amdgcn_s_sleep(1);
+              val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              ready = __all(val >= need);
+            }
+          }
+          sd_bar();
+          SD_TL_AT(g, i, nt, 4);
+          if (sh.stop) return false;
+          pcp = cp;
+          pi = i;
+          if (has_next) {
+            // every wave is past its last read of this row's input sphere order (the slot of step i+1): the next
+            // step's order may land there (LDS-DMA, before the next row's loads, so that the counted wait at the
+            // next row's start covers it too)
+            if (ni != i) sd_perm_dma_asm<M>(pk + (size_t)ni * (1 << (3 * M)), slot + (ni & 1) * (1 << (3 * M)));
+            sd_issue_pipe<M>(raw, rs, slot + ((ni + 1) & 1) * (1 << (3 * M)), ncp, (unsigned)((ni + 1) % NB) * bufb,
+                             r0b + (unsigned)(ni + 1) * rowb, rowb);
+          }
+          SD_TL_AT(g, i, nt, 5);
+          return true;
+        }
+      } mid{pcp, pi, raw, dk, lk, err, cp, i, ncp, ni, lo, hi, B, NB, nt, spin_limit, rowb, bufb, r0b, has_next, sh,
+            pk, slot, rs, g, pfp, pneed, pval};
+      status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, pslot(i + 1), pslot(i), reg + (size_t)(i % NB) * R * L +
+                                 (size_t)cp * L, UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) +
+                                 (size_t)cp * L, sh, sds, mid, df_all, uo_all);
+      SD_TL(6);
+    }
+  }
+  if (tid == 0) {
+    if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
+    if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
+  }
+  SD_FLUSH();
 }
 
 bool sdt_supported(const PyrGeom &G) {
@@ -936,15 +1259,32 @@ bool sdt_supported(const PyrGeom &G) {
   return true;
 }
 
+hipError_t launch_sdt_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
+                           const uint32_t *perm, double *V, double *S, size_t kstride, size_t r0off, uint16_t *UU,
+                           size_t uu_stride_k) {
+  if (!sdt_supported(G)) return hipErrorInvalidValue;
+  if (G.M == 4) {
+    hipLaunchKernelGGL(k_sdt_chain<4>, dim3(P.K), dim3(256), 0, s, P, G, Lv.beta, perm, V);
+    hipLaunchKernelGGL(k_sdt_row0<4>, dim3(P.nt, P.K), dim3(512), 0, s, P, Lv, G, perm, (const double *)V, S, kstride,
+                       r0off, UU, uu_stride_k);
+  } else {
+    hipLaunchKernelGGL(k_sdt_chain<3>, dim3(P.K), dim3(256), 0, s, P, G, Lv.beta, perm, V);
+    hipLaunchKernelGGL(k_sdt_row0<3>, dim3(P.nt, P.K), dim3(64), 0, s, P, Lv, G, perm, (const double *)V, S, kstride,
+                       r0off, UU, uu_stride_k);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
-                          const uint32_t *perm, double *S, size_t buf_stride, uint16_t *UU, size_t s_stride,
-                          size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, int kint, size_t lds) {
+                          const uint32_t *perm, double *S, size_t kstride, int NB, uint16_t *UU, size_t uu_stride_k,
+                          int32_t *counters, int32_t *flags, int nwg, unsigned spin_limit, size_t lds) {
   if (!sdt_supported(G)) return hipErrorInvalidValue;
   // cooperative launch: the runtime checks at launch time that every workgroup can be resident at once (the
   // row hand-off spins on other workgroups), and refuses the launch otherwise (hipErrorCooperativeLaunchTooLarge)
-  void *args[] = {(void *)&P, (void *)&Lv, (void *)&G, (void *)&perm, (void *)&S, (void *)&buf_stride, (void *)&UU,
-                  (void *)&s_stride, (void *)&uu_stride_k, (void *)&counters, (void *)&flags, (void *)&nwg,
-                  (void *)&kint};
+  void *args[] = {(void *)&P,     (void *)&Lv,       (void *)&G,         (void *)&perm,
+                  (void *)&S,     (void *)&kstride,  (void *)&NB,        (void *)&UU,
+                  (void *)&uu_stride_k, (void *)&counters, (void *)&flags, (void *)&nwg, (void *)&spin_limit,
+                  (void *)&P.df,  (void *)&P.uold};
   if (G.M == 4)
     return hipLaunchCooperativeKernel((const void *)k_sdt_run<4>, dim3(nwg), dim3(512), args, (unsigned)lds, s);
   return hipLaunchCooperativeKernel((const void *)k_sdt_run<3>, dim3(nwg), dim3(64), args, (unsigned)lds, s);
@@ -974,7 +1314,7 @@ hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
 
 #if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
 extern "C" int32_t mioc_debug_sdt_timeline(unsigned long long *out, int64_t nrows) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sdt_tl), (size_t)nrows * 64 * 4 * sizeof(unsigned long long)) ==
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sdt_tl), (size_t)nrows * 64 * 8 * sizeof(unsigned long long)) ==
                  hipSuccess
              ? 0
              : -4;

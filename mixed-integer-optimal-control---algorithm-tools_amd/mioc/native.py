@@ -5,9 +5,12 @@ visible, every entry point raises ``MiocNativeError``.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import math
 import os
+import sys
+import weakref
 
 import numpy as np
 
@@ -27,6 +30,7 @@ MIOC_ENONFINITE = -7
 
 MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
 MIOC_OPT_ALGO, MIOC_OPT_TIMING, MIOC_OPT_PERSIST, MIOC_OPT_PRED_FMA = 1, 2, 3, 4
+MIOC_OPT_SPIN_LIMIT, MIOC_OPT_SDT_BUFFERS = 5, 6
 MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID, MIOC_ALGO_SEPARABLE = 0, 1, 2, 3, 4
 MIOC_ALGO_FUSED, MIOC_ALGO_FUSED_SEPARABLE = 5, 6
 MIOC_ODE_FISHING, MIOC_ODE_DOUBLETANK, MIOC_ODE_VANDERPOL = 1, 2, 3
@@ -141,10 +145,29 @@ def cost_spec(p, L=None, levels=None):
     return MIOC_P_TABLE, 1, np.ascontiguousarray((d.sum(axis=2) ** (1.0 / float(p))).reshape(-1))
 
 
+_LIVE = weakref.WeakSet()  # contexts not yet closed
+
+
+@atexit.register
+def _close_live_contexts():
+    """Destroy every context still open while the HIP runtime is alive: atexit handlers run before the C
+    runtime's exit() tears down libamdhip64's static state, whereas a __del__ reached during interpreter
+    finalisation (or from a garbage cycle collected then) can run after it ('What's weak' 5)."""
+    for c in list(_LIVE):
+        try:
+            c.close()
+        except Exception:
+            pass
+
+
 class Context:
-    """One device context: levels + cost + the resident DP (fronts / argmin table / class tables)."""
+    """One device context: levels + cost + the resident DP (fronts / argmin table / class tables).
+
+    Close it explicitly (``close()`` or ``with Context(0) as ctx:``); contexts left open are closed by an atexit
+    handler, never from ``__del__`` during interpreter shutdown."""
 
     def __init__(self, device=0):
+        self.h = None
         self.lib = load_library()
         h = ctypes.c_void_p()
         rc = self.lib.mioc_create(int(device), ctypes.byref(h))
@@ -155,13 +178,26 @@ class Context:
         self.M = None
         self.nt = None
         self.B = None
+        _LIVE.add(self)
 
     def close(self):
         if self.h:
-            self.lib.mioc_destroy(self.h)
-            self.h = None
+            h, self.h = self.h, None
+            _LIVE.discard(self)
+            self.lib.mioc_destroy(h)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     def __del__(self):
+        # an unreferenced context is destroyed while the program runs; at shutdown the atexit handler has
+        # already closed it, and a HIP call from a finaliser that runs after the runtime's teardown is unsafe
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

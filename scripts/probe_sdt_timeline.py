@@ -1,74 +1,70 @@
-"""Persistent separable-transform kernel timeline (diagnostic build libmioc_stamps_tl.so, make stamps_tl): per row and step
-(i < 64) the dependency-wait begin/end, row-body end and done publish (s_memrealtime, 100 MHz), plus the
-in-row phase clocks of the last processed row (s_memtime)."""
-import ctypes, os, sys
+"""Timeline of the pipelined persistent separable-transform kernel (diagnostic build libmioc_stamps_tl.so, `make
+stamps_tl`): for every row and the 64 steps from nt/2 down, s_memrealtime (100 MHz) at 8 points of the row body:
+0 start, 1 loads consumed, 2 mid point, 3 previous row drained, 4 next row's inputs ready, 5 next row's loads issued,
+6 stores issued.  Prints the phase durations, the step period and the pipeline skew between neighbouring rows.
+Usage: python scripts/probe_sdt_timeline.py [nt] [NB]"""
+import ctypes
+import os
+import sys
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")
 os.environ["MIOC_LIB"] = os.path.join(PKG, "lib", "libmioc_stamps_tl.so")
-sys.path.insert(0, PKG); sys.path.insert(0, ROOT)
-import numpy as np
-from mioc import native
-from mioc.synth import CONFIGS, make_inputs
-nt = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+from mioc import native  # noqa: E402
+from mioc.synth import CONFIGS, make_inputs  # noqa: E402
+
+nt = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+nb = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 cfg = CONFIGS["C4"]
 lt, df, uo = make_inputs(cfg, nt=nt)
-ctx = native.Context(0); ctx.set_levels(lt); ctx.set_cost(1, cfg.beta)
-ctx.set_option(native.MIOC_OPT_ALGO, native.MIOC_ALGO_SEPARABLE)
-ctx.set_option(native.MIOC_OPT_TIMING, 1)
-ctx.set_option(native.MIOC_OPT_PERSIST, 1)
-ctx.bellman(df, uo, cfg.B, cfg.dt)  # warm-up: code object load, first-touch of the buffers
-ctx.synchronize()
-ctx.reset_stats()
-ctx.bellman(df, uo, cfg.B, cfg.dt)
-ctx.synchronize()
-ms, n, name = ctx.kernel_stats(0)
-print(f"{name}: {ms:.3f} ms for {nt - 1} steps = {1e3 * ms / (nt - 1):.2f} us/step")
-nb = cfg.B + 1
-lib = native.load_library()
-f = lib.mioc_debug_sdt_timeline; f.argtypes = [ctypes.c_void_p, ctypes.c_int64]; f.restype = ctypes.c_int32
-buf = (ctypes.c_ulonglong * (nb * 64 * 4))()
-assert f(buf, nb) == 0
-tl = np.array(buf, dtype=np.int64).reshape(nb, 64, 4)
-steps = range(2, 62)
-t0 = tl[:, 2:62, :][tl[:, 2:62, :] > 0].min()
-W = (tl[:, steps, 1] - tl[:, steps, 0]) / 100.0   # us waiting
-Bd = (tl[:, steps, 2] - tl[:, steps, 1]) / 100.0  # us row body
-Pu = (tl[:, steps, 3] - tl[:, steps, 2]) / 100.0  # us drain + publish
-print("per row-step (us): wait median %.2f p90 %.2f | body median %.2f p90 %.2f max %.2f | drain+publish median %.2f p90 %.2f"
-      % (np.median(W), np.percentile(W, 90), np.median(Bd), np.percentile(Bd, 90), Bd.max(), np.median(Pu), np.percentile(Pu, 90)))
-# step period: time between consecutive done publishes of the same row
-per = -np.diff(tl[:, steps, 3], axis=1) / 100.0
-print("step period per row (us): median %.2f p10 %.2f p90 %.2f" % (np.median(per), np.percentile(per, 10), np.percentile(per, 90)))
-# critical chain: done(row) at step i vs the latest done among its sources at step i+1
-lag = []
-for i in range(2, 61):
-    for c in range(nb):
-        src = tl[max(0, c - 28):c + 1, i + 1, 3]
-        lag.append((tl[c, i, 1] - src.max()) / 100.0)
-lag = np.array(lag)
-print("hand-off latency (latest source done -> wait end) us: median %.2f p90 %.2f" % (np.median(lag), np.percentile(lag, 90)))
-body_by_row = np.median(Bd, axis=1)
-print("slowest rows by median body (row, us):", sorted([(int(r), round(float(body_by_row[r]), 2)) for r in range(nb)], key=lambda t: -t[1])[:6])
-print("diagnostics", ctx.diagnostics())
-# which dependency gates each row: RAW (rows c'-28..c'-1 of step i+1 done) vs WAR (rows c'+1..c'+28 of
-# step i+2 past their loads; approximated by their wait end + 3 us) vs the workgroup's own previous row
-raw_gap, war_gap, by_row = [], [], np.zeros(nb)
-for c in range(nb):
-    g = []
-    for i in range(2, 60):
-        raw = tl[max(0, c - 28):c, i + 1, 3].max() if c > 0 else 0
-        war = tl[c + 1:c + 29, i + 2, 1].max() if c + 1 < nb else 0
-        g.append((tl[c, i, 1] - raw) / 100.0)
-        war_gap.append((tl[c, i, 1] - war) / 100.0)
-    by_row[c] = np.median(g)
-    raw_gap += g
-raw_gap, war_gap = np.array(raw_gap), np.array(war_gap)
-print("wait end - latest RAW done (us): median %.2f p10 %.2f p90 %.2f" % (np.median(raw_gap), np.percentile(raw_gap, 10), np.percentile(raw_gap, 90)))
-print("wait end - latest WAR wait end at i+2 (us): median %.2f p10 %.2f p90 %.2f" % (np.median(war_gap), np.percentile(war_gap, 10), np.percentile(war_gap, 90)))
-print("median (wait end - RAW done) by row, every 8th row:", [round(float(x), 2) for x in by_row[::8]])
-st = tl[:, 10, 1] / 100.0
-print("step 10 wait end relative to row 0 (us), every 8th row:", [round(float(x), 2) for x in (st - st[0])[::8]])
-ref = tl[0, 14, 0]
-for c in (0, 1, 2, 28, 29, 128, 227, 228, 255, 256):
-    print(f"row {c:3d} steps 14..10 [wait begin, wait end, body end, done] us rel.:",
-          [[round((int(x) - int(ref)) / 100.0, 2) for x in tl[c, i]] for i in range(14, 9, -1)])
+with native.Context(0) as ctx:
+    ctx.set_levels(lt)
+    ctx.set_cost(1, cfg.beta)
+    ctx.set_option(native.MIOC_OPT_ALGO, native.MIOC_ALGO_SEPARABLE)
+    ctx.set_option(native.MIOC_OPT_TIMING, 1)
+    ctx.set_option(native.MIOC_OPT_PERSIST, 1)
+    ctx.set_option(native.MIOC_OPT_SDT_BUFFERS, nb)
+    ctx.bellman(df, uo, cfg.B, cfg.dt)  # warm-up: code object load, first touch of the buffers
+    ctx.synchronize()
+    ctx.reset_stats()
+    ctx.bellman(df, uo, cfg.B, cfg.dt)
+    ctx.synchronize()
+    ms, n, name = ctx.kernel_stats(0)
+    print(f"{name}: {ms:.3f} ms for {nt - 1} steps = {1e3 * ms / (nt - 1):.3f} us/step (NB={nb}); "
+          f"diagnostics {ctx.diagnostics()}")
+    R = cfg.B + 1
+    lib = native.load_library()
+    f = lib.mioc_debug_sdt_timeline
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    f.restype = ctypes.c_int32
+    buf = (ctypes.c_ulonglong * (R * 64 * 8))()
+    assert f(buf, R) == 0
+tl = np.array(buf, dtype=np.int64).reshape(R, 64, 8).astype(np.float64) / 100.0  # us
+if len(sys.argv) > 3:
+    np.save(sys.argv[3], tl)
+rows = np.arange(1, R)  # row 0 has no workgroup
+steps = np.arange(2, 62)
+T = tl[rows][:, steps, :]
+ok = np.all(T[:, :, :7] > 0, axis=2)
+names = ["loads consumed + reductions (0->1)", "stamp + passes (1->2)", "drain previous row (2->3)",
+         "poll next inputs (3->4)", "issue next loads (4->5)", "winners + scans + stores (5->6)"]
+for q, nm in enumerate(names):
+    d = (T[:, :, q + 1] - T[:, :, q])[ok]
+    print(f"{nm:36s} median {np.median(d):6.3f}  p10 {np.percentile(d, 10):6.3f}  p90 {np.percentile(d, 90):6.3f} us")
+# period: start of step i-1 minus start of step i, same row (steps descend with the index here)
+per = (T[:, 1:, 0] - T[:, :-1, 0])
+print(f"step period per row: median {np.median(per):.3f}  p10 {np.percentile(per, 10):.3f}  p90 "
+      f"{np.percentile(per, 90):.3f} us")
+rest = (T[:, 1:, 0] - T[:, :-1, 6])
+print(f"stores issued -> next row start: median {np.median(rest):.3f} us")
+skew = T[1:, :, 0] - T[:-1, :, 0]  # row c starts step i this long after row c-1
+print(f"skew row c vs row c-1 (same step start): median {np.median(skew):.3f}  p10 {np.percentile(skew, 10):.3f}  "
+      f"p90 {np.percentile(skew, 90):.3f} us; total over rows 1..{R - 1}: {np.median(T[-1, :, 0] - T[0, :, 0]):.1f} us")
+by_row = np.median(T[:, :, 4] - T[:, :, 3], axis=1)
+print("poll wait by row (median, every 16th row):", [round(float(x), 3) for x in by_row[::16]])
+ld = np.median(T[:, :, 1] - T[:, :, 0], axis=1)
+print("load wait by row (median, every 16th row):", [round(float(x), 3) for x in ld[::16]])

@@ -1,5 +1,6 @@
-"""GPU parity of the batched ODE gradient producer: mioc_ode_eval_device against the host mirror
-of julia_opt/ODEObjective.jl:125-184 with the fishing / doubletank / vanderpol hooks (mioc/ode.py).
+"""GPU parity of the batched ODE gradient producer: mioc_ode_eval_device against the scalar oracle
+oracle/ode_oracle.py (ODEObjective.jl:125-184 with the fishing / doubletank / vanderpol hooks, pinned by the reference's
+own finite-difference test_df) and against the product's host mirror (mioc/ode.py).
 
 Bar: J and df within 1e-12 relative of the mirror (the mirror's numpy small dot / matvec may round in another
 order or through BLAS; the device sums left to right without FMA), and a whole batched trust-region iteration
@@ -44,13 +45,44 @@ def test_ode_eval_vs_host_mirror(name, prob, nt):
     ctx.ode_eval_tensors(prob, dx, obj.T0, obj.T1, J, df)
     ctx.synchronize()
     J, df = J.cpu().numpy(), df.cpu().numpy()
-    exact = 0
+    from oracle.ode_oracle import ODEOracle
+    o = ODEOracle(name, nt)
+    exact = exact_o = 0
     for k in range(K):
         assert abs(J[k] - Jh[k]) <= 1e-12 * abs(Jh[k]), (k, J[k], Jh[k])
         d, h = df[k].T, dfh[k]
         assert np.max(np.abs(d - h)) <= 1e-12 * max(1e-300, np.max(np.abs(h))), k
         exact += int(J[k] == Jh[k]) + int(np.array_equal(d, h))
-    print(f"{name}: {exact} of {2 * K} J / df arrays bit-identical to the host mirror")
+        Jo, dfo = o.eval_df([tuple(c) for c in xs[k].T])
+        dfo = np.array(dfo).T
+        assert abs(J[k] - Jo) <= 1e-12 * abs(Jo), (k, J[k], Jo)
+        assert np.max(np.abs(d - dfo)) <= 1e-12 * max(1e-300, np.max(np.abs(dfo))), k
+        exact_o += int(J[k] == Jo) + int(np.array_equal(d, dfo))
+    print(f"{name}: {exact} of {2 * K} J / df arrays bit-identical to the host mirror, {exact_o} to the oracle")
+    ctx.close()
+
+
+def test_ode_eval_j_only_after_smaller_gradient_call():
+    """A J-only call with more restarts / steps than an earlier gradient call (the forward states are stored for
+    every restart either way, so the context's state buffer must grow for both: ADVICE r2)."""
+    import torch
+    from oracle.ode_oracle import ODEOracle
+    ctx = native.Context(0)
+    obj = _obj("fishing", 64)
+    x1 = torch.tensor(np.ascontiguousarray(np.stack([mioc.rand_func(obj, rng=k).T for k in range(4)])),
+                      dtype=torch.float64, device="cuda")
+    ctx.ode_eval_tensors(native.MIOC_ODE_FISHING, x1, obj.T0, obj.T1, None, torch.empty_like(x1))
+    nt, K = 512, 1024
+    o = ODEOracle("fishing", nt)
+    big = _obj("fishing", nt)
+    xs = [mioc.rand_func(big, rng=1000 + k) for k in range(K)]
+    x2 = torch.tensor(np.ascontiguousarray(np.stack([x.T for x in xs])), dtype=torch.float64, device="cuda")
+    J = torch.empty(K, dtype=torch.float64, device="cuda")
+    ctx.ode_eval_tensors(native.MIOC_ODE_FISHING, x2, big.T0, big.T1, J, None)
+    ctx.synchronize()
+    for k in (0, 517, K - 1):
+        Jo = o.eval_f([tuple(c) for c in xs[k].T])
+        assert abs(J[k].item() - Jo) <= 1e-12 * abs(Jo), k
     ctx.close()
 
 
