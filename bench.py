@@ -5,7 +5,8 @@ independent subproblems (default 1), each a full bellman_TRM! (DP over nt=65536 
 x B+1=257 budget rows) followed by eval_u_TRM! (backtrack), inputs already resident in HBM.
 
 Alongside the headline it measures the batch config C5 (`batch`: `--batch-size` random restarts of the
-36-level heat-shaped subproblem per GPU, the fused small-state DP) and the p=Inf variant of C4.
+36-level heat-shaped subproblem per GPU, the fused small-state DP), the same config at a fixed total
+(`batch_strong`: `--batch-total` restarts split over the ranks, strong scaling) and the p=Inf variant of C4.
 
 Multi-GPU: `python bench.py --gpus N` launches N ranks itself (one process per GPU, before anything
 touches a GPU); under torchrun it uses the given RANK / WORLD_SIZE.  The problem descriptor is broadcast
@@ -52,10 +53,16 @@ def parse(argv=None):
     ap.add_argument("--config", default="C4")
     ap.add_argument("--p", default=None, help="override p: 1 or inf")
     ap.add_argument("--batch", type=int, default=1, help="subproblems per rank per step (headline config)")
+    ap.add_argument("--total", type=int, default=0,
+                    help="headline config: subproblems per step in total, split over the ranks (strong scaling; "
+                         "default 0: --batch per rank, weak scaling)")
     ap.add_argument("--nt", type=int, default=None, help="truncate nt (profiling passes only; not a bench line)")
     ap.add_argument("--variant", default="pinf", help="extra p=Inf line on the same config ('' or none to skip)")
     ap.add_argument("--batch-config", default="C5", help="the batch line's config ('none' to skip)")
     ap.add_argument("--batch-size", type=int, default=1024, help="batch line: subproblems per rank per step")
+    ap.add_argument("--batch-total", type=int, default=1024,
+                    help="strong-scaling batch line (batch_strong): this many subproblems per step in total, split "
+                         "over the ranks (0 to skip)")
     ap.add_argument("--pinf-batch-config", default="C2",
                     help="the p=Inf batch line's config (the reference's main() runs C1-C3 at p=Inf; 'none' to skip)")
     ap.add_argument("--heat-restarts", type=int, default=4096,
@@ -186,8 +193,9 @@ class OracleSolver:
 
 
 # ------------------------------------------------------------------------------------------------------
-def run(args, cfg_name, K, p_over, nt_over, rank, world, device, dist, torch, steps, warmup):
-    """One config: `steps` timed + `warmup` untimed steps, each a global batch of world*K subproblems."""
+def run(args, cfg_name, K, p_over, nt_over, rank, world, device, dist, torch, steps, warmup, total=None):
+    """One config: `steps` timed + `warmup` untimed steps, each a global batch of world*K subproblems (weak
+    scaling), or of `total` subproblems split over the ranks (strong scaling)."""
     from mioc.batch import gather_results, shard
     from mioc.synth import CONFIGS, make_inputs
 
@@ -209,10 +217,11 @@ def run(args, cfg_name, K, p_over, nt_over, rank, world, device, dist, torch, st
     solver = (NativeSolver if args.solver == "native" else OracleSolver)(device, levels, p, beta, torch)
     nsets = warmup + steps
     dfs, uos = [], []
-    lo, hi = shard(world * K, world, rank)  # this rank's contiguous block of each step's global batch
+    G = world * K if total is None else total  # each step's global batch
+    lo, hi = shard(G, world, rank)  # this rank's contiguous block of it
     for s in range(nsets):
         for b in range(lo, hi):
-            _, df, uo = make_inputs(cfg, k=s * world * K + b, nt=nt, levels=levels)
+            _, df, uo = make_inputs(cfg, k=s * G + b, nt=nt, levels=levels)
             dfs.append(df)
             uos.append(uo)
     solver.load(dfs, uos, nsets, hi - lo, levels.M)
@@ -222,7 +231,7 @@ def run(args, cfg_name, K, p_over, nt_over, rank, world, device, dist, torch, st
         solver.solve(s, B, dt)
         if world > 1:  # controls as level ranks (uint16 payload) + Φ*, gathered to rank 0 over RCCL
             r, ph = solver.results()
-            gathered.append(gather_results(dist, r, ph, world * K, world, rank))
+            gathered.append(gather_results(dist, r, ph, G, world, rank))
 
     for s in range(warmup):
         step(s)
@@ -242,8 +251,8 @@ def run(args, cfg_name, K, p_over, nt_over, rank, world, device, dist, torch, st
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    res = dict(config=cfg_name, elapsed=elapsed, K=K, nt=nt, B=B, p=p, levels=levels, uo=uos[-1], steps=steps,
-               world=world)
+    res = dict(config=cfg_name, elapsed=elapsed, K=hi - lo, G=G, nt=nt, B=B, p=p, levels=levels, uo=uos[-1],
+               steps=steps, world=world)
     if world > 1 and rank == 0:
         R, PH = gathered[-1]
         res["gathered_checksum"] = float(PH.double().sum().item()) + float(R.double().sum().item())
@@ -565,22 +574,23 @@ def main():
             dist.init_process_group("gloo")
     device = local
     res = run(args, args.config, args.batch, args.p, args.nt, rank, world, device, dist, torch, args.steps,
-              args.warmup)
+              args.warmup, total=args.total or None)
     variant = batch = None
     if args.variant == "pinf" and args.p is None and args.nt is None and math.isfinite(res["p"]):
         r2 = run(args, args.config, args.batch, "inf", None, rank, world, device, dist, torch,
                  max(args.steps, 3), args.warmup)
         roof2, valu2 = roofline_of(r2)
-        variant = {"p": "inf", "value": round(world * r2["K"] * r2["steps"] / r2["elapsed"], 6),
+        variant = {"p": "inf", "value": round(r2["G"] * r2["steps"] / r2["elapsed"], 6),
                    "unit": "subproblems/s", "ms_per_step": round(1e3 * r2["elapsed"] / r2["steps"], 3),
                    "algorithm": native_name(r2["algo"]), "roofline": roof2, "roofline_valu": valu2,
                    "backtrack_ms": round(r2["walk_ms"] / max(1, r2["steps"]), 3)}
-    def batch_line(cfg_name):
+    def batch_line(cfg_name, total=None):
         r3 = run(args, cfg_name, args.batch_size, None, None, rank, world, device, dist, torch,
-                 max(args.steps, 3), args.warmup)
-        line = {"config": {"workload": workload(r3), "parallelism": f"dp{world} (independent restarts)"},
-                "value": round(world * r3["K"] * r3["steps"] / r3["elapsed"], 3), "unit": "subproblems/s",
-                "n_gpus": world, "scaling": "weak", "steps": r3["steps"],
+                 max(args.steps, 3), args.warmup, total=total)
+        line = {"config": {"workload": workload(r3), "parallelism": f"dp{world} (independent restarts)",
+                           "global_batch": r3["G"], "per_rank": r3["K"]},
+                "value": round(r3["G"] * r3["steps"] / r3["elapsed"], 3), "unit": "subproblems/s",
+                "n_gpus": world, "scaling": "weak" if total is None else "strong", "steps": r3["steps"],
                 "ms_per_step": round(1e3 * r3["elapsed"] / r3["steps"], 3),
                 "algorithm": {native_name(r3["algo"]): r3["dom_name"]},
                 "checksum": r3.get("gathered_checksum")}
@@ -599,10 +609,17 @@ def main():
         heat = heat_line(args, rank, world, device, dist, torch)
     if args.batch_config not in ("", "none") and args.nt is None:
         batch = batch_line(args.batch_config)
+    strong = None
+    if args.batch_total > 0 and args.batch_config not in ("", "none") and args.nt is None:
+        if batch is not None and world == 1 and args.batch_total == args.batch_size:
+            strong = dict(batch, scaling="strong")  # one rank: the same workload as the weak line
+        else:  # fixed total work split over the ranks (C5 x 1024 on 8 GPUs: 128 restarts per GPU)
+            strong = batch_line(args.batch_config, total=args.batch_total)
+            strong.pop("cpu_baseline", None)
     if args.pinf_batch_config not in ("", "none") and args.nt is None:
         batch_pinf = batch_line(args.pinf_batch_config)
     if rank == 0:
-        value = world * res["K"] * args.steps / res["elapsed"]
+        value = res["G"] * args.steps / res["elapsed"]
         out = {
             "metric": METRIC,
             "value": round(value, 6),
@@ -612,7 +629,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * res["elapsed"] / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.total else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded N(0,1) df, rand_func_int-shaped u_old; SURVEY §8 d)",
@@ -631,6 +648,8 @@ def main():
             out["variant_p_inf"] = variant
         if batch:
             out["batch"] = batch
+        if strong:
+            out["batch_strong"] = strong
         if batch_pinf:
             out["batch_p_inf"] = batch_pinf
         if heat:

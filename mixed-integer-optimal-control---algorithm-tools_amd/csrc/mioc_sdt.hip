@@ -47,6 +47,9 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_RUN_MINW
 #define SDT_RUN_MINW 2                   // persistent kernel: waves per SIMD the registers must allow (4: two workgroups per CU, but the row code then spills)
 #endif
+#ifndef SDT_PASS_SPLIT
+#define SDT_PASS_SPLIT 0                 // passes as two independent half-chains + a combine (experiment)
+#endif
 #ifndef SDT_PREFETCH
 #define SDT_PREFETCH 1                   // load the sphere orders ahead of the dependency wait
 #endif
@@ -75,18 +78,29 @@ __device__ unsigned long long g_sdt_stamps[4096][16];
 #define SD_TL_AT(gg, ii, ntt, k) \
   do {                           \
   } while (0)
+#define SD_TL_FLUSH(gg) \
+  do {                  \
+  } while (0)
 #elif defined(MIOC_STAMPS)
-// persistent-kernel timeline (diagnostic build, make stamps_tl): per row g and for the 64 steps from nt/2 down,
-// s_memrealtime (100 MHz) at 8 points of a row: 0 start, 1 its loads consumed (after the first barrier), 2 mid
-// point reached, 3 previous row drained, 4 next row's inputs ready (poll done), 5 next row's loads issued, 6 stores
-// issued
+// persistent-kernel timeline (diagnostic build, make stamps_tl): per workgroup (its chunk's first row) and for the 64
+// steps from nt/2 down, s_memrealtime (100 MHz) at 7 points of a row: 0 start, 1 loads consumed (h.early), 2 drain
+// point, 3 after the drain barrier, 4 polls matched, 5 the next row's loads and DMAs issued, 6 stores issued.  Kept
+// in LDS during the launch (a global store would join the vector-memory queue the driver counts) and copied out at
+// the end.
 __device__ unsigned long long g_sdt_tl[4096][64][8];
+__shared__ unsigned long long sd_tl_lds[64][8];
 #define SD_TL_AT(gg, ii, ntt, k)                                                                          \
   do {                                                                                                    \
     if (threadIdx.x == 0 && (gg) < 4096 && (unsigned)((ii) - ((ntt) >> 1)) < 64u)                          \
-      g_sdt_tl[gg][(ii) - ((ntt) >> 1)][k] = __builtin_amdgcn_s_memrealtime();                             \
+      sd_tl_lds[(ii) - ((ntt) >> 1)][k] = __builtin_amdgcn_s_memrealtime();                                \
   } while (0)
 #define SD_TL(k) SD_TL_AT(g, i, P.nt, k)
+#define SD_TL_FLUSH(gg)                                                                                   \
+  do {                                                                                                    \
+    if (threadIdx.x == 0 && (gg) < 4096)                                                                  \
+      for (int _j = 0; _j < 64; ++_j)                                                                     \
+        for (int _q = 0; _q < 8; ++_q) g_sdt_tl[gg][_j][_q] = sd_tl_lds[_j][_q];                           \
+  } while (0)
 #define SD_STAMP(k) \
   do {              \
   } while (0)
@@ -102,6 +116,9 @@ __device__ unsigned long long g_sdt_tl[4096][64][8];
   } while (0)
 #define SD_TL_AT(gg, ii, ntt, k) \
   do {                           \
+  } while (0)
+#define SD_TL_FLUSH(gg) \
+  do {                  \
   } while (0)
 #define SD_STAMP(k) \
   do {              \
@@ -141,6 +158,33 @@ __device__ __forceinline__ double sd_merge(double a, double b, double tol) {
   const double m = sd_min(a, b);
   const bool close = fabs(a - b) <= tol;
   return __hiloint2double(__double2hiint(m), __double2loint(m) | (close ? SD_FLAG : 0));
+}
+
+// Wave-wide reductions through DPP (no LDS round trip, unlike __shfl_xor's ds_bpermute): four steps leave every
+// lane with its 16-lane row's result (quad_perm xor 1, xor 2, row_half_mirror, row_mirror), then the four row
+// results are read as scalars.
+template <int CTRL>
+__device__ __forceinline__ int sd_dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double sd_dpp_d(double x) {
+  return __hiloint2double(sd_dpp_i<CTRL>(__double2hiint(x)), sd_dpp_i<CTRL>(__double2loint(x)));
+}
+__device__ __forceinline__ double sd_rdl(double x, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l), __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+__device__ __forceinline__ void sd_wave_stats(double &mn, double &mx, int &n) {
+#define SD_STEP(C)                             \
+  mn = fmin(mn, sd_dpp_d<C>(mn));              \
+  mx = fmax(mx, sd_dpp_d<C>(mx));              \
+  n += sd_dpp_i<C>(n);
+  SD_STEP(0xB1) SD_STEP(0x4E) SD_STEP(0x141) SD_STEP(0x140)
+#undef SD_STEP
+  mn = fmin(fmin(sd_rdl(mn, 0), sd_rdl(mn, 16)), fmin(sd_rdl(mn, 32), sd_rdl(mn, 48)));
+  mx = fmax(fmax(sd_rdl(mx, 0), sd_rdl(mx, 16)), fmax(sd_rdl(mx, 32), sd_rdl(mx, 48)));
+  n = (__builtin_amdgcn_readlane(n, 0) + __builtin_amdgcn_readlane(n, 16)) +
+      (__builtin_amdgcn_readlane(n, 32) + __builtin_amdgcn_readlane(n, 48));
 }
 
 // LDS position of rank r (3 bits per dimension): XOR swizzle so that each 32-lane half of a pass reads
@@ -318,6 +362,15 @@ struct SdtShared {
   int cnt[2];  // targets sent to the exact scan (near ties, direct rows), flushed to the global counters once
 };
 
+template <int M>
+__host__ __device__ constexpr size_t sd_slot_offset() {  // the two sphere-order slots follow the row body's arrays
+  return ((size_t)1 << (3 * M)) * (2 * sizeof(double) + sizeof(uint16_t)) + SD_LCAP * sizeof(uint16_t);
+}
+template <int M>
+__host__ __device__ constexpr size_t sd_dfuo_offset() {  // then df(:, i), u_old(:, i) per wave (persistent driver)
+  return sd_slot_offset<M>() + 2 * ((size_t)1 << (3 * M)) * sizeof(uint32_t);
+}
+
 // The sphere orders a step reads (step i+1, for the sources) and writes (step i, for the output row), as the
 // position pairs 2(tid + T·q) + {0, 1} of this thread, plus both heads (position 0).  Loaded at the start of
 // a row (per-step kernel) or ahead of the dependency wait (persistent kernel): they are static, so their
@@ -347,21 +400,22 @@ __device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restr
 //            S_{i+1}[c' - b̃_j(i+1)][pos_{i+1}(j)] (+Inf where that row is below 0); loaded by the caller (the
 //            persistent driver issues these loads one row ahead, so they may still be in flight on entry).
 //   pin    : LDS copy of the sphere order of step i+1 (rank | b̃ << 16 by position), pout: of step i.
-//   mid    : mid.early() once every wave has consumed `v` (the driver publishes `loaded` and issues its dependency
-//            polls without waiting for them); mid() at a uniform point after the last use of `v` and of `pin`,
-//            before the passes: the driver drains the previous row's stores, publishes them, checks the polls and
-//            issues the next row's loads (both no-ops for one launch per step).  mid() returns false when the
-//            launch is being abandoned (a dependency wait timed out).
-// Returns -1 (abandoned), 1 (the row is all +Inf: no target in the trust region or no finite source) or 0.
+//   h      : the driver's pipeline hooks (no-ops for one launch per step): h.early() once every wave has consumed
+//            `v` (publish `loaded`, issue this wave's dependency polls without waiting); h.drain() right before the
+//            first barrier after the last use of `v` and `pin` (this wave's stores of the previous row have landed);
+//            h.go() after that barrier (publish the previous row, check the polls, issue the next row's loads, the
+//            next step's sphere order and df / u_old).  A timed-out wait sets sh.stop, which the driver reads after
+//            the row.
+// Returns 1 if the row is all +Inf (no target in the trust region or no finite source), else 0.
 // Writes row c' of S_i (sphere order of u_old(i)) and of UU_i: exactly five 16-byte vector-memory stores per
 // thread on every path, the last vector-memory instructions of the row (the persistent driver's counted wait
 // for the next row's loads relies on it).  Every barrier is LDS-only (sd_bar): nothing here waits for the
 // caller's outstanding loads or stores.
-template <int M, bool PERSIST, class Mid>
+template <int M, bool PERSIST, class Hooks>
 __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int k, int cp,
                                          int i, double (&v)[8], const uint32_t *pin, const uint32_t *pout,
                                          double *Sout, uint16_t *UU, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
-                                         unsigned char *sds, Mid &&mid, const double *__restrict__ df_all,
+                                         unsigned char *sds, Hooks &h, const double *__restrict__ df_all,
                                          const double *__restrict__ uo_all) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
   double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
@@ -371,10 +425,11 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   const int tid = sd_tid(), lane = tid & 63, w = tid >> 6;
   const int B = P.B;
   const double beta = Lv.beta;
-  // df / u_old of this step (kernel arguments marked __restrict__: uniform scalar loads, which do not join the vector
-  // memory queue the persistent driver keeps busy)
-  const double *dfi = df_all + ((size_t)k * P.nt + i) * M;
-  const double *uoi = uo_all + ((size_t)k * P.nt + i) * M;
+  // df / u_old of this step: the persistent driver has copied them into this wave's LDS words (LDS-DMA issued one
+  // row ahead: a global load here would cost a memory round trip per row); the per-step driver reads them directly
+  const double *dfi = PERSIST ? reinterpret_cast<const double *>(sds + sd_dfuo_offset<M>()) + 2 * M * (threadIdx.x >> 6)
+                              : df_all + ((size_t)k * P.nt + i) * M;
+  const double *uoi = PERSIST ? dfi + M : uo_all + ((size_t)k * P.nt + i) * M;
   SD_RSTAMP(13);
   SD_STAMP(0);
   uint2 ein[4];
@@ -418,19 +473,14 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   int nv = __popc(valid);  // targets in the trust region (low 16 bits) + finite sources (high 16 bits)
 #pragma unroll
   for (int q = 0; q < 8; ++q) nv += (v[q] < INFINITY) << 16;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    pmn = fmin(pmn, __shfl_xor(pmn, off));
-    pmx = fmax(pmx, __shfl_xor(pmx, off));
-    nv += __shfl_xor(nv, off);
-  }
+  sd_wave_stats(pmn, pmx, nv);
   if (lane == 0) {
     sh.rmn[w] = pmn;
     sh.rmx[w] = pmx;
     sh.rnv[w] = nv;
   }
   sd_bar();  // every wave has consumed its loads of S_{i+1} (their values are in LDS)
-  mid.early();
+  h.early();
 #pragma unroll
   for (int q = 0; q < NW; ++q) {
     pmn = fmin(pmn, sh.rmn[q]);
@@ -498,11 +548,15 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
         }
         dtv[sd_swz(j)] = V;
       }
+    h.drain();
     sd_bar();
     SD_STAMP(2);
+  } else {
+    h.drain();
+    sd_bar();
   }
   // `v` and `pin` are dead from here on: the driver may reuse the latter
-  if (!mid()) return -1;
+  h.go();
   if (transform) {
     // ---- M passes: forward and backward sweep along the 8 levels of one dimension, unit step 1.0 -----
 #pragma unroll
@@ -510,9 +564,26 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       int pos[8];
 #pragma unroll
       for (int x = 0; x < 8; ++x) {
-        pos[x] = sd_swz(sd_rank(tid, m, x));
+        pos[x] = sd_swz(sd_rank((int)threadIdx.x, m, x));  // tid-only: hoisted out of the row loop
         o[x] = dtv[pos[x]];
       }
+#if SDT_PASS_SPLIT
+      // two independent chains (prefix f over sources <= x, strict suffix b over sources > x: disjoint candidate
+      // sets), then one merge per point: half the dependency depth of the in-place sweeps, 20 merges instead of 14
+      {
+        double f[8], b[8];
+        f[0] = o[0];
+        b[7] = o[7];
+#pragma unroll
+        for (int x = 1; x < 8; ++x) {
+          f[x] = sd_merge(o[x], f[x - 1] + 1.0, tol);
+          if (x < 7) b[7 - x] = sd_merge(o[7 - x], b[8 - x] + 1.0, tol);
+        }
+#pragma unroll
+        for (int x = 0; x < 7; ++x) o[x] = sd_merge(f[x], b[x + 1] + 1.0, tol);
+        o[7] = f[7];
+      }
+#else
       // in place: after the forward sweep o[x] covers the sources at <= x; a backward merge of o[x] with
       // o[x+1] + 1 compares a source at <= x with itself shifted by >= 2, never within tol, so every
       // flagged tie is between two distinct sources (as in a merge of disjoint sets)
@@ -520,6 +591,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       for (int x = 1; x < 8; ++x) o[x] = sd_merge(o[x], o[x - 1] + 1.0, tol);
 #pragma unroll
       for (int x = 6; x >= 0; --x) o[x] = sd_merge(o[x], o[x + 1] + 1.0, tol);
+#endif
       if (m + 1 < M) {
 #pragma unroll
         for (int x = 0; x < 8; ++x) dtv[pos[x]] = o[x];
@@ -829,20 +901,16 @@ __device__ __forceinline__ void sdt_rowB(const ProblemDev &P, const LevelsDev &L
 }
 
 // per-step driver: no pipeline hooks
-struct SdMidNone {
-  __device__ __forceinline__ void early() const {}
-  __device__ __forceinline__ bool operator()() const { return true; }
+struct SdHooksNone {
+  __device__ __forceinline__ void early() {}
+  __device__ __forceinline__ void drain() {}
+  __device__ __forceinline__ void go() {}
 };
 
 // LDS bytes of the row body: Ψ by rank, the transform / output values, the U row, the scan list, and two
 // sphere-order slots (steps i+1 and i)
-template <int M>
-__host__ __device__ constexpr size_t sd_slot_offset() {  // the two sphere-order slots follow the row body's arrays
-  return ((size_t)1 << (3 * M)) * (2 * sizeof(double) + sizeof(uint16_t)) + SD_LCAP * sizeof(uint16_t);
-}
 size_t sdt_lds_bytes(const PyrGeom &G) {
-  const size_t L = (size_t)1 << (3 * G.M);
-  return (G.M == 4 ? sd_slot_offset<4>() : sd_slot_offset<3>()) + 2 * L * sizeof(uint32_t);
+  return G.M == 4 ? sd_dfuo_offset<4>() + 2 * 4 * sizeof(double) * 8 : sd_dfuo_offset<3>() + 2 * 3 * sizeof(double);
 }
 
 // copy one step's sphere order (L uint32) into an LDS slot with LDS-DMA (1 KiB per wave-instruction, no VGPRs);
@@ -879,6 +947,24 @@ __device__ __forceinline__ void sd_perm_dma_asm(const uint32_t *src, uint32_t *s
   }
 }
 
+// df(:, i) and u_old(:, i) (M doubles each) into this wave's LDS words: lanes 0..4M-1 move one dword each
+// (global_load_lds_dword, LDS-DMA, inline asm for the same reason as sd_perm_dma_asm)
+template <int M>
+__device__ __forceinline__ void sd_dfuo_dma(const double *df, const double *uo, unsigned char *sds) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane < 4 * M) {
+    const char *g = lane < 2 * M ? (const char *)df + 4 * lane : (const char *)uo + 4 * (lane - 2 * M);
+    const unsigned lds0 =
+        (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)(sds + sd_dfuo_offset<M>())) + wave * 16u * M;
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(lds0);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(m0)
+                 : "memory");
+  }
+}
+
 // One launch per step: one workgroup per (source row c', subproblem k).
 template <int M>
 __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i,
@@ -909,9 +995,10 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
     double v[8];
     sd_issue_loads<M, false>(v, slot, cp, Sin_all + (size_t)k * s_stride, (P.B + 1) * L * (int)sizeof(double),
                              nullptr);
+    SdHooksNone hooks;
     sdt_body<M, false>(P, Lv, G, k, cp, i, v, slot, slot + L, Sout_all + (size_t)k * s_stride + (size_t)cp * L,
                        UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(P.B + 1) * L) + (size_t)cp * L, sh,
-                       sds, SdMidNone{}, P.df, P.uold);
+                       sds, hooks, P.df, P.uold);
     if (tid == 0) {
       if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
       if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
@@ -924,6 +1011,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
 // Row 0 of every step has at most one finite source, j0(i+1) = the level at L1 distance 0 from u_old(i+1), so
 //   S_i[0][pos_i(l)] = Φ_i[l, b̃_l(i)] = fl(fl(T1(l, i) + β·d(l, j0(i+1))) + V(i+1))   (+Inf where b̃_l(i) > B),
 //   V(i) = S_i[0][0] = Φ_i[j0(i), 0], V(nt-1) = T1(j0(nt-1), nt-1), U_i[l, b̃_l(i)] = j0(i+1),
+// with V(i) = +Inf where u_old(i) is off the level grid (no level at distance 0),
 // (HelpFunctions.jl:29-43, 45-77 restricted to budget row 0).  V is a scalar chain in time: k_sdt_chain folds it
 // once (its additions in the reference's order), k_sdt_row0 expands every step's row 0 into R0[k][i][pos] and its
 // U row, and the persistent kernel's rows 1..28 read row 0 from there instead of waiting for a workgroup.
@@ -936,6 +1024,9 @@ __global__ __launch_bounds__(256) void k_sdt_chain(ProblemDev P, PyrGeom G, doub
   const uint32_t *pk = perm_all + (size_t)k * nt * L;
   double *Vk = V + (size_t)k * nt;
   auto j0 = [&](int i) { return (int)(pk[(size_t)i * L] & 0xFFFFu); };
+  // Φ_i[j0(i), 0] exists only where u_old(i) is a level (the head at distance 0); an off-grid u_old(i) leaves
+  // budget row 0 empty at step i, and then at every earlier step (+Inf propagates through the additions)
+  auto on_grid = [&](int i) { return (pk[(size_t)i * L] >> 16) == 0u; };
   auto t1 = [&](int r, int i) {  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
     const double *dfi = P.df + ((size_t)k * nt + i) * M;
     double t = 0.0;
@@ -943,14 +1034,14 @@ __global__ __launch_bounds__(256) void k_sdt_chain(ProblemDev P, PyrGeom G, doub
     for (int m = 0; m < M; ++m) t = t + (P.dt * dfi[m]) * (double)(G.base[m] + ((r >> (3 * m)) & 7));
     return t;
   };
-  double run = t1(j0(nt - 1), nt - 1);  // the terminal row (no switching term)
+  double run = on_grid(nt - 1) ? t1(j0(nt - 1), nt - 1) : INFINITY;  // the terminal row (no switching term)
   if (tid == 0) Vk[nt - 1] = run;
   for (int hi = nt - 2; hi >= 0; hi -= CH) {  // steps hi, hi-1, ..., lo
     const int lo = max(0, hi - CH + 1), n = hi - lo + 1;
     for (int q = tid; q < n; q += blockDim.x) {
       const int i = hi - q, r = j0(i);
       const unsigned d = sd_l1(sd_bytes((unsigned)r), sd_bytes((unsigned)j0(i + 1)));
-      av[q] = t1(r, i) + beta * (double)d;  // temp_val_2, HelpFunctions.jl:67
+      av[q] = on_grid(i) ? t1(r, i) + beta * (double)d : INFINITY;  // temp_val_2, HelpFunctions.jl:67
     }
     __syncthreads();
     if (tid == 0) {
@@ -1030,24 +1121,29 @@ template <int M>
 __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t rs, const uint32_t *pin, int cp,
                                               unsigned boff, unsigned r0, const unsigned rowb) {
   constexpr int L = 1 << (3 * M), T = L / 8;
-  const int tid = sd_tid();
-  unsigned mask = 0;
+  const int tid = threadIdx.x;
+  uint2 e[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) e[q] = *reinterpret_cast<const uint2 *>(pin + 2 * (tid + T * q));  // reads first
+  // an offset beyond the resource's range drops the access (the load returns 0 without touching memory): rows
+  // below 0, and the second element wherever the pair does not straddle (it came with the first)
+  constexpr unsigned OOB = 0xFFFFFFF0u;
+  unsigned oa[4], ob[4], mask = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int p2 = 2 * (tid + T * q);
-    const uint2 e = *reinterpret_cast<const uint2 *>(pin + p2);
-    const int ra = cp - (int)(e.x >> 16), rb = cp - (int)(e.y >> 16);
-    // an offset beyond the resource's range drops the access (the load returns 0 without touching memory): rows
-    // below 0, and the second element wherever the pair does not straddle (it came with the first)
-    constexpr unsigned OOB = 0xFFFFFFF0u;
-    const unsigned oa = ra >= 1 ? boff + (unsigned)ra * rowb + (unsigned)p2 * 8u : ra == 0 ? r0 + (unsigned)p2 * 8u : OOB;
-    const unsigned ob = rb == ra ? OOB
-                        : rb >= 1 ? boff + (unsigned)rb * rowb + (unsigned)(p2 + 1) * 8u
-                        : rb == 0 ? r0 + (unsigned)(p2 + 1) * 8u
-                                  : OOB;
-    w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa, 0, 16);
-    w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob, 0, 16);
+    const int ra = cp - (int)(e[q].x >> 16), rb = cp - (int)(e[q].y >> 16);
+    oa[q] = ra >= 1 ? boff + (unsigned)ra * rowb + (unsigned)p2 * 8u : ra == 0 ? r0 + (unsigned)p2 * 8u : OOB;
+    ob[q] = rb == ra ? OOB
+            : rb >= 1 ? boff + (unsigned)rb * rowb + (unsigned)(p2 + 1) * 8u
+            : rb == 0 ? r0 + (unsigned)(p2 + 1) * 8u
+                      : OOB;
     mask |= ((unsigned)(ra < 0) | (unsigned)(rb < 0) << 1 | (unsigned)(ra != rb) << 2) << (3 * q);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa[q], 0, 16);
+    w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob[q], 0, 16);
   }
   w.mask = mask;
 }
@@ -1086,6 +1182,97 @@ __device__ __forceinline__ void sd_take(double (&v)[8], const SdRaw &w) {
 // Every wait points at an item of an earlier step, or of the same step and a lower row, so with every workgroup
 // resident nothing deadlocks; a wait beyond spin_limit polls sets *err and every workgroup leaves (the host then
 // redoes the DP with per-step launches: check_run).
+// The pipeline hooks of the persistent driver (the row body calls them, see sdt_body).
+template <int M>
+struct SdPipe {
+  static constexpr int L = 1 << (3 * M);
+  // the current row (cp, step i) and the next one (ncp, step ni)
+  int cp, i, ncp, ni;
+  bool has_next;
+  // constants of the launch
+  int lo, hi, B, NB, nt, k, g0;
+  unsigned spin_limit, rowb, bufb, r0b;
+  int32_t *dk, *lk, *err;
+  const uint32_t *pk;
+  uint32_t *slot;
+  __amdgpu_buffer_rsrc_t rs;
+  const double *dfa, *uoa;
+  unsigned char *sds;
+  SdtShared<(1 << (3 * M - 3)) / 64> *sh;
+  // carried from row to row: the previous row (its `done` is published at this row's go()), this wave's polls, the
+  // next row's loads in flight
+  int pcp, pi;
+  int32_t *fp;
+  int need, val;
+  SdRaw raw;
+
+  // this row's loads have been consumed by every wave: publish `loaded`; every wave polls its own dependency flags
+  // (lanes 0-31 RAW for the next row, 32-63 WAR for this row's stores; a lane without one polls a flag that always
+  // passes -- every lane loads, no branch), checked in go()
+  __device__ __forceinline__ void early() {
+    SD_TL_AT(g0, i, nt, 1);
+    const int tid = threadIdx.x, lane = tid & 63, s = lane < 32 ? lane + 1 : lane - 31;
+    if (tid == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fp = lk + cp;
+    need = INT32_MIN;
+    if (lane < 32) {
+      const int r = ncp - s;
+      if (has_next && s <= 7 * M && r >= 1 && r < lo && nt - 2 - ni > 0) {
+        fp = dk + r;
+        need = nt - 2 - ni;  // token(ni + 1)
+      }
+    } else {
+      const int r = cp + s;
+      if (s <= 7 * M && r <= B && r >= hi && nt - i - NB > 0) {
+        fp = lk + r;
+        need = nt - i - NB;  // token(i + NB - 1)
+      }
+    }
+    val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // every wave, right before a barrier: its stores of the previous row (and its polls) have landed
+  __device__ __forceinline__ void drain() {
+    SD_TL_AT(g0, i, nt, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  // after that barrier: publish the previous row; this wave waits until its polls match (re-polling), then issues
+  // the first quarter of the next row's loads -- the measured-valid consumer form: the polling wave loads only
+  // after its own poll matched
+  __device__ __forceinline__ void go() {
+    SD_TL_AT(g0, i, nt, 3);
+    const int tid = threadIdx.x;
+    // evaluated before the flag store below: the compiler's wait for `val` would otherwise cover that store
+    bool ready = __all(val >= need);
+    if (tid == 0 && pcp >= 0) __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (!ready) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
+        if ((tid & 63) == 0) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sh->stop = 1;  // read by the driver after the row's next barrier: the launch is abandoned
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ready = __all(val >= need);
+    }
+    SD_TL_AT(g0, i, nt, 4);
+    pcp = cp;
+    pi = i;
+    // the next row's loads; then (LDS-DMA, after them so that they do not wait for it) the next step's sphere order
+    // into the slot of step i+1 (every wave is past its last read of it: the drain barrier) and the next row's df /
+    // u_old; all of it is older than this row's five stores, so the counted wait at the next row's start covers it
+    if (has_next) {
+      sd_issue_pipe<M>(raw, rs, slot + ((ni + 1) & 1) * L, ncp, (unsigned)((ni + 1) % NB) * bufb,
+                       r0b + (unsigned)(ni + 1) * rowb, rowb);
+      if (ni != i) sd_perm_dma_asm<M>(pk + (size_t)ni * L, slot + (ni & 1) * L);
+      sd_dfuo_dma<M>(dfa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + ni) * M, sds);
+    }
+    SD_TL_AT(g0, i, nt, 5);
+  }
+};
+
 template <int M>
 __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, LevelsDev Lv, PyrGeom G,
                                                               const uint32_t *__restrict__ perm_all, double *S_all,
@@ -1110,139 +1297,60 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   // this subproblem's region: NB staging buffers of R rows, then row 0 of every step (k_sdt_row0); one buffer
   // resource over all of it (the host checks it is below 4 GiB)
   double *reg = S_all + (size_t)k * kstride;
-  const unsigned rowb = (unsigned)L * 8u, bufb = (unsigned)R * rowb, r0b = (unsigned)NB * bufb;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(r0b + (unsigned)nt * rowb), 0x00020000);
-  auto boff = [&](int step) { return (unsigned)(step % NB) * bufb; };
-  const uint32_t *pk = perm_all + (size_t)k * nt * L;
-  int32_t *dk = done + k * R, *lk = loaded + k * R;
+  SdPipe<M> h;
+  h.lo = lo, h.hi = hi, h.B = B, h.NB = NB, h.nt = nt, h.k = k, h.g0 = k * R + lo;
+  h.spin_limit = spin_limit, h.rowb = (unsigned)L * 8u, h.bufb = (unsigned)R * h.rowb, h.r0b = (unsigned)NB * h.bufb;
+  h.dk = done + k * R, h.lk = loaded + k * R, h.err = err;
+  h.pk = perm_all + (size_t)k * nt * L, h.slot = slot;
+  h.rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(h.r0b + (unsigned)nt * h.rowb), 0x00020000);
+  h.dfa = df_all, h.uoa = uo_all, h.sds = sds, h.sh = &sh;
+  h.pcp = -1, h.pi = 0;
   if (tid == 0) {
     sh.stop = 0;
     sh.cnt[0] = sh.cnt[1] = 0;
   }
-  // prologue: both sphere orders of the first step, and the first row's loads (the terminal row was written by an
-  // earlier launch)
-  sd_perm_dma_asm<M>(pk + (size_t)(nt - 1) * L, pslot(nt - 1));
-  sd_perm_dma_asm<M>(pk + (size_t)(nt - 2) * L, pslot(nt - 2));
+  // prologue: both sphere orders of the first step, df / u_old, and the first row's loads (the terminal row was
+  // written by an earlier launch)
+  sd_perm_dma_asm<M>(h.pk + (size_t)(nt - 1) * L, pslot(nt - 1));
+  sd_perm_dma_asm<M>(h.pk + (size_t)(nt - 2) * L, pslot(nt - 2));
+  sd_dfuo_dma<M>(df_all + ((size_t)k * nt + nt - 2) * M, uo_all + ((size_t)k * nt + nt - 2) * M, sds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   sd_bar();
-  SdRaw raw;
-  sd_issue_pipe<M>(raw, rs, pslot(nt - 1), lo, boff(nt - 1), r0b + (unsigned)(nt - 1) * rowb, rowb);
+  sd_issue_pipe<M>(h.raw, h.rs, pslot(nt - 1), lo, (unsigned)((nt - 1) % NB) * h.bufb, h.r0b + (unsigned)(nt - 1) * h.rowb,
+                   h.rowb);
   // a wait the compiler sees (vmcnt(0), other counters untouched): entering the loop with these loads pending would
   // make it assume, at the loop head, that nothing younger can be outstanding, and wait for every store there
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  int pcp = -1, pi = 0;  // the previous row, whose `done` is published at this row's mid point
-  int32_t *pfp;           // wave 0's dependency polls (Mid::early / Mid::operator())
-  int pneed, pval;
-  int status = 0;         // the previous row's sdt_body result: 1 = its outputs are all +Inf
+  int status = 0;  // the previous row's sdt_body result: 1 = its outputs are all +Inf
+  bool stop = false;
 #pragma nounroll
-  for (int i = nt - 2; i >= 0 && status >= 0; --i) {
+  for (int i = nt - 2; i >= 0 && !stop; --i) {
 #pragma nounroll
-    for (int cp = lo; cp < hi && status >= 0; ++cp) {
+    for (int cp = lo; cp < hi && !stop; ++cp) {
       const bool last_row = cp + 1 == hi;
-      const int ncp = last_row ? lo : cp + 1, ni = last_row ? i - 1 : i;  // the next row
-      const bool has_next = ni >= 0;
-      const int g = k * R + cp;  // timeline stamps
+      h.cp = cp, h.i = i;
+      h.ncp = last_row ? lo : cp + 1, h.ni = last_row ? i - 1 : i;  // the next row
+      h.has_next = h.ni >= 0;
+      const int g = cp == lo ? h.g0 : 1 << 30;  // timeline stamps: the chunk's first row
       (void)g;
       SD_TL(0);
+      // this row's loads, sphere order and df / u_old (everything but the previous row's five stores) have landed;
+      // the memory clobber keeps the LDS reads of what the DMA wrote below this point
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       double v[8];
-      sd_take(v, raw);
-      // one row per workgroup: its sphere-0 source (position 0, the level at distance 0 from u_old(i+1)) is this
-      // workgroup's own output of the previous row, still in LDS (the loaded copy predates it)
-      if (hi - lo == 1 && pcp >= 0 && tid == 0)
+      sd_take(v, h.raw);
+      SD_TL(7);
+      // one row per workgroup: a sphere-0 source at distance 0 (u_old(i+1) on the level grid: position 0 with b̃ = 0)
+      // is this workgroup's own output of the previous row, still in LDS (the loaded copy predates it); an off-grid
+      // u_old(i+1) has b̃ >= 1 everywhere and no such source
+      if (hi - lo == 1 && h.pcp >= 0 && tid == 0 && (pslot(i + 1)[0] >> 16) == 0)
         v[0] = status == 1 ? INFINITY : dtv[pslot(i + 1)[0] & 0xFFFFu];
-      struct Mid {
-        int &pcp, &pi;
-        SdRaw &raw;
-        int32_t *dk, *lk, *err;
-        int cp, i, ncp, ni, lo, hi, B, NB, nt;
-        unsigned spin_limit, rowb, bufb, r0b;
-        bool has_next;
-        SdtShared<(1 << (3 * M - 3)) / 64> &sh;
-        const uint32_t *pk;
-        uint32_t *slot;
-        __amdgpu_buffer_rsrc_t rs;
-        int g;
-        // wave 0: this lane's dependency flag (a flag that always passes where it has none), the token it needs and
-        // the polled value -- kernel-scope variables, never re-initialised in the loop: a fresh value here would be
-        // a write to the register the last poll loaded into, and the compiler would wait for every store first
-        int32_t *&fp;
-        int &need, &val;
-        // loads of this row consumed: publish `loaded`; wave 0 issues its dependency polls (lanes 0-31 RAW for the
-        // next row, 32-63 WAR for this row's stores), results checked at the mid point
-        __device__ __forceinline__ void early() {
-          SD_TL_AT(g, i, nt, 1);
-          const int tid = threadIdx.x;
-          if (tid == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (tid < 64) {
-            const int lane = tid, s = lane < 32 ? lane + 1 : lane - 31;
-            fp = lk + cp;  // no dependency: any value passes
-            need = INT32_MIN;
-            if (lane < 32) {
-              const int r = ncp - s;
-              if (has_next && s <= 7 * M && r >= 1 && r < lo && nt - 2 - ni > 0) {
-                fp = dk + r;
-                need = nt - 2 - ni;  // token(ni + 1)
-              }
-            } else {
-              const int r = cp + s;
-              if (s <= 7 * M && r <= B && r >= hi && nt - i - NB > 0) {
-                fp = lk + r;
-                need = nt - i - NB;  // token(i + NB - 1)
-              }
-            }
-            val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every lane: no branch
-          }
-        }
-        __device__ __forceinline__ bool operator()() {
-          const int tid = threadIdx.x;
-          SD_TL_AT(g, i, nt, 2);
-          // the previous row's stores (every wave's) have landed: publish them
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          sd_bar();
-          SD_TL_AT(g, i, nt, 3);
-          if (tid < 64) {
-            const int lane = tid;
-            // evaluated before the flag store below: the compiler's wait for `val` would otherwise cover that store
-            bool ready = __all(val >= need);
-            if (lane == 0 && pcp >= 0)
-              __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            unsigned spins = 0;
-            for (;;) {
-              if (ready) break;
-              if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
-                if (lane == 0) {
-                  __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  sh.stop = 1;
-                }
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
-              val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              ready = __all(val >= need);
-            }
-          }
-          sd_bar();
-          SD_TL_AT(g, i, nt, 4);
-          if (sh.stop) return false;
-          pcp = cp;
-          pi = i;
-          if (has_next) {
-            // every wave is past its last read of this row's input sphere order (the slot of step i+1): the next
-            // step's order may land there (LDS-DMA, before the next row's loads, so that the counted wait at the
-            // next row's start covers it too)
-            if (ni != i) sd_perm_dma_asm<M>(pk + (size_t)ni * (1 << (3 * M)), slot + (ni & 1) * (1 << (3 * M)));
-            sd_issue_pipe<M>(raw, rs, slot + ((ni + 1) & 1) * (1 << (3 * M)), ncp, (unsigned)((ni + 1) % NB) * bufb,
-                             r0b + (unsigned)(ni + 1) * rowb, rowb);
-          }
-          SD_TL_AT(g, i, nt, 5);
-          return true;
-        }
-      } mid{pcp, pi, raw, dk, lk, err, cp, i, ncp, ni, lo, hi, B, NB, nt, spin_limit, rowb, bufb, r0b, has_next, sh,
-            pk, slot, rs, g, pfp, pneed, pval};
-      status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, pslot(i + 1), pslot(i), reg + (size_t)(i % NB) * R * L +
-                                 (size_t)cp * L, UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) +
-                                 (size_t)cp * L, sh, sds, mid, df_all, uo_all);
+      status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, pslot(i + 1), pslot(i),
+                                 reg + (size_t)(i % NB) * R * L + (size_t)cp * L,
+                                 UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L, sh,
+                                 sds, h, df_all, uo_all);
       SD_TL(6);
+      stop = sh.stop != 0;  // written before a barrier the row has passed since (every path has one)
     }
   }
   if (tid == 0) {
@@ -1250,6 +1358,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
     if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
   }
   SD_FLUSH();
+  SD_TL_FLUSH(h.g0);
 }
 
 bool sdt_supported(const PyrGeom &G) {

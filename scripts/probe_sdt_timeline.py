@@ -49,7 +49,7 @@ if len(sys.argv) > 3:
 rows = np.arange(1, R)  # row 0 has no workgroup
 steps = np.arange(2, 62)
 T = tl[rows][:, steps, :]
-ok = np.all(T[:, :, :7] > 0, axis=2)
+ok = np.all(T[:, :, :8] > 0, axis=2)
 names = ["loads consumed + reductions (0->1)", "stamp + passes (1->2)", "drain previous row (2->3)",
          "poll next inputs (3->4)", "issue next loads (4->5)", "winners + scans + stores (5->6)"]
 for q, nm in enumerate(names):
@@ -59,6 +59,8 @@ for q, nm in enumerate(names):
 per = (T[:, 1:, 0] - T[:, :-1, 0])
 print(f"step period per row: median {np.median(per):.3f}  p10 {np.percentile(per, 10):.3f}  p90 "
       f"{np.percentile(per, 90):.3f} us")
+d = (T[:, :, 7] - T[:, :, 0])[ok]
+print(f"{'  of it: waiting for the loads (0->7)':36s} median {np.median(d):6.3f}  p10 {np.percentile(d, 10):6.3f}  p90 {np.percentile(d, 90):6.3f} us")
 rest = (T[:, 1:, 0] - T[:, :-1, 6])
 print(f"stores issued -> next row start: median {np.median(rest):.3f} us")
 skew = T[1:, :, 0] - T[:-1, :, 0]  # row c starts step i this long after row c-1

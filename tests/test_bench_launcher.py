@@ -10,10 +10,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(gpus, batch):
+def _bench(gpus, batch, total=0):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--solver", "oracle", "--backend",
            "gloo", "--config", "C5", "--nt", "10", "--batch", str(batch), "--steps", "2", "--warmup", "1",
-           "--no-cpu-baseline"]
+           "--no-cpu-baseline", "--total", str(total)]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
@@ -30,3 +30,14 @@ def test_launcher_world2_matches_world1():
     # the same global batch per step (world x batch = 4 restarts): identical controls and Φ*
     assert two["checksum"] == one["checksum"]
     assert two["value"] > 0 and one["value"] > 0
+
+
+def test_launcher_strong_scaling_world2_matches_world1():
+    """Strong scaling (`--total`, the mode of bench.py's batch_strong line): a fixed global batch per step split
+    over the ranks -- 5 restarts as 3 + 2 on two ranks -- gives the same controls and Φ* as one rank solving all 5."""
+    two = _bench(2, 1, total=5)
+    one = _bench(1, 1, total=5)
+    assert two["scaling"] == "strong" and one["scaling"] == "strong"
+    assert two["checksum"] == one["checksum"]
+    weak = _bench(1, 5)
+    assert weak["checksum"] == one["checksum"] and weak["scaling"] == "weak"
