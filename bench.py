@@ -322,7 +322,7 @@ def roofline_of(res):
         ops = 1.0 * steps * K * (B + 1) * L * M * (14 / 8) * 4
         note = "separable transform FP64 ops (4 per merge); brute-force-equivalent candidates/s = " \
                f"{steps * K * ncand_step / avg_s:.4g}"
-    elif name in ("k_fused_run", "k_fsep_run"):
+    elif name in ("k_fused_run", "k_fsep_run", "k_fsep2"):
         # one launch = every step of K subproblems; the value fronts never leave the CU's LDS, so the HBM bytes
         # the DP must move are U (one byte per cell), df and u_old in, and Φ_0 out for the backtrack's argmin
         steps = nt - 1
@@ -330,6 +330,19 @@ def roofline_of(res):
         if name == "k_fused_run":
             ops = 2.0 * K * steps * ncand_step  # v_add_f64 + v_min_f64 per candidate
             note = "min-plus candidates: 2 FP64 ops each"
+        elif name == "k_fsep2":
+            # two lanes per row: x0 pass N1 lines x 2(N0-1) merges, x1 pass per column 2 x 2(H-1) local merges
+            # + 2H cross-half merges (H = N1/2); 6 32-bit VALU ops per merge (add_sat, min, sad, cmp, cndmask, or)
+            n0, n1 = len(lv.nu[0]), len(lv.nu[1])
+            h = n1 // 2
+            merges = n1 * 2 * (n0 - 1) + n0 * (4 * (h - 1) + 2 * h)
+            ops = 6.0 * K * steps * (B + 1) * merges
+            seg = res.get("diag", [0] * 9)[8] if len(res.get("diag", [])) > 8 else 1
+            if seg and seg > 1:  # the segment boundaries' outbox rows: written once, read once per step
+                bytes_per_launch += K * (seg - 1) * steps * (n0 + n1 - 2) * L * 8 * 2
+            note = (f"separable transform VALU lane-ops ({merges} fixed-point merges x 6 per row, {seg} row "
+                    f"segment(s) per subproblem); brute-force-equivalent candidates/s = "
+                    f"{K * steps * ncand_step / avg_s:.4g}")
         else:
             n0 = len(lv.nu[0])
             merges = 2 * (n0 - 1) * L // n0 + 2 * (L // n0 - 1) * L // (L // n0)  # both passes, both sweeps
@@ -358,8 +371,10 @@ def roofline_of(res):
             "traffic_source": tsrc, "kernel": name,
             "avg_launch_us": round(avg_s * 1e6, 3), "bytes_per_launch": bytes_per_launch,
             "us_per_dp_step": round(avg_s * 1e6 / steps, 3)}
+    # FP64 and 32-bit VALU ops issue at the same rate on gfx950 (16 lanes per SIMD per clock)
     valu = {"bound": "valu", "achieved": round(ops / avg_s / 1e12, 6), "peak": FP64_VALU_PEAK_TOPS,
-            "unit": "TFP64op/s", "frac": round(ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS, 6)}
+            "unit": "T VALU lane-ops/s" if name == "k_fsep2" else "TFP64op/s",
+            "frac": round(ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS, 6)}
     if note:
         valu["note"] = note
     return roof, valu

@@ -72,6 +72,10 @@ extern "C" {
                                  (default 2^24; a tiny value forces that fallback, for tests) */
 #define MIOC_OPT_SDT_BUFFERS 6 /* persistent separable transform: staging buffers (4..64, default 64; more
                                   buffers let rows run further apart, which hides the row hand-off) */
+#define MIOC_OPT_FSEP_SEGMENTS 7 /* fused separable DP: row segments per subproblem, each on its own workgroup
+                                    (0, default: chosen from the batch size -- more than one only when the
+                                    batch alone cannot fill the GPU; 1..8: forced; -1: the one-lane-per-row
+                                    kernel of mioc_fused.hip) */
 
 typedef struct mioc_ctx mioc_ctx;
 
@@ -250,7 +254,9 @@ int32_t mioc_last_algo(mioc_ctx *ctx);
  * settles up to 64 steps), [3] internal consistency failures (must be 0); [4..7] pyramid internals: rows whose
  * value hash overflowed, targets whose value was not found, values flagged as colliding (after a separable-transform
  * DP, [6] instead counts this context's persistent DPs redone with per-step launches: cooperative launch refused, or
- * a dependency wait timed out -- 0 on a healthy run); [7] fused DP: resident workgroups per CU (occupancy query).
+ * a dependency wait timed out -- 0 on a healthy run; after a fused separable DP, the segmented launches redone with
+ * one workgroup per subproblem); [7] fused DP: resident workgroups per CU (occupancy query); [8] fused separable DP:
+ * row segments per subproblem (0: the one-lane-per-row kernel).  n may be up to 9.
  */
 int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n);
 

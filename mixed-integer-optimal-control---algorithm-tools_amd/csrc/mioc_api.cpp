@@ -93,6 +93,8 @@ void ev_collect(mioc_ctx *ctx);
 void free_all(mioc_ctx *ctx) {
   if (ctx->d_runflags) hipFree(ctx->d_runflags);
   if (ctx->d_chain) hipFree(ctx->d_chain);
+  if (ctx->d_ring) hipFree(ctx->d_ring);
+  if (ctx->d_segflags) hipFree(ctx->d_segflags);
   if (ctx->h_run_err) hipHostFree(ctx->h_run_err);
   void *ptrs[] = {ctx->d_nuval, ctx->d_nuint,  ctx->d_gidx,      ctx->d_numin,       ctx->d_numax,
                   ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
@@ -366,9 +368,61 @@ int run_bellman(mioc_ctx *ctx) {
       ev_begin(ctx, 0, "k_fused_run");
       HIP_TRY(ctx, launch_fused_run(ctx->stream, P, Lv, ctx->d_front, front_stride, (uint8_t *)ctx->d_U, u_stride_k));
     } else {
-      ev_begin(ctx, 0, "k_fsep_run");
-      HIP_TRY(ctx, launch_fsep_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_front, front_stride, (uint8_t *)ctx->d_U,
-                                   u_stride_k, ctx->d_counters));
+      // two lanes per row, the front in place (mioc_fsep.hip); S row segments per subproblem when the batch alone
+      // would leave CUs idle (two resident subproblems per CU when the front is half the LDS)
+      FsepPlan plan;
+      int S = ctx->force_steps ? 1 : ctx->opt_fsep_seg;
+      if (S == 0) {
+        int ncu = 0;
+        HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        S = 1;
+        while (S < 8 && (size_t)K * (size_t)(2 * S) <= (size_t)ncu && fsep2_plan(ctx->pyr, ctx->B, 2 * S, nullptr))
+          S *= 2;
+      }
+      // a u_old off the level grid can send a target further than SMAX rows up, past a segment's outbox rows
+      if (S > 1 && bmax > ctx->pyr.n[0] + ctx->pyr.n[1] - 2) S = 1;
+      const bool v2 = S >= 1 && fsep2_plan(ctx->pyr, ctx->B, S, &plan);
+      ctx->last_fsep_seg = v2 ? S : 0;
+      if (v2) ctx->occupancy = fsep2_blocks_per_cu(ctx->pyr, plan);
+      if (v2 && S > 1) {
+        const int NB = 8, SM = ctx->pyr.n[0] + ctx->pyr.n[1] - 2;
+        rc = grow(ctx, &ctx->d_ring, &ctx->ring_cap, K * (size_t)S * NB * SM * L * sizeof(double), "segment rings");
+        if (!rc) rc = grow(ctx, &ctx->d_segflags, &ctx->segflag_cap, (2 * K * (size_t)S + 1) * sizeof(int32_t),
+                           "segment flags");
+        if (rc) return rc;
+        if (!ctx->h_run_err) HIP_TRY(ctx, hipHostMalloc(&ctx->h_run_err, 16, 0));
+        *ctx->h_run_err = 0;
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_segflags, 0, (2 * K * (size_t)S + 1) * sizeof(int32_t), ctx->stream));
+        ev_begin(ctx, 0, "k_fsep2");
+        const hipError_t le = launch_fsep2(ctx->stream, P, Lv, ctx->pyr, plan, ctx->d_front, front_stride,
+                                           (uint8_t *)ctx->d_U, u_stride_k, ctx->d_counters, ctx->d_ring, NB,
+                                           ctx->d_segflags, ctx->spin_limit);
+        if (le == hipErrorCooperativeLaunchTooLarge) {  // not every segment resident: one workgroup per subproblem
+          (void)hipGetLastError();
+          ev_end(ctx, 0, 0);
+          ctx->n_persist_fallbacks += 1;
+          ctx->force_steps = true;
+          const int rcs = run_bellman(ctx);
+          ctx->force_steps = false;
+          return rcs;
+        }
+        HIP_TRY(ctx, le);
+        ev_end(ctx, 0, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_segflags + 2 * K * (size_t)S, sizeof(int32_t),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        ctx->run_pending = true;
+        ctx->have_dp = true;
+        return MIOC_OK;
+      }
+      if (v2) {
+        ev_begin(ctx, 0, "k_fsep2");
+        HIP_TRY(ctx, launch_fsep2(ctx->stream, P, Lv, ctx->pyr, plan, ctx->d_front, front_stride, (uint8_t *)ctx->d_U,
+                                  u_stride_k, ctx->d_counters, nullptr, 1, nullptr, ctx->spin_limit));
+      } else {
+        ev_begin(ctx, 0, "k_fsep_run");
+        HIP_TRY(ctx, launch_fsep_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_front, front_stride, (uint8_t *)ctx->d_U,
+                                     u_stride_k, ctx->d_counters));
+      }
     }
     ev_end(ctx, 0, 1);
   } else if (algo == MIOC_ALGO_GENERIC) {
@@ -584,6 +638,11 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   if (option == MIOC_OPT_SDT_BUFFERS) {
     if (value < 4 || value > kSdtMaxBuffers) return fail(ctx, MIOC_EINVAL, "staging buffers must be in [4, 64]");
     ctx->opt_nb = (int)value;
+    return MIOC_OK;
+  }
+  if (option == MIOC_OPT_FSEP_SEGMENTS) {
+    if (value < -1 || value > 8) return fail(ctx, MIOC_EINVAL, "fused separable segments must be in [-1, 8]");
+    ctx->opt_fsep_seg = (int)value;
     return MIOC_OK;
   }
   return fail(ctx, MIOC_EINVAL, "unknown option");
@@ -1094,9 +1153,13 @@ int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
   HIP_TRY(ctx, hipMemcpy(f, ctx->d_flags, sizeof f, hipMemcpyDeviceToHost));
   // slot 6: the separable transform's persistent DPs redone with per-step launches (cooperative launch refused or a
   // dependency wait timed out) -- its kernels write no c[6]; the pyramid's value-collision count otherwise
-  const int64_t c6 = ctx->algo == MIOC_ALGO_SEPARABLE ? ctx->n_persist_fallbacks : c[6];
-  const int64_t all[8] = {c[0], c[1], f[2], f[3], c[4], c[5], c6, ctx->occupancy};
-  for (int32_t q = 0; q < n && q < 8; ++q) counters[q] = all[q];
+  // slot 8: row segments per subproblem of the last fused separable DP (0: the one-lane-per-row kernel)
+  const int64_t c6 = ctx->algo == MIOC_ALGO_SEPARABLE || ctx->algo == MIOC_ALGO_FUSED_SEPARABLE
+                         ? ctx->n_persist_fallbacks
+                         : c[6];
+  const int64_t all[9] = {c[0], c[1], f[2], f[3], c[4], c[5], c6, ctx->occupancy,
+                          ctx->algo == MIOC_ALGO_FUSED_SEPARABLE ? ctx->last_fsep_seg : 0};
+  for (int32_t q = 0; q < n && q < 9; ++q) counters[q] = all[q];
   return MIOC_OK;
 }
 

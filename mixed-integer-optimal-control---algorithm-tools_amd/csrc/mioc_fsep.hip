@@ -1,0 +1,593 @@
+// mioc_fsep.hip -- the fused separable DP of a small 2-D product grid (p = 1, the batch path):
+// bellman_TRM! (HelpFunctions.jl:20-83) for one subproblem entirely on chip, round-3 layout.
+//
+//   * Two lanes per source row c': lane pair (2r, 2r+1) splits the N0 x N1 grid into its x1 halves, so one
+//     wave carries 32 rows and a row's separable transform is half as long.  Lane 2r holds x1 = 0..H-1 in its
+//     slots s = 0..H-1, lane 2r+1 holds x1 = N1-1..H in the same slots (mirrored), which makes the cross-half
+//     step of the x1 pass the same instruction on both lanes: take the partner's slot H-1 (DPP swap) and merge
+//     it into slot H-1-t at cost t+1.
+//   * The front Φ is updated IN PLACE: read phase (every lane reads its row, runs the transform, gathers its
+//     results into registers), barrier, write phase (results, the inbox of the segment below, +Inf cells, the
+//     next step's K table), barrier.  One copy of the front (~79 KB at C5) lets two subproblems share a CU.
+//   * A subproblem may be split into S row segments on S workgroups (strong scaling: 128 restarts still fill
+//     256 CUs).  Segment q owns rows [lo_q, hi_q); the targets its rows send above hi_q (at most SMAX rows) go
+//     to an outbox ring in HBM that segment q+1 reads one step later.  The hand-off is one-directional, so
+//     segment q never waits for q+1 except to reuse a ring slot (NB steps back).  Flags are relaxed agent-scope
+//     atomics in the measured-valid form of MI355X_MICROARCH.md (sc1 stores drained by every storing wave,
+//     then one lane's flag store behind a barrier; the consumer loads the bytes only after its own poll
+//     matched).  S > 1 is a cooperative launch (every workgroup resident); a wait past the spin limit sets
+//     *err and every workgroup leaves, and the host redoes the DP with S = 1 (check_run).
+//
+// Certified argmin, as in mioc_fused.hip's k_fsep_run: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) with the source
+// coordinates x0 | x1 << 3 in the 6 low mantissa bits and bit 6 as the near-tie flag; an unflagged winner is the
+// reference's unique argmin and its value is recomputed with the reference's expression
+// fl(fl(T1_l + fl(β·d)) + Ψ_j*) from the per-step table K_l[d].  Flagged targets and rows outside the binade run
+// the reference loop (HelpFunctions.jl:60-77) exactly, one lane per target.  The merge order of a separable pass
+// does not matter for the certificate: any binary merge tree compares the eventual winner's candidate set with
+// every other set's minimum, so a candidate within tol of the winner always sets the flag.
+//
+// HBM traffic per subproblem: df, u_old once, U = (nt-1)·L·(B+1) bytes, Φ_0 = L·RP·8 bytes at the end, plus
+// (S > 1) the outbox rows: (nt-1)·SMAX·L·8 bytes per segment boundary, written once and read once.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+
+#include "mioc_internal.h"
+
+namespace mioc {
+
+namespace {
+
+constexpr int FS2_FLAG = 64;  // near-tie flag (payload bit 6)
+constexpr int FS2_MAXT = 512;  // threads per workgroup: 256 budget rows + row B (larger B: mioc_fused.hip)
+
+__device__ __forceinline__ void fs_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ double fs_min(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// merge of two candidate sets in 32-bit fixed point: the smaller, flagged when the two are within tolq (the
+// neighbour's set arrives at distance cost d, +Inf saturating)
+__device__ __forceinline__ unsigned fs_qmerge(unsigned a, unsigned nb, unsigned d, unsigned tolq) {
+  const unsigned t = __builtin_elementwise_add_sat(nb, d);
+  const unsigned m = min(a, t);
+  unsigned diff;  // |a - t|
+  asm("v_sad_u32 %0, %1, %2, 0" : "=v"(diff) : "v"(a), "v"(t));
+  return m | (diff <= tolq ? (unsigned)FS2_FLAG : 0u);
+}
+
+__device__ __forceinline__ unsigned fs_swap_u(unsigned x) {
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+}
+
+// the partner lane's (tid ^ 1) value: DPP quad_perm [1, 0, 3, 2], no LDS round trip
+__device__ __forceinline__ double fs_swap(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ int fs_uint(double u) { return (int)fmin(fmax(u, -1.0e8), 1.0e8); }
+
+__device__ __forceinline__ double fs_ld(const double *p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void fs_st(double *p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace
+
+// diagnostic build (make stamps): per-wave phase cycles (s_memtime), summed over the steps
+#if defined(MIOC_STAMPS)
+__device__ unsigned long long g_fs_stamps[4096][8];
+#define FS_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define FS_ACC(q, a, b) acc[q] += (b) - (a)
+#else
+#define FS_T(v)
+#define FS_ACC(q, a, b)
+#endif
+
+struct FsepArgs {
+  double *front0;
+  size_t front_stride;
+  uint8_t *U;
+  size_t u_stride_k;
+  int32_t *counters;
+  double *ring;    // [K][S][NB][SMAX][L]: segment q's outbox (rows hi_q .. hi_q + SMAX - 1), read by q + 1
+  int32_t *flags;  // [K][S][2] {outbox token, consumed token}, then the error flag at [2·K·S]
+  int S, RS, NB;   // segments, rows per segment (a multiple of 32), ring depth
+  int koff;        // K table offset in the LDS (doubles)
+  unsigned spin_limit;
+  int base0, base1;
+};
+
+template <int N0, int N1, bool SEG>
+__global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, FsepArgs A) {
+  constexpr int L = N0 * N1, H = N1 / 2, V = N0 * H, SMAX = N0 + N1 - 2, ND = SMAX + 1;
+  constexpr int FS = (L + 1) | 1;  // odd row stride (8-byte words)
+  static_assert(N1 % 2 == 0 && N0 <= 8 && N1 <= 8 && V <= 32, "grid shape");
+  extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+  __shared__ int s_stop;
+  constexpr int NIN = 8;  // inbox cells per thread (host: SMAX·L <= 8·threads)
+  const int S = SEG ? A.S : 1, k = (int)blockIdx.x / S, q = (int)blockIdx.x - k * S;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nthr = blockDim.x, nw = nthr >> 6;
+  const int B = P.B, R = B + 1, nt = P.nt, NB = A.NB;
+  const int lo = min(R, q * A.RS), hi = q == S - 1 ? R : min(R, (q + 1) * A.RS);
+  const int nloc = min(R, hi + SMAX) - lo;  // LDS rows: own rows, then the outbox halo
+  double *const F = reinterpret_cast<double *>(fsm);
+  double *const Kt = F + A.koff;
+  const int cx = lo + (nthr >> 1);  // past the lane pairs: the extra row (row B) when cx < hi
+  const double beta = Lv.beta, inv = Lv.inv_beta;
+  const double numx0 = (double)max(abs(A.base0), abs(A.base0 + N0 - 1)),
+               numx1 = (double)max(abs(A.base1), abs(A.base1 + N1 - 1));
+  int32_t *const fl = A.flags + 2 * ((size_t)k * S + q);
+  int32_t *const err = A.flags + 2 * (size_t)P.K * S;
+  const size_t ring_seg = (size_t)NB * SMAX * L;
+  double *const ring_out = A.ring + ((size_t)k * S + q) * ring_seg;
+  const double *const ring_in = A.ring + ((size_t)k * S + (q > 0 ? q - 1 : 0)) * ring_seg;
+
+  auto inputs = [&](int s, double &a0, double &a1, double &u0, double &u1) {
+    const double *dfs = P.df + ((size_t)k * nt + s) * 2;
+    const double *uos = P.uold + ((size_t)k * nt + s) * 2;
+    a0 = P.dt * dfs[0];
+    a1 = P.dt * dfs[1];
+    u0 = uos[0];
+    u1 = uos[1];
+  };
+  // per-step table, HelpFunctions.jl:52-67: K_l[d] = fl(T1(l) + fl(β·d))
+  auto prepare = [&](double a0, double a1) {
+    for (int e = tid; e < L * ND; e += nthr) {
+      const int l = e / ND, d = e - l * ND;
+      const double t1 = (0.0 + a0 * (double)(A.base0 + l % N0)) + a1 * (double)(A.base1 + l / N0);
+      Kt[e] = t1 + beta * (double)d;
+    }
+  };
+  // a wave-uniform wait for a flag to reach `need`; false (and the launch abandoned) past the spin limit
+  auto wait_flag = [&](const int32_t *f, int &val, int need) {
+    unsigned spins = 0;
+    while (!__all(val >= need)) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > A.spin_limit) {
+        if (lane == 0) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_stop = 1;
+        }
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      val = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+  };
+
+  // ---- terminal step (HelpFunctions.jl:27-43): Φ_{nt-1}[c][l] = T1 where b̃_l(nt-1) = c --------------------
+  double ca0 = 0.0, ca1 = 0.0;
+  int cu0 = 0, cu1 = 0;
+  {
+    double a0, a1, u0, u1;
+    inputs(nt - 1, a0, a1, u0, u1);
+    const int iu0 = fs_uint(u0), iu1 = fs_uint(u1);
+    for (int e = tid; e < nloc * FS; e += nthr) {
+      const int c = lo + e / FS, l = e % FS;
+      double v = INFINITY;
+      if (l < L && abs(A.base0 + l % N0 - iu0) + abs(A.base1 + l / N0 - iu1) == c)
+        v = (0.0 + a0 * (double)(A.base0 + l % N0)) + a1 * (double)(A.base1 + l / N0);
+      F[e] = v;
+    }
+    if (nt >= 2) {
+      inputs(nt - 2, a0, a1, u0, u1);
+      prepare(a0, a1);
+      ca0 = a0;
+      ca1 = a1;
+      cu0 = fs_uint(u0);
+      cu1 = fs_uint(u1);
+    }
+    if (tid == 0) s_stop = 0;
+  }
+  __syncthreads();
+  uint8_t *Uk = A.U + (size_t)k * A.u_stride_k;
+  int nflag = 0, nscan = 0;
+#if defined(MIOC_STAMPS)
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+#pragma nounroll
+  for (int i = nt - 2; i >= 0; --i) {
+    // this lane's row and slots, derived from an opaque copy of the thread index every step: hoisted out of the
+    // step loop, the per-target constants (LDS offsets, U offsets) would take more registers than the row itself
+    int tido = tid;
+    asm volatile("" : "+v"(tido));
+    const int hf = tido & 1;
+    const int cp = lo + (tido >> 1);  // this lane pair's source row
+    const bool act = cp < hi;
+    const int room = act ? B - cp : -1;  // target l of this row is inside the trust region iff b̃_l <= room
+    const int cl = act ? cp - lo : 0;
+    const int lb = cl * FS + (hf ? N0 * (N1 - 1) : 0), ls = hf ? -N0 : N0;  // slot s, x0 at F[lb + ls·s + x0]
+    int x1v[H];
+#pragma unroll
+    for (int s = 0; s < H; ++s) x1v[s] = hf ? N1 - 1 - s : s;
+    const int su0 = __builtin_amdgcn_readfirstlane(cu0), su1 = __builtin_amdgcn_readfirstlane(cu1);
+    auto btl = [&](int x0, int x1) { return abs(A.base0 + x0 - su0) + abs(A.base1 + x1 - su1); };
+    // U_i[l][c] through a buffer resource (bounds-checked to the step's L·R bytes: a store past them is dropped)
+    const __amdgpu_buffer_rsrc_t Ur =
+        __builtin_amdgcn_make_buffer_rsrc(Uk + (size_t)i * ((size_t)L * R), 0, L * R, 0x00020000);
+    double na0 = 0.0, na1 = 0.0, nu0 = 0.0, nu1 = 0.0;
+    if (i >= 1) inputs(i - 1, na0, na1, nu0, nu1);
+    // polls, issued now and checked later: the outbox of the segment below for this step (RAW), and whether
+    // the segment above has consumed the ring slot this step's outbox overwrites (WAR)
+    const int need_in = SEG && q > 0 ? nt - 1 - i : INT_MIN;
+    const int need_cons = SEG && q < S - 1 && i + NB <= nt - 2 ? nt - 1 - (i + NB) : INT_MIN;
+    int vin = 0, vcons = 0;
+    if (SEG && q > 0) vin = __hip_atomic_load(fl - 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (SEG && need_cons != INT_MIN) vcons = __hip_atomic_load(fl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    // ================= read phase: Φ_{i+1} rows into registers, the transform, results into registers ========
+    FS_T(q0);
+    double o[V];
+#pragma unroll
+    for (int s = 0; s < H; ++s)
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) o[x0 + N0 * s] = F[lb + ls * s + x0];
+    const double a0 = ca0, a1 = ca1;
+    // ---- row statistics over the finite sources (both lanes of the pair) ----------------------------------
+    double pmn = o[0], pmx = o[0];
+#pragma unroll
+    for (int j = 1; j < V; ++j) {
+      pmn = fs_min(pmn, o[j]);
+      pmx = fmax(pmx, o[j]);
+    }
+    pmn = fs_min(pmn, fs_swap(pmn));
+    pmx = fmax(pmx, fs_swap(pmx));
+    const bool infrow = !(pmx < INFINITY);
+    if (__ballot(infrow && pmn < INFINITY)) {  // some sources unreachable: the maximum over the finite ones
+      double m2 = pmn;
+#pragma unroll
+      for (int j = 0; j < V; ++j) m2 = fmax(m2, o[j] < INFINITY ? o[j] : pmn);
+      pmx = fmax(m2, fs_swap(m2));
+    }
+    // ---- 32-bit fixed point: A_j = trunc((Ψ_j - Ψmin)/β · 2^Fb) << 7 | x0 | x1 << 3, +Inf = 0xFFFFFFFF --------
+    // (β units, grid g = 2^-Fb; every candidate value A + d·2^(Fb+7) stays below 2^31, so unit steps are exact
+    // integer additions and +Inf saturates)
+    const double rs = (pmx - pmn) * inv + (double)SMAX;  // scaled range of every candidate value
+    const bool scale_ok = rs < 0x1p19;
+    const int E = ilogb(fmin(rs, 0x1p19) * (1.0 + 0x1p-20) + 1.0) + 1;  // 2^E > rs
+    const int Fb = 24 - E;
+    const double g = ldexp(1.0, -Fb);
+    const double qmax = beta * (double)SMAX + fmax(fabs(pmn), fabs(pmx)) + fabs(a0) * numx0 + fabs(a1) * numx1;
+    // 2 x stamping error (< g) + 2 x the reference's rounding (<= 4u·qmax per candidate), in units of β
+    const double tol = 3.0 * g + 0x1p-49 * qmax * inv;
+    const bool none = !(pmn < INFINITY);
+    const bool direct = !none && !(scale_ok && tol < 0.25);
+    const double sc = ldexp(inv, Fb);
+    const unsigned U1 = 1u << (Fb + 7);                                    // one unit of distance
+    const unsigned tolq = direct ? 0u : (unsigned)(tol * ldexp(1.0, Fb + 7));  // |A - T| <= tolq <=> within tol
+    if (none) pmn = 0.0;
+    unsigned a[V];
+#pragma unroll
+    for (int s = 0; s < H; ++s)
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        const int t = x0 + N0 * s;
+        const unsigned q0 = (unsigned)((o[t] - pmn) * sc) << 7 | (unsigned)(x0 | x1v[s] << 3);
+        a[t] = o[t] < INFINITY ? q0 : 0xFFFFFFFFu;
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    FS_T(q1);
+    // ---- pass along x0: this lane's H lines are whole --------------------------------------------------------
+#pragma unroll
+    for (int s = 0; s < H; ++s) {
+#pragma unroll
+      for (int x0 = 1; x0 < N0; ++x0) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[s * N0 + x0 - 1], U1, tolq);
+#pragma unroll
+      for (int x0 = N0 - 2; x0 >= 0; --x0) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[s * N0 + x0 + 1], U1, tolq);
+    }
+    // ---- pass along x1: this lane's H slots (orientation-free), then the partner's boundary slot ------------
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) {
+#pragma unroll
+      for (int s = 1; s < H; ++s) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[(s - 1) * N0 + x0], U1, tolq);
+#pragma unroll
+      for (int s = H - 2; s >= 0; --s) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[(s + 1) * N0 + x0], U1, tolq);
+    }
+#pragma unroll
+    for (int x0 = 0; x0 < N0; ++x0) {
+      const unsigned pb = fs_swap_u(a[(H - 1) * N0 + x0]);
+#pragma unroll
+      for (int t = 0; t < H; ++t) a[(H - 1 - t) * N0 + x0] = fs_qmerge(a[(H - 1 - t) * N0 + x0], pb, (t + 1) * U1, tolq);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    FS_T(q2);
+    // ---- the segment below has published this step's outbox: load it (consumed in the write phase) --------
+    double inb[SEG ? NIN : 1];
+    if (SEG) {
+#pragma unroll
+      for (int u = 0; u < NIN; ++u) inb[u] = INFINITY;
+      if (q > 0 && wait_flag(fl - 2, vin, need_in)) {
+        const double *slot = ring_in + (size_t)(i % NB) * SMAX * L;
+#pragma unroll
+        for (int u = 0; u < NIN; ++u)
+          if (tid + u * nthr < SMAX * L) inb[u] = fs_ld(slot + tid + u * nthr);
+      }
+    }
+    // ---- winners: R(l, j*) = fl(K_l[d(l, j*)] + Ψ_j*) for the certified winner j* ----------------------------
+    unsigned vmask = 0, smask = 0;
+    const unsigned dirb = direct ? 1u : 0u;
+    uint32_t jw[(V + 3) / 4];
+#pragma unroll
+    for (int u = 0; u < (V + 3) / 4; ++u) jw[u] = 0;
+#pragma unroll
+    for (int s = 0; s < H; ++s) {
+      double kv[N0], pv[N0];
+      int jj[N0];
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        const int t = x0 + N0 * s, x1 = x1v[s], l = x0 + N0 * x1;
+        const int yl = (int)a[t];
+        const int wx0 = yl & 7, wx1 = (yl >> 3) & 7;
+        jj[x0] = wx0 + N0 * wx1;
+        const int d = abs(x0 - wx0) + abs(x1 - wx1);
+        kv[x0] = Kt[l * ND + min(d, SMAX)];
+        pv[x0] = F[cl * FS + jj[x0]];
+      }
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        const int t = x0 + N0 * s;
+        // the mask bits as integer arithmetic (shift-or with an inline shift count; a condition would become a
+        // select between 0 and a materialised 1 << t in a register per bit)
+        const unsigned vb = ((unsigned)(room - btl(x0, x1v[s])) >> 31) ^ 1u;  // b̃_l <= room
+        const unsigned fb = min(~a[t], 1u);                                     // finite
+        const unsigned gb = (a[t] >> 6) & 1u;                                   // near-tie flag
+        vmask |= vb << t;
+        smask |= (vb & (dirb | (fb & gb))) << t;
+        o[t] = (vb & fb) ? kv[x0] + pv[x0] : INFINITY;
+        jw[t >> 2] |= (uint32_t)(jj[x0] & 0xFF) << (8 * (t & 3));
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one line's gathers at a time (all in flight would need 4·V VGPRs)
+    }
+    FS_T(q3);
+    // the masks stay VGPR words: seen through, the compiler keeps one 64-bit lane mask per target in SGPRs
+    // through the barrier (and spills them)
+    asm volatile("" : "+v"(vmask), "+v"(smask));
+    // ---- exact scans (near ties, rows outside the binade): the reference loop, one lane per target ---------
+    if (__ballot(smask != 0)) {
+#pragma unroll
+      for (int s = 0; s < H; ++s)
+#pragma unroll
+        for (int x0 = 0; x0 < N0; ++x0) {
+          const int t = x0 + N0 * s;
+          if ((smask >> t) & 1u) {
+            const int x1 = x1v[s], l = x0 + N0 * x1;
+            double best = INFINITY;
+            int bj = 0;
+#pragma unroll 4
+            for (int j = 0; j < L; ++j) {
+              const int dj = abs(x0 - j % N0) + abs(x1 - j / N0);
+              const double v = Kt[l * ND + dj] + F[cl * FS + j];
+              if (v < best) {  // strict: the first j in iterator order wins ties (HelpFunctions.jl:71-76)
+                best = v;
+                bj = j;
+              }
+            }
+            o[t] = best;
+            jw[t >> 2] = (jw[t >> 2] & ~(0xFFu << (8 * (t & 3)))) | ((uint32_t)bj << (8 * (t & 3)));
+          }
+        }
+      nscan += __popc(smask);
+      nflag += direct ? 0 : __popc(smask);
+    }
+    // ---- the extra row (row B, past the lane pairs): its one target, u_old(i) itself, by an exact scan -------
+    double xv = INFINITY;
+    int xj = 0, xl = -1;
+    if (w == nw - 1 && cx < hi) {
+      const int x0t = su0 - A.base0, x1t = su1 - A.base1;
+      if (x0t >= 0 && x0t < N0 && x1t >= 0 && x1t < N1) {
+        xl = x0t + N0 * x1t;
+        double v = INFINITY;
+        if (lane < L)
+          v = Kt[xl * ND + abs(x0t - lane % N0) + abs(x1t - lane / N0)] + F[(cx - lo) * FS + lane];
+        int j = lane;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          const double ov = __shfl_xor(v, off);
+          const int oj = __shfl_xor(j, off);
+          if (ov < v || (ov == v && oj < j)) {
+            v = ov;
+            j = oj;
+          }
+        }
+        xv = v;
+        xj = j;
+        if (lane == 0) nscan += 1;
+      }
+    }
+    FS_T(q4);
+    // every wave's outstanding global accesses (the previous write phase's U / outbox stores, this step's
+    // inbox loads) complete before the barrier: the flags published after it cover them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fs_bar();  // ---- every lane has read Φ_{i+1}: the front may be overwritten ---------------------------------
+    FS_T(q5);
+    if (SEG && tid == 0) {
+      if (q < S - 1 && i + 1 <= nt - 2)
+        __hip_atomic_store(fl, nt - 1 - (i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // outbox of i+1
+      if (q > 0) __hip_atomic_store(fl + 1, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // inbox i read
+    }
+    // ================= write phase: Φ_i ======================================================================
+    if (SEG && need_cons != INT_MIN) wait_flag(fl + 3, vcons, need_cons);
+    double *const ring_slot = ring_out + (size_t)(i % NB) * SMAX * L;
+    // the write offsets from a second opaque copy of the thread index, taken after the barrier: computed before
+    // it, they would stay live through the whole read phase
+    int tidw = tid;
+    asm volatile("" : "+v"(tidw));
+    const int hfw = tidw & 1, cpw = lo + (tidw >> 1);
+#pragma unroll
+    for (int s = 0; s < H; ++s)
+#pragma unroll
+      for (int x0 = 0; x0 < N0; ++x0) {
+        const int t = x0 + N0 * s, x1 = hfw ? N1 - 1 - s : s, l = x0 + N0 * x1;
+        if ((vmask >> t) & 1u) {
+          const int c = cpw + btl(x0, x1);
+          F[(c - lo) * FS + l] = o[t];
+          if (SEG && c >= hi) fs_st(ring_slot + (c - hi) * L + l, o[t]);  // the segment above's cell
+        }
+        const int c = cpw + btl(x0, x1);
+        // (l varies across the lane pair: the whole offset goes in the VGPR operand, soffset must stay uniform)
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(jw[t >> 2] >> (8 * (t & 3))), Ur,
+                                             ((vmask >> t) & 1u) && o[t] < INFINITY ? l * R + c : 0x40000000, 0, 0);
+      }
+    if (xl >= 0 && lane == 0) {
+      F[(cx - lo) * FS + xl] = xv;
+      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)xj, Ur, xv < INFINITY ? xl * R + cx : 0x40000000, 0, 0);
+    }
+    if (SEG && q > 0) {  // the inbox: cells of rows lo .. lo+SMAX-1 whose source row is below lo
+#pragma unroll
+      for (int u = 0; u < NIN; ++u) {
+        const int e = tid + u * nthr;
+        const int c = lo + e / L, l = e % L;
+        const int b = btl(l % N0, l / N0);
+        if (e < SMAX * L && c < hi && c >= b && c - b < lo) F[(c - lo) * FS + l] = inb[u];
+      }
+    }
+    // cells below the target's own budget class: +Inf (target l by wave l % nw)
+#pragma unroll 1
+    for (int l = w; l < L; l += nw) {
+      const int b = min(btl(l % N0, l / N0), hi);
+      for (int c = lo + lane; c < b; c += 64) F[(c - lo) * FS + l] = INFINITY;
+    }
+    if (i >= 1) prepare(na0, na1);
+    ca0 = na0;
+    ca1 = na1;
+    cu0 = fs_uint(nu0);
+    cu1 = fs_uint(nu1);
+    FS_T(q6);
+    fs_bar();  // ---- Φ_i complete -------------------------------------------------------------------------------
+    FS_T(q7);
+    FS_ACC(0, q0, q1);
+    FS_ACC(1, q1, q2);
+    FS_ACC(2, q2, q3);
+    FS_ACC(3, q3, q4);
+    FS_ACC(4, q4, q5);
+    FS_ACC(5, q5, q6);
+    FS_ACC(6, q6, q7);
+    FS_ACC(7, q0, q7);
+    if (s_stop) break;
+  }
+#if defined(MIOC_STAMPS)
+  if (lane == 0)
+    for (int u = 0; u < 8; ++u) g_fs_stamps[((int)blockIdx.x * nw + w) & 4095][u] = acc[u];
+#endif
+  // the last step's outbox
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (SEG && tid == 0 && q < S - 1 && !s_stop)
+    __hip_atomic_store(fl, nt - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    nflag += __shfl_xor(nflag, off);
+    nscan += __shfl_xor(nscan, off);
+  }
+  if (lane == 0 && (nflag | nscan)) {  // diagnostics: [0] near-tie targets, [1] other exact-scan targets
+    atomicAdd(&A.counters[0], nflag);
+    atomicAdd(&A.counters[1], nscan - nflag);
+  }
+  // ---- Φ_0 to HBM in the generic layout [L][RP] (the backtrack's argmin reads it): this segment's rows -----
+  double *f0 = A.front0 + (size_t)k * A.front_stride;
+  const int chi = q == S - 1 ? P.RP : hi;
+  for (int e = tid; e < L * (chi - lo); e += nthr) {
+    const int l = e / (chi - lo), c = lo + e % (chi - lo);
+    f0[(size_t)l * P.RP + c] = c < R ? F[(c - lo) * FS + l] : INFINITY;
+  }
+}
+
+// ---- host side ---------------------------------------------------------------------------------------------
+namespace {
+bool fsep2_shape(const PyrGeom &G) {
+  const int n0 = G.n[0], n1 = G.n[1];
+  return G.M == 2 && ((n0 == 6 && n1 == 6) || (n0 == 4 && n1 == 4) || (n0 == 8 && n1 == 8) || (n0 == 8 && n1 == 4));
+}
+template <bool SEG>
+const void *fsep2_fn_t(const PyrGeom &G) {
+  return G.n[0] == 6 ? (const void *)k_fsep2<6, 6, SEG>
+         : G.n[0] == 4 ? (const void *)k_fsep2<4, 4, SEG>
+         : G.n[1] == 8 ? (const void *)k_fsep2<8, 8, SEG>
+                       : (const void *)k_fsep2<8, 4, SEG>;
+}
+const void *fsep2_fn(const PyrGeom &G, int S) { return S > 1 ? fsep2_fn_t<true>(G) : fsep2_fn_t<false>(G); }
+}  // namespace
+
+bool fsep2_plan(const PyrGeom &G, int B, int S, FsepPlan *out) {
+  if (!fsep2_shape(G) || B < 0 || S < 1) return false;
+  const int L = G.n[0] * G.n[1], SMAX = G.n[0] + G.n[1] - 2, ND = SMAX + 1, FS = (L + 1) | 1, R = B + 1;
+  FsepPlan p;
+  p.S = S;
+  if (S == 1) {
+    p.W = std::max(1, (R - 1 + 31) / 32);  // lane pairs for rows 0 .. 32W-1; row B beyond them is the extra row
+    p.RS = 32 * p.W;
+    p.rows = R;
+  } else {
+    p.RS = 32 * std::max(1, (R - 1 + 32 * S - 1) / (32 * S));
+    p.W = p.RS / 32;
+    if ((S - 1) * p.RS >= R || p.RS < SMAX + 1) return false;  // an empty last segment / a halo past the next one
+    p.rows = std::min(R, p.RS + 1 + SMAX);
+  }
+  if (64 * p.W > FS2_MAXT) return false;
+  if (S > 1 && SMAX * L > 8 * 64 * p.W) return false;  // inbox cells per thread
+  p.koff = (p.rows * FS + 1) / 2 * 2;
+  p.lds = (size_t)(p.koff + L * ND) * sizeof(double);
+  if (p.lds > 160 * 1024) return false;
+  p.threads = 64 * p.W;
+  if (out) *out = p;
+  return true;
+}
+
+int fsep2_blocks_per_cu(const PyrGeom &G, const FsepPlan &p) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fsep2_fn(G, p.S), p.threads, p.lds) != hipSuccess) return 0;
+  return n;
+}
+
+hipError_t launch_fsep2(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, const FsepPlan &p,
+                        double *front0, size_t front_stride, uint8_t *U, size_t u_stride_k, int32_t *counters,
+                        double *ring, int NB, int32_t *flags, unsigned spin_limit) {
+  if (P.M != 2 || !fsep2_shape(G)) return hipErrorInvalidValue;
+  FsepArgs A;
+  A.front0 = front0;
+  A.front_stride = front_stride;
+  A.U = U;
+  A.u_stride_k = u_stride_k;
+  A.counters = counters;
+  A.ring = ring;
+  A.flags = flags;
+  A.S = p.S;
+  A.RS = p.RS;
+  A.NB = NB;
+  A.koff = p.koff;
+  A.spin_limit = spin_limit;
+  A.base0 = G.base[0];
+  A.base1 = G.base[1];
+  ProblemDev Pc = P;
+  LevelsDev Lc = Lv;
+  const dim3 grid((unsigned)(P.K * p.S)), block((unsigned)p.threads);
+  if (p.S > 1) {  // the segments of a subproblem wait for each other: every workgroup must be resident
+    void *args[] = {&Pc, &Lc, &A};
+    return hipLaunchCooperativeKernel(fsep2_fn(G, p.S), grid, block, args, (unsigned)p.lds, s);
+  }
+  void *args[] = {&Pc, &Lc, &A};
+  return hipLaunchKernel(fsep2_fn(G, p.S), grid, block, args, p.lds, s);
+}
+
+#if defined(MIOC_STAMPS)
+extern "C" int32_t mioc_debug_fsep_stamps(unsigned long long *out, int64_t nwaves) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fs_stamps), (size_t)nwaves * 8 * sizeof(unsigned long long)) ==
+                 hipSuccess
+             ? 0
+             : -4;
+}
+#endif
+
+}  // namespace mioc

@@ -120,6 +120,19 @@ bool fsep_supported(const PyrGeom &G, int B, size_t *lds_out, int *threads_out);
 int fused_blocks_per_cu(int algo_sep, const PyrGeom &G, int L, int B);  // occupancy query (diagnostics [7])
 hipError_t launch_fsep_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, double *front0,
                            size_t front_stride, uint8_t *U, size_t u_stride_k, int32_t *counters);
+// ... round-3 layout (mioc_fsep.hip): two lanes per row, the front updated in place, optionally S row segments per
+// subproblem on S workgroups chained by an outbox ring (strong scaling)
+struct FsepPlan {
+  int S = 1, RS = 0, W = 0;  // segments, rows per segment (multiple of 32), waves per workgroup
+  int rows = 0, koff = 0;    // LDS front rows, K table offset (doubles)
+  int threads = 0;
+  size_t lds = 0;
+};
+bool fsep2_plan(const PyrGeom &G, int B, int S, FsepPlan *out);
+int fsep2_blocks_per_cu(const PyrGeom &G, const FsepPlan &p);
+hipError_t launch_fsep2(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, const FsepPlan &p,
+                        double *front0, size_t front_stride, uint8_t *U, size_t u_stride_k, int32_t *counters,
+                        double *ring, int NB, int32_t *flags, unsigned spin_limit);
 
 // ---- p = Inf collapse (mioc_pinf.hip) -----------------------------------------------------------
 struct PinfDev {
@@ -241,6 +254,12 @@ struct mioc_ctx {
   unsigned spin_limit = 1u << 24;  // persistent DP: polls before a dependency wait gives up (MIOC_OPT_SPIN_LIMIT)
   size_t stage_kstride = 0;        // doubles between two subproblems' staging blocks in the last pyramid / sdt DP
   int opt_nb = mioc::kSdtMaxBuffers;    // staging buffers of a persistent separable DP (MIOC_OPT_SDT_BUFFERS)
+  int opt_fsep_seg = 0;            // fused separable DP: row segments (MIOC_OPT_FSEP_SEGMENTS)
+  double *d_ring = nullptr;        // fused separable DP, S > 1: the segments' outbox rings
+  size_t ring_cap = 0;
+  int32_t *d_segflags = nullptr;   // ... and their flags (+ err)
+  size_t segflag_cap = 0;
+  int last_fsep_seg = 0;           // segments of the last fused separable launch (0: the mioc_fused.hip kernel)
   size_t runflag_cap = 0;
   int32_t *h_run_err = nullptr;    // pinned copy of err
   bool run_pending = false;
