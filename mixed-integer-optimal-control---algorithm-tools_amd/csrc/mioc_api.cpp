@@ -386,7 +386,8 @@ int run_bellman(mioc_ctx *ctx) {
       if (v2) ctx->occupancy = fsep2_blocks_per_cu(ctx->pyr, plan);
       if (v2 && S > 1) {
         const int NB = 8, SM = ctx->pyr.n[0] + ctx->pyr.n[1] - 2;
-        rc = grow(ctx, &ctx->d_ring, &ctx->ring_cap, K * (size_t)S * NB * SM * L * sizeof(double), "segment rings");
+        (void)SM;
+        rc = grow(ctx, &ctx->d_ring, &ctx->ring_cap, K * (size_t)S * NB * (size_t)plan.slot_bytes, "segment rings");
         if (!rc) rc = grow(ctx, &ctx->d_segflags, &ctx->segflag_cap, (2 * K * (size_t)S + 1) * sizeof(int32_t),
                            "segment flags");
         if (rc) return rc;

@@ -51,15 +51,42 @@ __device__ __forceinline__ double fs_min(double a, double b) {
   return r;
 }
 
-// merge of two candidate sets in 32-bit fixed point: the smaller, flagged when the two are within tolq (the
-// neighbour's set arrives at distance cost d, +Inf saturating)
-__device__ __forceinline__ unsigned fs_qmerge(unsigned a, unsigned nb, unsigned d, unsigned tolq) {
-  const unsigned t = __builtin_elementwise_add_sat(nb, d);
+// merge of two candidate sets in 32-bit fixed point (finite values < 2^29, +Inf = 2^30, so every operand and sum
+// stays below 2^31): the smaller, flagged (bit 6) when the two are within tolerance.  ntol = -(tolq + 1):
+// |a - t| + ntol has bit 31 set exactly when |a - t| <= tolq.  Five VALU ops.
+__device__ __forceinline__ unsigned fs_qmerge(unsigned a, unsigned nb, unsigned d, unsigned ntol) {
+  const unsigned t = nb + d;
   const unsigned m = min(a, t);
-  unsigned diff;  // |a - t|
-  asm("v_sad_u32 %0, %1, %2, 0" : "=v"(diff) : "v"(a), "v"(t));
-  return m | (diff <= tolq ? (unsigned)FS2_FLAG : 0u);
+  unsigned x;
+  asm("v_sad_u32 %0, %1, %2, %3" : "=v"(x) : "v"(a), "v"(t), "v"(ntol));
+  return m | ((x >> 25) & (unsigned)FS2_FLAG);
 }
+
+__device__ __forceinline__ double fs_max(double a, double b) {  // v_max_f64 without the canonicalising operands
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+template <int CTRL>
+__device__ __forceinline__ double fs_dpp(double x) {
+  return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false),
+                          __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double fs_rdl(double x, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l), __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+// minimum over the wave: DPP within each row of 16 lanes (quad swaps, half-row and row mirrors), then the four
+// rows' lane 0, 16, 32, 48
+__device__ __forceinline__ double fs_wave_min(double v) {
+  v = fs_min(v, fs_dpp<0xB1>(v));
+  v = fs_min(v, fs_dpp<0x4E>(v));
+  v = fs_min(v, fs_dpp<0x141>(v));
+  v = fs_min(v, fs_dpp<0x140>(v));
+  return fs_min(fs_min(fs_rdl(v, 0), fs_rdl(v, 16)), fs_min(fs_rdl(v, 32), fs_rdl(v, 48)));
+}
+
+typedef unsigned fs_u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ unsigned fs_swap_u(unsigned x) {
   return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
@@ -74,21 +101,12 @@ __device__ __forceinline__ double fs_swap(double x) {
 
 __device__ __forceinline__ int fs_uint(double u) { return (int)fmin(fmax(u, -1.0e8), 1.0e8); }
 
-__device__ __forceinline__ double fs_ld(const double *p) {
-  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p),
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void fs_st(double *p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 }  // namespace
 
 // diagnostic build (make stamps): per-wave phase cycles (s_memtime), summed over the steps
 #if defined(MIOC_STAMPS)
 __device__ unsigned long long g_fs_stamps[4096][8];
-#define FS_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define FS_T(v) [[maybe_unused]] unsigned long long v = __builtin_amdgcn_s_memtime()
 #define FS_ACC(q, a, b) acc[q] += (b) - (a)
 #else
 #define FS_T(v)
@@ -105,18 +123,20 @@ struct FsepArgs {
   int32_t *flags;  // [K][S][2] {outbox token, consumed token}, then the error flag at [2·K·S]
   int S, RS, NB;   // segments, rows per segment (a multiple of 32), ring depth
   int koff;        // K table offset in the LDS (doubles)
+  int stg;         // S > 1: the inbox staging rows in the LDS (doubles)
+  int slot_bytes;  // S > 1: bytes per ring slot (SMAX·L doubles, rounded up to 1 KiB: whole LDS-DMA chunks)
   unsigned spin_limit;
   int base0, base1;
 };
 
 template <int N0, int N1, bool SEG>
-__global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, FsepArgs A) {
+__global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG && N0 * N1 <= 36 ? 4 : 2))) void k_fsep2(
+    ProblemDev P, LevelsDev Lv, FsepArgs A) {
   constexpr int L = N0 * N1, H = N1 / 2, V = N0 * H, SMAX = N0 + N1 - 2, ND = SMAX + 1;
   constexpr int FS = (L + 1) | 1;  // odd row stride (8-byte words)
   static_assert(N1 % 2 == 0 && N0 <= 8 && N1 <= 8 && V <= 32, "grid shape");
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
   __shared__ int s_stop;
-  constexpr int NIN = 8;  // inbox cells per thread (host: SMAX·L <= 8·threads)
   const int S = SEG ? A.S : 1, k = (int)blockIdx.x / S, q = (int)blockIdx.x - k * S;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nthr = blockDim.x, nw = nthr >> 6;
   const int B = P.B, R = B + 1, nt = P.nt, NB = A.NB;
@@ -124,15 +144,20 @@ __global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, 
   const int nloc = min(R, hi + SMAX) - lo;  // LDS rows: own rows, then the outbox halo
   double *const F = reinterpret_cast<double *>(fsm);
   double *const Kt = F + A.koff;
+  // d(l, j), the L1 distance of two levels, one byte each (static: built once)
+  unsigned char *const Dt = reinterpret_cast<unsigned char *>(Kt + L * ND);
   const int cx = lo + (nthr >> 1);  // past the lane pairs: the extra row (row B) when cx < hi
   const double beta = Lv.beta, inv = Lv.inv_beta;
   const double numx0 = (double)max(abs(A.base0), abs(A.base0 + N0 - 1)),
                numx1 = (double)max(abs(A.base1), abs(A.base1 + N1 - 1));
   int32_t *const fl = A.flags + 2 * ((size_t)k * S + q);
   int32_t *const err = A.flags + 2 * (size_t)P.K * S;
-  const size_t ring_seg = (size_t)NB * SMAX * L;
-  double *const ring_out = A.ring + ((size_t)k * S + q) * ring_seg;
-  const double *const ring_in = A.ring + ((size_t)k * S + (q > 0 ? q - 1 : 0)) * ring_seg;
+  // rings through buffer resources (32-bit offsets, sc1 accesses); the inbox slot is copied into the LDS staging
+  // rows by LDS-DMA (no registers held across the read phase)
+  const size_t ring_seg = SEG ? (size_t)NB * A.slot_bytes : 0;
+  const __amdgpu_buffer_rsrc_t ring_out =
+      __builtin_amdgcn_make_buffer_rsrc((char *)A.ring + ((size_t)k * S + q) * ring_seg, 0, (int)ring_seg, 0x00020000);
+  const char *const ring_in = (const char *)A.ring + ((size_t)k * S + (q > 0 ? q - 1 : 0)) * ring_seg;
 
   auto inputs = [&](int s, double &a0, double &a1, double &u0, double &u1) {
     const double *dfs = P.df + ((size_t)k * nt + s) * 2;
@@ -190,6 +215,10 @@ __global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, 
       cu1 = fs_uint(u1);
     }
     if (tid == 0) s_stop = 0;
+    for (int e = tid; e < L * L; e += nthr) {
+      const int l = e / L, j = e - l * L;
+      Dt[e] = (unsigned char)(abs(l % N0 - j % N0) + abs(l / N0 - j / N0));
+    }
   }
   __syncthreads();
   uint8_t *Uk = A.U + (size_t)k * A.u_stride_k;
@@ -240,42 +269,45 @@ __global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, 
 #pragma unroll
     for (int j = 1; j < V; ++j) {
       pmn = fs_min(pmn, o[j]);
-      pmx = fmax(pmx, o[j]);
+      pmx = fs_max(pmx, o[j]);
     }
     pmn = fs_min(pmn, fs_swap(pmn));
-    pmx = fmax(pmx, fs_swap(pmx));
+    pmx = fs_max(pmx, fs_swap(pmx));
     const bool infrow = !(pmx < INFINITY);
     if (__ballot(infrow && pmn < INFINITY)) {  // some sources unreachable: the maximum over the finite ones
       double m2 = pmn;
 #pragma unroll
-      for (int j = 0; j < V; ++j) m2 = fmax(m2, o[j] < INFINITY ? o[j] : pmn);
-      pmx = fmax(m2, fs_swap(m2));
+      for (int j = 0; j < V; ++j) m2 = fs_max(m2, o[j] < INFINITY ? o[j] : pmn);
+      pmx = fs_max(m2, fs_swap(m2));
     }
-    // ---- 32-bit fixed point: A_j = trunc((Ψ_j - Ψmin)/β · 2^Fb) << 7 | x0 | x1 << 3, +Inf = 0xFFFFFFFF --------
-    // (β units, grid g = 2^-Fb; every candidate value A + d·2^(Fb+7) stays below 2^31, so unit steps are exact
-    // integer additions and +Inf saturates)
+    // ---- 32-bit fixed point: A_j = trunc((Ψ_j - Ψmin)/β · 2^Fb) << 7 | j (rank), +Inf = 2^30 -----------------
+    // (β units, grid g = 2^-Fb; every finite candidate value A + d·2^(Fb+7) stays below 2^29, so unit steps are
+    // exact integer additions; +Inf plus any distance stays in [2^30, 2^31))
     const double rs = (pmx - pmn) * inv + (double)SMAX;  // scaled range of every candidate value
-    const bool scale_ok = rs < 0x1p19;
-    const int E = ilogb(fmin(rs, 0x1p19) * (1.0 + 0x1p-20) + 1.0) + 1;  // 2^E > rs
-    const int Fb = 24 - E;
+    const bool scale_ok = rs < 0x1p17;
+    const int E = ilogb(fmin(rs, 0x1p17) * (1.0 + 0x1p-20) + 1.0) + 1;  // 2^E > rs
+    const int Fb = 22 - E;
     const double g = ldexp(1.0, -Fb);
     const double qmax = beta * (double)SMAX + fmax(fabs(pmn), fabs(pmx)) + fabs(a0) * numx0 + fabs(a1) * numx1;
-    // 2 x stamping error (< g) + 2 x the reference's rounding (<= 4u·qmax per candidate), in units of β
+    // 2 x stamping error (< g, the fma's rounding included) + 2 x the reference's rounding (<= 4u·qmax per
+    // candidate), in units of β
     const double tol = 3.0 * g + 0x1p-49 * qmax * inv;
     const bool none = !(pmn < INFINITY);
     const bool direct = !none && !(scale_ok && tol < 0.25);
     const double sc = ldexp(inv, Fb);
-    const unsigned U1 = 1u << (Fb + 7);                                    // one unit of distance
-    const unsigned tolq = direct ? 0u : (unsigned)(tol * ldexp(1.0, Fb + 7));  // |A - T| <= tolq <=> within tol
+    const unsigned U1 = 1u << (Fb + 7);  // one unit of distance
+    const unsigned ntol = direct ? ~0u : ~(unsigned)(tol * ldexp(1.0, Fb + 7));  // -(tolq + 1)
     if (none) pmn = 0.0;
+    const double c0 = -pmn * sc;
     unsigned a[V];
 #pragma unroll
     for (int s = 0; s < H; ++s)
 #pragma unroll
       for (int x0 = 0; x0 < N0; ++x0) {
         const int t = x0 + N0 * s;
-        const unsigned q0 = (unsigned)((o[t] - pmn) * sc) << 7 | (unsigned)(x0 | x1v[s] << 3);
-        a[t] = o[t] < INFINITY ? q0 : 0xFFFFFFFFu;
+        // +Inf converts to 0xFFFFFFFF (clamped), which the min turns into 2^30
+        const unsigned q0 = (unsigned)__builtin_fma(o[t], sc, c0) << 7 | (unsigned)(x0 + N0 * x1v[s]);
+        a[t] = min(q0, 0x40000000u);
       }
     __builtin_amdgcn_sched_barrier(0);
     FS_T(q1);
@@ -283,70 +315,77 @@ __global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, 
 #pragma unroll
     for (int s = 0; s < H; ++s) {
 #pragma unroll
-      for (int x0 = 1; x0 < N0; ++x0) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[s * N0 + x0 - 1], U1, tolq);
+      for (int x0 = 1; x0 < N0; ++x0) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[s * N0 + x0 - 1], U1, ntol);
 #pragma unroll
-      for (int x0 = N0 - 2; x0 >= 0; --x0) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[s * N0 + x0 + 1], U1, tolq);
+      for (int x0 = N0 - 2; x0 >= 0; --x0) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[s * N0 + x0 + 1], U1, ntol);
     }
     // ---- pass along x1: this lane's H slots (orientation-free), then the partner's boundary slot ------------
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
 #pragma unroll
-      for (int s = 1; s < H; ++s) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[(s - 1) * N0 + x0], U1, tolq);
+      for (int s = 1; s < H; ++s) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[(s - 1) * N0 + x0], U1, ntol);
 #pragma unroll
-      for (int s = H - 2; s >= 0; --s) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[(s + 1) * N0 + x0], U1, tolq);
+      for (int s = H - 2; s >= 0; --s) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[(s + 1) * N0 + x0], U1, ntol);
     }
 #pragma unroll
     for (int x0 = 0; x0 < N0; ++x0) {
       const unsigned pb = fs_swap_u(a[(H - 1) * N0 + x0]);
 #pragma unroll
-      for (int t = 0; t < H; ++t) a[(H - 1 - t) * N0 + x0] = fs_qmerge(a[(H - 1 - t) * N0 + x0], pb, (t + 1) * U1, tolq);
+      for (int t = 0; t < H; ++t) a[(H - 1 - t) * N0 + x0] = fs_qmerge(a[(H - 1 - t) * N0 + x0], pb, (t + 1) * U1, ntol);
     }
     __builtin_amdgcn_sched_barrier(0);
     FS_T(q2);
     // ---- the segment below has published this step's outbox: load it (consumed in the write phase) --------
-    double inb[SEG ? NIN : 1];
-    if (SEG) {
-#pragma unroll
-      for (int u = 0; u < NIN; ++u) inb[u] = INFINITY;
-      if (q > 0 && wait_flag(fl - 2, vin, need_in)) {
-        const double *slot = ring_in + (size_t)(i % NB) * SMAX * L;
-#pragma unroll
-        for (int u = 0; u < NIN; ++u)
-          if (tid + u * nthr < SMAX * L) inb[u] = fs_ld(slot + tid + u * nthr);
+    if (SEG && q > 0 && wait_flag(fl - 2, vin, need_in)) {
+      // LDS-DMA of the slot, 1 KiB chunks by wave (inline asm: the compiler does not make later LDS accesses
+      // wait for it; the drain before barrier 1 completes it, the barrier publishes it)
+      const char *slot = ring_in + (size_t)(i % NB) * A.slot_bytes;
+      const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)(fsm)) + A.stg * 8u;
+      for (int c = w; c < A.slot_bytes / 1024; c += nw) {
+        const char *gsrc = slot + c * 1024 + lane * 16;
+        const unsigned m0 = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)c * 1024u);
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(gsrc), "s"(m0)
+                     : "memory");
       }
     }
     // ---- winners: R(l, j*) = fl(K_l[d(l, j*)] + Ψ_j*) for the certified winner j* ----------------------------
+    // b̃_l = |ν0 - u0| + |ν1 - u1| splits into a wave-uniform x0 part (SGPRs) and this lane's x1 part per slot
     unsigned vmask = 0, smask = 0;
     const unsigned dirb = direct ? 1u : 0u;
     uint32_t jw[(V + 3) / 4];
 #pragma unroll
     for (int u = 0; u < (V + 3) / 4; ++u) jw[u] = 0;
+    const double *const Frow = F + cl * FS;
 #pragma unroll
     for (int s = 0; s < H; ++s) {
+      const int x1 = x1v[s];
+      const int rr = abs(A.base1 + x1 - su1) - room - 1;  // + |ν0 - u0| < 0  <=>  b̃_l <= room
+      const double *const Ks = Kt + N0 * x1 * ND;         // K_l[·] of l = x0 + N0·x1 at Ks + x0·ND
+      const unsigned char *const Ds = Dt + N0 * x1 * L;   // d(l, ·) at Ds + x0·L
       double kv[N0], pv[N0];
-      int jj[N0];
 #pragma unroll
       for (int x0 = 0; x0 < N0; ++x0) {
-        const int t = x0 + N0 * s, x1 = x1v[s], l = x0 + N0 * x1;
-        const int yl = (int)a[t];
-        const int wx0 = yl & 7, wx1 = (yl >> 3) & 7;
-        jj[x0] = wx0 + N0 * wx1;
-        const int d = abs(x0 - wx0) + abs(x1 - wx1);
-        kv[x0] = Kt[l * ND + min(d, SMAX)];
-        pv[x0] = F[cl * FS + jj[x0]];
+        const unsigned jx = a[x0 + N0 * s] & 63u;
+        kv[x0] = Ks[x0 * ND + Ds[x0 * L + jx]];
+        pv[x0] = Frow[jx];
       }
 #pragma unroll
       for (int x0 = 0; x0 < N0; ++x0) {
         const int t = x0 + N0 * s;
+        const unsigned av = a[t];
         // the mask bits as integer arithmetic (shift-or with an inline shift count; a condition would become a
         // select between 0 and a materialised 1 << t in a register per bit)
-        const unsigned vb = ((unsigned)(room - btl(x0, x1v[s])) >> 31) ^ 1u;  // b̃_l <= room
-        const unsigned fb = min(~a[t], 1u);                                     // finite
-        const unsigned gb = (a[t] >> 6) & 1u;                                   // near-tie flag
+        const unsigned vb = (unsigned)(rr + abs(A.base0 + x0 - su0)) >> 31;  // b̃_l <= room
+        const bool fin = av < 0x40000000u;
+        const unsigned gb = (av >> 6) & 1u;                                  // near-tie flag
         vmask |= vb << t;
-        smask |= (vb & (dirb | (fb & gb))) << t;
-        o[t] = (vb & fb) ? kv[x0] + pv[x0] : INFINITY;
-        jw[t >> 2] |= (uint32_t)(jj[x0] & 0xFF) << (8 * (t & 3));
+        smask |= (vb & (dirb | (fin ? gb : 0u))) << t;
+        const double sum = kv[x0] + pv[x0];
+        o[t] = fin ? sum : INFINITY;
+        jw[t >> 2] |= (av & 63u) << (8 * (t & 3));
       }
       __builtin_amdgcn_sched_barrier(0);  // one line's gathers at a time (all in flight would need 4·V VGPRs)
     }
@@ -391,18 +430,9 @@ __global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, 
         double v = INFINITY;
         if (lane < L)
           v = Kt[xl * ND + abs(x0t - lane % N0) + abs(x1t - lane / N0)] + F[(cx - lo) * FS + lane];
-        int j = lane;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-          const double ov = __shfl_xor(v, off);
-          const int oj = __shfl_xor(j, off);
-          if (ov < v || (ov == v && oj < j)) {
-            v = ov;
-            j = oj;
-          }
-        }
-        xv = v;
-        xj = j;
+        xv = fs_wave_min(v);
+        const unsigned long long at = __ballot(v == xv);  // the first source attaining it (iterator order)
+        xj = at ? (int)__builtin_ctzll(at) : 0;
         if (lane == 0) nscan += 1;
       }
     }
@@ -419,46 +449,84 @@ __global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, 
     }
     // ================= write phase: Φ_i ======================================================================
     if (SEG && need_cons != INT_MIN) wait_flag(fl + 3, vcons, need_cons);
-    double *const ring_slot = ring_out + (size_t)(i % NB) * SMAX * L;
     // the write offsets from a second opaque copy of the thread index, taken after the barrier: computed before
     // it, they would stay live through the whole read phase
     int tidw = tid;
     asm volatile("" : "+v"(tidw));
     const int hfw = tidw & 1, cpw = lo + (tidw >> 1);
+    double *const padw = F + (cpw < hi ? cpw - lo : 0) * FS + L;  // this lane pair's pad word (never read)
 #pragma unroll
-    for (int s = 0; s < H; ++s)
+    for (int s = 0; s < H; ++s) {
+      const int x1 = hfw ? N1 - 1 - s : s;
+      const int cb = cpw + abs(A.base1 + x1 - su1);  // target row minus the wave-uniform |ν0 - u0|
+      double *const Fw = F + (int)__umul24((unsigned)(cb - lo), (unsigned)FS) + N0 * x1;
+      // U offset l·R + c, less x0·R + |ν0 - u0| (kept opaque: re-associated, the x0·R terms become a v_mul_lo
+      // per target)
+      int ub = (int)__umul24((unsigned)(N0 * x1), (unsigned)R) + cb;
+      asm volatile("" : "+v"(ub));
 #pragma unroll
       for (int x0 = 0; x0 < N0; ++x0) {
-        const int t = x0 + N0 * s, x1 = hfw ? N1 - 1 - s : s, l = x0 + N0 * x1;
-        if ((vmask >> t) & 1u) {
-          const int c = cpw + btl(x0, x1);
-          F[(c - lo) * FS + l] = o[t];
-          if (SEG && c >= hi) fs_st(ring_slot + (c - hi) * L + l, o[t]);  // the segment above's cell
-        }
-        const int c = cpw + btl(x0, x1);
-        // (l varies across the lane pair: the whole offset goes in the VGPR operand, soffset must stay uniform)
+        const int t = x0 + N0 * s, bx0 = abs(A.base0 + x0 - su0);
+        const bool v = (vmask >> t) & 1u;
+        // branch-free: a target outside the trust region writes this row's pad word (column L) instead
+        double *const dst = v ? Fw + (bx0 * FS + x0) : padw;
+        *dst = o[t];
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(jw[t >> 2] >> (8 * (t & 3))), Ur,
-                                             ((vmask >> t) & 1u) && o[t] < INFINITY ? l * R + c : 0x40000000, 0, 0);
+                                             v && o[t] < INFINITY ? ub + x0 * R + bx0 : 0x40000000, 0, 0);
       }
+    }
+    FS_T(w1);
+    // the outbox: targets above hi (only waves whose rows reach within SMAX of hi), sc1 stores into the ring
+    if (SEG && q < S - 1 && lo + 32 * (w + 1) + SMAX > hi) {
+      const unsigned slot0 = (unsigned)(i % NB) * (unsigned)A.slot_bytes;
+#pragma unroll
+      for (int s = 0; s < H; ++s) {
+        const int x1 = hfw ? N1 - 1 - s : s;
+        const int cb = cpw + abs(A.base1 + x1 - su1);
+#pragma unroll
+        for (int x0 = 0; x0 < N0; ++x0) {
+          const int t = x0 + N0 * s, c = cb + abs(A.base0 + x0 - su0);
+          const bool v = ((vmask >> t) & 1u) && c >= hi;
+          const double ov = o[t];
+          __builtin_amdgcn_raw_buffer_store_b64(
+              (fs_u32x2){(unsigned)__double2loint(ov), (unsigned)__double2hiint(ov)}, ring_out,
+              v ? slot0 + (unsigned)(((c - hi) * L + N0 * x1 + x0) * 8) : 0x80000000u, 0, 16);
+        }
+      }
+    }
     if (xl >= 0 && lane == 0) {
       F[(cx - lo) * FS + xl] = xv;
       __builtin_amdgcn_raw_buffer_store_b8((unsigned char)xj, Ur, xv < INFINITY ? xl * R + cx : 0x40000000, 0, 0);
     }
-    if (SEG && q > 0) {  // the inbox: cells of rows lo .. lo+SMAX-1 whose source row is below lo
-#pragma unroll
-      for (int u = 0; u < NIN; ++u) {
-        const int e = tid + u * nthr;
-        const int c = lo + e / L, l = e % L;
-        const int b = btl(l % N0, l / N0);
-        if (e < SMAX * L && c < hi && c >= b && c - b < lo) F[(c - lo) * FS + l] = inb[u];
+    FS_T(w2);
+    if (SEG && q > 0 && lane < L) {  // the inbox: cells of rows lo .. lo+SMAX-1 whose source row is below lo
+      const int bl = abs(A.base0 + lane % N0 - su0) + abs(A.base1 + lane / N0 - su1);
+      const double *stg = F + A.stg;
+      for (int r = w; r < SMAX; r += nw) {
+        const int c = lo + r;
+        if (c < hi && c >= bl && c - bl < lo) F[r * FS + lane] = stg[r * L + lane];
       }
     }
-    // cells below the target's own budget class: +Inf (target l by wave l % nw)
+    FS_T(w3);
+    // cells below the target's own budget class (c < b̃_l: no source row): +Inf.  On the level grid b̃ <= SMAX, so
+    // these are rows < SMAX, one pass of the workgroup over SMAX·L cells (the first segment only); an off-grid
+    // u_old (wave-uniform test) takes the general loop
+    if (abs(A.base0 - su0) + abs(A.base0 + N0 - 1 - su0) <= N0 - 1 &&
+        abs(A.base1 - su1) + abs(A.base1 + N1 - 1 - su1) <= N1 - 1) {  // u_old(i) inside the grid's box
+      if (lo < SMAX)
+        for (int e = tid; e < SMAX * L; e += nthr) {
+          const int c = e / L, l = e - c * L;
+          if (c >= lo && c < hi && c < btl(l % N0, l / N0)) F[(c - lo) * FS + l] = INFINITY;
+        }
+    } else {
+      const int ws = __builtin_amdgcn_readfirstlane(w);
 #pragma unroll 1
-    for (int l = w; l < L; l += nw) {
-      const int b = min(btl(l % N0, l / N0), hi);
-      for (int c = lo + lane; c < b; c += 64) F[(c - lo) * FS + l] = INFINITY;
+      for (int l = ws; l < L; l += nw) {
+        const int b = min(btl(l % N0, l / N0), hi);
+        for (int c = lo + lane; c < b; c += 64) F[(c - lo) * FS + l] = INFINITY;
+      }
     }
+    FS_T(w4);
     if (i >= 1) prepare(na0, na1);
     ca0 = na0;
     ca1 = na1;
@@ -467,6 +535,16 @@ __global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, 
     FS_T(q6);
     fs_bar();  // ---- Φ_i complete -------------------------------------------------------------------------------
     FS_T(q7);
+#if defined(MIOC_STAMPS_WRITE)  // the write phase in detail
+    FS_ACC(0, q0, q5);
+    FS_ACC(1, q5, w1);
+    FS_ACC(2, w1, w2);
+    FS_ACC(3, w2, w3);
+    FS_ACC(4, w3, w4);
+    FS_ACC(5, w4, q6);
+    FS_ACC(6, q6, q7);
+    FS_ACC(7, q0, q7);
+#else
     FS_ACC(0, q0, q1);
     FS_ACC(1, q1, q2);
     FS_ACC(2, q2, q3);
@@ -475,6 +553,7 @@ __global__ __launch_bounds__(FS2_MAXT) void k_fsep2(ProblemDev P, LevelsDev Lv, 
     FS_ACC(5, q5, q6);
     FS_ACC(6, q6, q7);
     FS_ACC(7, q0, q7);
+#endif
     if (s_stop) break;
   }
 #if defined(MIOC_STAMPS)
@@ -536,9 +615,11 @@ bool fsep2_plan(const PyrGeom &G, int B, int S, FsepPlan *out) {
     p.rows = std::min(R, p.RS + 1 + SMAX);
   }
   if (64 * p.W > FS2_MAXT) return false;
-  if (S > 1 && SMAX * L > 8 * 64 * p.W) return false;  // inbox cells per thread
   p.koff = (p.rows * FS + 1) / 2 * 2;
-  p.lds = (size_t)(p.koff + L * ND) * sizeof(double);
+  p.slot_bytes = (SMAX * L * 8 + 1023) / 1024 * 1024;
+  const int dend = p.koff + L * ND + (L * L + 7) / 8;  // K table, then the distance bytes
+  p.stg = (dend + 1) / 2 * 2;
+  p.lds = (size_t)(S > 1 ? p.stg * 8 + p.slot_bytes : dend * 8);
   if (p.lds > 160 * 1024) return false;
   p.threads = 64 * p.W;
   if (out) *out = p;
@@ -567,6 +648,8 @@ hipError_t launch_fsep2(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv,
   A.RS = p.RS;
   A.NB = NB;
   A.koff = p.koff;
+  A.stg = p.stg;
+  A.slot_bytes = p.slot_bytes;
   A.spin_limit = spin_limit;
   A.base0 = G.base[0];
   A.base1 = G.base[1];

@@ -125,6 +125,7 @@ hipError_t launch_fsep_run(hipStream_t s, const ProblemDev &P, const LevelsDev &
 struct FsepPlan {
   int S = 1, RS = 0, W = 0;  // segments, rows per segment (multiple of 32), waves per workgroup
   int rows = 0, koff = 0;    // LDS front rows, K table offset (doubles)
+  int stg = 0, slot_bytes = 0;  // S > 1: inbox staging offset (doubles), ring slot bytes
   int threads = 0;
   size_t lds = 0;
 };

@@ -8,7 +8,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")
-os.environ["MIOC_LIB"] = os.path.join(PKG, "lib", "libmioc_stamps.so")
+os.environ["MIOC_LIB"] = os.path.join(PKG, "lib", os.environ.get("FS_LIB", "libmioc_stamps.so"))
 sys.path.insert(0, PKG)
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
@@ -50,9 +50,12 @@ with native.Context(0) as ctx:
     buf = (ctypes.c_ulonglong * (nw * 8))()
     assert f(buf, nw) == 0
 a = np.array(buf, dtype=np.float64).reshape(nw, 8) / (nt - 1)
+wpb = 8 if d[8] <= 1 else max(1, 8 // d[8])  # waves per workgroup (B = 256)
+per_wave = a[: (len(a) // wpb) * wpb].reshape(-1, wpb, 8)
 a = a[a[:, 7] > 0]
 us = 1e3 * ms / (nt - 1)
 print(f"{name} K={K} S={d[8]} nt={nt}: {us:.3f} us/step; waves sampled {len(a)}")
 names = ["read+stats+stamp", "passes", "winners", "scans+extra", "drain+barrier1", "write phase", "barrier2", "step"]
 for q, nm in enumerate(names):
-    print(f"  {nm:18s} mean {a[:, q].mean():8.0f}  min {a[:, q].min():8.0f}  max {a[:, q].max():8.0f} cycles/step")
+    print(f"  {nm:18s} mean {a[:, q].mean():8.0f}  min {a[:, q].min():8.0f}  max {a[:, q].max():8.0f} cycles/step"
+          f"   by wave: {[int(x) for x in per_wave[:, :, q].mean(axis=0)]}")
