@@ -569,7 +569,26 @@ def native_name(algo):
         algo, str(algo))
 
 
+def _exit_maps():
+    """MIOC_EXIT_MAPS=path: write /proc/self/maps there at interpreter exit (before the C library's exit handlers
+    run), so that the PCs of a crash inside exit() can be mapped to libraries (the rocprofv3 exit
+    SIGSEGV)."""
+    path = os.environ.get("MIOC_EXIT_MAPS")
+    if not path:
+        return
+    import atexit
+
+    def dump():
+        try:
+            with open("/proc/self/maps") as f, open(path, "w") as g:
+                g.write(f.read())
+        except OSError:
+            pass
+    atexit.register(dump)
+
+
 def main():
+    _exit_maps()
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args))

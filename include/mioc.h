@@ -173,6 +173,33 @@ int32_t mioc_tv_device(mioc_ctx *ctx, int64_t K, const double *d_u, int64_t nx, 
  *   ared = J_old − J_new + β·(tv_old − tv_new);   decision = 2 if pred <= 0 (stop: optimal),
  *   1 if ared < σ·pred (bad step: halve Δ), else 0 (good step: accept).  d_ared nullable; enqueued.
  */
+/*
+ * Device-resident TRM control (multi-trust.jl:92-163) for K restarts, so that the host reads back one flag per
+ * inner-loop chunk instead of K decisions plus stream syncs per inner iteration:
+ *   mioc_trm_state_bytes(K): bytes of the zero-initialised state block the caller allocates on the device
+ *     (offset 0: gate word, 4: any-active word, 8: copy word; then K doubles Δᵏ, K doubles TV_old, K int32 k,
+ *     K int32 flags (1 inner, 2 halved, 4 stopped), K int32 outer iterations per restart).
+ *   mioc_trm_attach(ctx, d_state): while the gate word is 0, the kernels of mioc_backtrack_batch*_device,
+ *     mioc_pred_batch_device, mioc_ode_eval_device and mioc_heat_eval_device return at once; NULL detaches.
+ *   mioc_trm_outer_begin_device: multi-trust.jl:99-107 (TV_old = TV_p(u), Δᵏ = Δ⁰, k = 1, budgets = B, every
+ *     restart not stopped enters its inner loop; the gate opens if any did).
+ *   mioc_trm_inner_end_device: multi-trust.jl:117-158 for the restarts inside their inner loop: pred (with TV_old),
+ *     ared, the decision (written to d_decision if not NULL: 0 accept, 1 halve, 2 stop, -1 not in the loop),
+ *     obj.x = trial, accept / halve / stop, k += 1, the next budgets; the gate stays open while any restart is
+ *     inside its inner loop.  n_per_restart = nt·nx doubles of u, u_old and trial per restart.
+ *   mioc_trm_poll: synchronises the stream once and returns {gate, any-active}.
+ */
+int64_t mioc_trm_state_bytes(int64_t K);
+int32_t mioc_trm_attach(mioc_ctx *ctx, void *d_state);
+int32_t mioc_trm_outer_begin_device(mioc_ctx *ctx, int64_t K, void *d_state, const double *d_tv_u, double D0,
+                                    int64_t B, int32_t *d_budgets);
+int32_t mioc_trm_inner_end_device(mioc_ctx *ctx, int64_t K, void *d_state, double sigma, int64_t kmax, double tau,
+                                  int64_t B, const double *d_int_val, const double *d_tv_new, const double *d_J_new,
+                                  double *d_J_old, double *d_J, double *d_tv_u, int32_t *d_budgets,
+                                  int32_t *d_decision, int64_t n_per_restart, const double *d_trial, double *d_u,
+                                  double *d_u_old);
+int32_t mioc_trm_poll(mioc_ctx *ctx, const void *d_state, int32_t *out);
+
 int32_t mioc_trm_decide_device(mioc_ctx *ctx, int64_t K, const double *d_J_old, const double *d_J_new,
                                const double *d_tv_old, const double *d_tv_new, const double *d_pred, double sigma,
                                double *d_ared, int32_t *d_decision);

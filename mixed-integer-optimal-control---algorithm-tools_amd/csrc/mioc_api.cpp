@@ -85,6 +85,7 @@ ProblemDev problem_dev(const mioc_ctx *ctx) {
   P.df = ctx->d_df;
   P.uold = ctx->d_uold;
   P.Bvec = ctx->Bvec;
+  P.gate = ctx->gate;
   return P;
 }
 
@@ -96,6 +97,7 @@ void free_all(mioc_ctx *ctx) {
   if (ctx->d_ring) hipFree(ctx->d_ring);
   if (ctx->d_segflags) hipFree(ctx->d_segflags);
   if (ctx->h_run_err) hipHostFree(ctx->h_run_err);
+  if (ctx->h_trm_poll) hipHostFree(ctx->h_trm_poll);
   void *ptrs[] = {ctx->d_nuval, ctx->d_nuint,  ctx->d_gidx,      ctx->d_numin,       ctx->d_numax,
                   ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
@@ -932,7 +934,7 @@ int32_t mioc_ode_eval_device(mioc_ctx *ctx, int32_t problem, int64_t K, const do
     if (rc) return rc;
   }
   const double tau = (T1 - T0) / (double)nt;  // ODEObjective.jl: τ = (T1 - T0) / nt
-  HIP_TRY(ctx, launch_ode_eval(ctx->stream, problem, (int)K, (int)nt, tau, par, np - 2, d_x, d_J, d_df,
+  HIP_TRY(ctx, launch_ode_eval(ctx->stream, ctx->gate, problem, (int)K, (int)nt, tau, par, np - 2, d_x, d_J, d_df,
                                ctx->d_ode_state));
   return MIOC_OK;
 }
@@ -1023,6 +1025,7 @@ TrmDev trm_dev(const mioc_ctx *ctx, int mode, int64_t K, int64_t nt) {
   T.p_kind = ctx->p_kind;
   T.p_int = (int)ctx->p_int;
   T.mode = mode;
+  T.gate = ctx->gate;
   T.fma = ctx->pred_fma ? 1 : 0;
   T.df = ctx->d_df;
   T.uold = ctx->d_uold;
@@ -1124,6 +1127,54 @@ int32_t mioc_trm_decide_device(mioc_ctx *ctx, int64_t K, const double *d_J_old, 
     return fail(ctx, MIOC_EINVAL, "null pointer");
   HIP_TRY(ctx, launch_trm_decide(ctx->stream, (int)K, d_J_old, d_J_new, d_tv_old, d_tv_new, d_pred, ctx->beta, sigma,
                                  d_ared, d_decision));
+  return MIOC_OK;
+}
+
+// ---- device-resident TRM control (multi-trust.jl:92-163) ---------------------------------------------------
+int64_t mioc_trm_state_bytes(int64_t K) { return K < 1 || K > 4096 ? -1 : (int64_t)trm_state_bytes((int)K); }
+
+int32_t mioc_trm_attach(mioc_ctx *ctx, void *d_state) {
+  if (!ctx) return MIOC_EINVAL;
+  ctx->gate = static_cast<const int32_t *>(d_state);
+  return MIOC_OK;
+}
+
+int32_t mioc_trm_outer_begin_device(mioc_ctx *ctx, int64_t K, void *d_state, const double *d_tv_u, double D0,
+                                    int64_t B, int32_t *d_budgets) {
+  if (!ctx) return MIOC_EINVAL;
+  if (K < 1 || K > 4096 || !d_state || !d_tv_u || !d_budgets) return fail(ctx, MIOC_EINVAL, "bad TRM state arguments");
+  if (B < 0 || B > (1 << 20) || !std::isfinite(D0)) return fail(ctx, MIOC_EINVAL, "bad budget");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, launch_trm_outer_begin(ctx->stream, (int)K, d_state, d_tv_u, D0, (int)B, d_budgets));
+  return MIOC_OK;
+}
+
+int32_t mioc_trm_inner_end_device(mioc_ctx *ctx, int64_t K, void *d_state, double sigma, int64_t kmax, double tau,
+                                  int64_t B, const double *d_int_val, const double *d_tv_new, const double *d_J_new,
+                                  double *d_J_old, double *d_J, double *d_tv_u, int32_t *d_budgets,
+                                  int32_t *d_decision, int64_t n_per_restart, const double *d_trial, double *d_u,
+                                  double *d_u_old) {
+  if (!ctx) return MIOC_EINVAL;
+  if (!ctx->have_cost) return fail(ctx, MIOC_ESTATE, "mioc_set_cost has not been called");
+  if (K < 1 || K > 4096 || !d_state || !d_int_val || !d_tv_new || !d_J_new || !d_J_old || !d_J || !d_tv_u ||
+      !d_budgets || !d_trial || !d_u || !d_u_old || n_per_restart < 1)
+    return fail(ctx, MIOC_EINVAL, "bad TRM state arguments");
+  if (!(tau > 0.0) || kmax < 0 || B < 0 || B > (1 << 20)) return fail(ctx, MIOC_EINVAL, "bad TRM parameters");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, launch_trm_inner_end(ctx->stream, (int)K, d_state, ctx->beta, sigma, (int)std::min<int64_t>(kmax, INT32_MAX),
+                                    tau, (int)B, d_int_val, d_tv_new, d_J_new, d_J_old, d_J, d_tv_u, d_budgets,
+                                    d_decision, (size_t)n_per_restart, d_trial, d_u, d_u_old));
+  return MIOC_OK;
+}
+
+int32_t mioc_trm_poll(mioc_ctx *ctx, const void *d_state, int32_t *out) {
+  if (!ctx || !d_state || !out) return MIOC_EINVAL;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (!ctx->h_trm_poll) HIP_TRY(ctx, hipHostMalloc(&ctx->h_trm_poll, 16, 0));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->h_trm_poll, d_state, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  out[0] = ctx->h_trm_poll[0];
+  out[1] = ctx->h_trm_poll[1];
   return MIOC_OK;
 }
 

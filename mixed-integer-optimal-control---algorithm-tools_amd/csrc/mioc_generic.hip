@@ -310,6 +310,7 @@ __device__ ArgKey block_argmin(ArgKey mine) {
 
 __global__ __launch_bounds__(1024) void k_generic_argmin0(ProblemDev P, LevelsDev Lv, const double *front0,
                                                           size_t front_stride, int Bu, Start *start) {
+  if (gate_closed(P.gate)) return;
   const int k = blockIdx.x;
   if (P.Bvec) Bu = P.Bvec[k];
   const double *f = front0 + (size_t)k * front_stride;
@@ -365,6 +366,7 @@ hipError_t launch_generic_argmin0(hipStream_t s, const ProblemDev &P, const Leve
 // u_old (the trust-region budget bounds the deviations), B the deviations themselves.
 // ---------------------------------------------------------------------------------------------
 __global__ void k_uold_rank(ProblemDev P, LevelsDev Lv, int32_t *urank) {
+  if (gate_closed(P.gate)) return;
   const int k = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.nt) return;
@@ -453,6 +455,7 @@ template <typename UT>
 __global__ __launch_bounds__(64) void k_generic_walk(ProblemDev P, LevelsDev Lv, const UT *__restrict__ U,
                                                      size_t u_stride_k, const Start *start, const int32_t *urank,
                                                      int32_t *ranks, int32_t *counters) {
+  if (gate_closed(P.gate)) return;
   const int k = blockIdx.x;
   const Start st = start[k];
   if (st.status != MIOC_OK) return;
@@ -480,6 +483,7 @@ hipError_t launch_generic_walk(hipStream_t s, const ProblemDev &P, const LevelsD
 // ---------------------------------------------------------------------------------------------
 __global__ void k_expand(ProblemDev P, LevelsDev Lv, const Start *start, const int32_t *ranks, double *u_out,
                          double *phi_star, int32_t *status) {
+  if (gate_closed(P.gate)) return;
   const int k = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const Start st = start[k];
@@ -510,6 +514,7 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_stage_argmin0(ProblemDev P, LevelsDev Lv, const uint32_t *perm_all,
                                                         const double *S0_all, size_t s_stride, int Bu, Start *start) {
+  if (gate_closed(P.gate)) return;
   const int k = blockIdx.x, L = Lv.L;
   if (P.Bvec) Bu = P.Bvec[k];
   const double *S0 = S0_all + (size_t)k * s_stride;
@@ -555,6 +560,7 @@ hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const Levels
 __global__ __launch_bounds__(64) void k_stage_walk(ProblemDev P, LevelsDev Lv, const uint16_t *__restrict__ UU,
                                                    size_t uu_stride_k, const Start *start, const int32_t *urank,
                                                    int32_t *ranks, int32_t *counters) {
+  if (gate_closed(P.gate)) return;
   const int k = blockIdx.x;
   const Start st = start[k];
   if (st.status != MIOC_OK) return;

@@ -79,6 +79,7 @@ struct HeatArgs {
   double *SC;                       // [tiles][2][Np][16] y, z when they do not fit LDS
   int K, nx, nt, Np;
   double tau, gamma;
+  const int32_t *gate;              // device TRM control gate (see ProblemDev::gate)
 };
 
 // acc1 = A1(tile t) · Bs (and acc2 = A2(t) · Bs when A2) for the two row tiles t0, t1 of this wave (a tile
@@ -135,6 +136,7 @@ __device__ __forceinline__ void heat_barrier() {
 
 template <bool GM>
 __global__ __launch_bounds__(HW * 64) void k_heat_run(HeatArgs H) {
+  if (gate_closed(H.gate)) return;
   extern __shared__ __attribute__((aligned(16))) double hsm[];
   const int Np = H.Np, nx = H.nx, nt = H.nt, E = Np * 16;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, c = lane & 15, tile = blockIdx.x;
@@ -474,6 +476,7 @@ int32_t mioc_heat_eval_device(mioc_ctx *ctx, int64_t K, const double *d_x, doubl
   A.GY = h->d_gy;
   A.K = (int)K, A.nx = (int)h->nx, A.nt = (int)h->nt, A.Np = (int)h->Np;
   A.tau = h->tau, A.gamma = h->gamma;
+  A.gate = ctx->gate;
   A.SC = nullptr;
   if (h->Np > HMAXN_LDS) {
     const size_t sneed = (size_t)tiles * 2 * h->Np * 16 * sizeof(double);

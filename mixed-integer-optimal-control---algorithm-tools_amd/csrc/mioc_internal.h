@@ -44,7 +44,10 @@ struct ProblemDev {
   const double *df = nullptr;      // [K][nt][M]  (each subproblem nx x nt column-major)
   const double *uold = nullptr;    // [K][nt][M]
   const int32_t *Bvec = nullptr;   // backtrack: per-subproblem budget B'_k (null: one B' for the batch)
+  const int32_t *gate = nullptr;   // device TRM control (mioc_trm_attach): backtrack kernels return at once while *gate == 0
 };
+// the kernels of a gated call return at once (uniformly) while the device TRM control's gate word is 0
+__device__ __forceinline__ bool gate_closed(const int32_t *gate) { return gate && *gate == 0; }
 
 // Product grid with consecutive integer levels per dimension (the L1-ball pyramid's domain).
 struct PyrGeom {
@@ -172,6 +175,7 @@ struct TrmDev {
   long long tvw_len = 0;
   double *out_int = nullptr, *out_told = nullptr, *out_tnew = nullptr, *out_pred = nullptr;  // [K] each
   int32_t *err = nullptr;          // bit 0: a TV key / rank outside the weight table
+  const int32_t *gate = nullptr;   // device TRM control gate (see ProblemDev::gate)
 };
 hipError_t launch_trm_pred(hipStream_t s, const TrmDev &T);
 hipError_t launch_trm_decide(hipStream_t s, int K, const double *J_old, const double *J_new, const double *tv_old,
@@ -179,7 +183,15 @@ hipError_t launch_trm_decide(hipStream_t s, int K, const double *J_old, const do
                              int32_t *decision);
 
 hipError_t launch_rand_start(hipStream_t s, int K, int nt, int jumps, uint64_t seed, const LevelsDev &Lv, double *U);
-hipError_t launch_ode_eval(hipStream_t s, int problem, int K, int nt, double tau, const double *params, int y0off,
+// device-resident TRM control (mioc_trm.hip)
+size_t trm_state_bytes(int K);
+hipError_t launch_trm_outer_begin(hipStream_t s, int K, void *state, const double *tv_u, double D0, int B,
+                                  int32_t *budgets);
+hipError_t launch_trm_inner_end(hipStream_t s, int K, void *state, double beta, double sigma, int kmax, double tau,
+                                int B, const double *int_val, const double *tv_new, const double *J_new,
+                                double *J_old, double *J, double *tv_u, int32_t *budgets, int32_t *decision,
+                                size_t n, const double *trial, double *u, double *u_old);
+hipError_t launch_ode_eval(hipStream_t s, const int32_t *gate, int problem, int K, int nt, double tau, const double *params, int y0off,
                            const double *X, double *J, double *DF, double *ST);
 
 struct HeatState;  // mioc_heat.hip: the PDE heat objective's device matrices (mioc_heat_setup)
@@ -255,6 +267,8 @@ struct mioc_ctx {
   unsigned spin_limit = 1u << 24;  // persistent DP: polls before a dependency wait gives up (MIOC_OPT_SPIN_LIMIT)
   size_t stage_kstride = 0;        // doubles between two subproblems' staging blocks in the last pyramid / sdt DP
   int opt_nb = mioc::kSdtMaxBuffers;    // staging buffers of a persistent separable DP (MIOC_OPT_SDT_BUFFERS)
+  const int32_t *gate = nullptr;   // device TRM control (mioc_trm_attach): the state block's gate word
+  int32_t *h_trm_poll = nullptr;   // pinned: the gate and any-active words (mioc_trm_poll)
   int opt_fsep_seg = 0;            // fused separable DP: row segments (MIOC_OPT_FSEP_SEGMENTS)
   double *d_ring = nullptr;        // fused separable DP, S > 1: the segments' outbox rings
   size_t ring_cap = 0;

@@ -121,7 +121,8 @@ struct Hooks<MIOC_ODE_VANDERPOL> {  // p = c[3], y0[2]
 
 template <int PROB>
 __global__ __launch_bounds__(64) void k_ode_eval(int K, int nt, double tau, OdePar P, int y0off, const double *X,
-                                                  double *J, double *DF, double *ST) {
+                                                  double *J, double *DF, double *ST, const int32_t *gate) {
+  if (gate_closed(gate)) return;
   using H = Hooks<PROB>;
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
@@ -166,20 +167,20 @@ __global__ __launch_bounds__(64) void k_ode_eval(int K, int nt, double tau, OdeP
 
 }  // namespace
 
-hipError_t launch_ode_eval(hipStream_t s, int problem, int K, int nt, double tau, const double *params, int y0off,
+hipError_t launch_ode_eval(hipStream_t s, const int32_t *gate, int problem, int K, int nt, double tau, const double *params, int y0off,
                            const double *X, double *J, double *DF, double *ST) {
   OdePar P;
   for (int q = 0; q < 14; ++q) P.p[q] = params[q];
   const dim3 grid((K + 63) / 64), block(64);
   switch (problem) {
     case MIOC_ODE_FISHING:
-      hipLaunchKernelGGL(k_ode_eval<MIOC_ODE_FISHING>, grid, block, 0, s, K, nt, tau, P, y0off, X, J, DF, ST);
+      hipLaunchKernelGGL(k_ode_eval<MIOC_ODE_FISHING>, grid, block, 0, s, K, nt, tau, P, y0off, X, J, DF, ST, gate);
       break;
     case MIOC_ODE_DOUBLETANK:
-      hipLaunchKernelGGL(k_ode_eval<MIOC_ODE_DOUBLETANK>, grid, block, 0, s, K, nt, tau, P, y0off, X, J, DF, ST);
+      hipLaunchKernelGGL(k_ode_eval<MIOC_ODE_DOUBLETANK>, grid, block, 0, s, K, nt, tau, P, y0off, X, J, DF, ST, gate);
       break;
     case MIOC_ODE_VANDERPOL:
-      hipLaunchKernelGGL(k_ode_eval<MIOC_ODE_VANDERPOL>, grid, block, 0, s, K, nt, tau, P, y0off, X, J, DF, ST);
+      hipLaunchKernelGGL(k_ode_eval<MIOC_ODE_VANDERPOL>, grid, block, 0, s, K, nt, tau, P, y0off, X, J, DF, ST, gate);
       break;
     default:
       return hipErrorInvalidValue;

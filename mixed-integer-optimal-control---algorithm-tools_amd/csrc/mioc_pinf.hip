@@ -323,6 +323,7 @@ __device__ __forceinline__ bool pkey_less(const PKey &a, const PKey &b) {
 }
 
 __global__ __launch_bounds__(1024) void k_pinf_start(ProblemDev P, LevelsDev Lv, PinfDev D, int Bu, Start *start) {
+  if (gate_closed(P.gate)) return;
   extern __shared__ __attribute__((aligned(16))) double sR1[];
   __shared__ PKey red[16];
   const int k = blockIdx.x, M = P.M, nt = P.nt;
@@ -419,6 +420,7 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 
 __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, PinfDev D, const Start *start,
                                                    int32_t *ranks, int32_t *nfallback) {
+  if (gate_closed(P.gate)) return;
   extern __shared__ __attribute__((aligned(16))) double wsm[];
   const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
   const int M = P.M, nt = P.nt, RP = P.RP, BWP = D.BWP, CH = D.CH, W = D.W;

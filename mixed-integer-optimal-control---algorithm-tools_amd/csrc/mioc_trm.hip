@@ -20,6 +20,8 @@
 // The file is built with -ffp-contract=off, like the DP kernels.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdint>
 
 #include "mioc_internal.h"
@@ -103,6 +105,7 @@ __device__ __forceinline__ double fold(const double *x, int n, double acc) {
 }
 
 __global__ __launch_bounds__(kTrmThreads) void k_trm_pred(TrmDev T) {
+  if (gate_closed(T.gate)) return;
   __shared__ double s_int[kTrmChunk], s_told[kTrmChunk], s_tnew[kTrmChunk];
   __shared__ int s_err;
   const int k = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -182,7 +185,153 @@ __global__ void k_trm_decide(int K, const double *J_old, const double *J_new, co
   decision[k] = (p <= 0.0) ? 2 : (a < sigma * p) ? 1 : 0;
 }
 
+// ---- device-resident TRM control (multi-trust.jl:92-163) for K restarts ------------------------------------
+// State block (TrmState, laid out by trm_state_layout): the gate word (any restart inside its inner loop: the
+// gated kernels of an inner iteration return at once while it is 0), the any-active word (any restart not
+// stopped), the copy word (any trial to copy), then per restart Δᵏ, TV_old, k, flags, outer iterations.
+constexpr int TRM_INNER = 1, TRM_HALVED = 2, TRM_STOP = 4, TRM_COPY_U = 8, TRM_COPY_UOLD = 16;
+
+struct TrmState {
+  int32_t *gate, *any_active, *any_copy;
+  double *Dk, *tv_old;
+  int32_t *k, *flags, *iters;
+};
+__host__ __device__ inline TrmState trm_state_layout(void *base, int K) {
+  TrmState S;
+  char *b = static_cast<char *>(base);
+  S.gate = reinterpret_cast<int32_t *>(b);
+  S.any_active = S.gate + 1;
+  S.any_copy = S.gate + 2;
+  S.Dk = reinterpret_cast<double *>(b + 16);
+  S.tv_old = S.Dk + K;
+  S.k = reinterpret_cast<int32_t *>(S.tv_old + K);
+  S.flags = S.k + K;
+  S.iters = S.flags + K;
+  return S;
+}
+
+// block-wide OR of one flag per thread into *out (one workgroup)
+__device__ __forceinline__ void trm_block_or(int v, int32_t *out) {
+  __shared__ int s_or;
+  if (threadIdx.x == 0) s_or = 0;
+  __syncthreads();
+  if (__ballot(v) && (threadIdx.x & 63) == 0) atomicOr(&s_or, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) *out = s_or;
+}
+
+// start of an outer iteration, multi-trust.jl:99-107: TV_old = TV_p(u), Δᵏ = Δ⁰, k = 1, every restart that has not
+// stopped enters its inner loop with the full budget B; the gate opens if any did
+__global__ __launch_bounds__(1024) void k_trm_outer_begin(int K, TrmState S, const double *tv_u, double D0, int B,
+                                                          int32_t *budgets) {
+  int any = 0;
+  for (int r = threadIdx.x; r < K; r += blockDim.x) {
+    const int f = S.flags[r];
+    const bool active = !(f & TRM_STOP);
+    S.tv_old[r] = tv_u[r];
+    S.Dk[r] = D0;
+    S.k[r] = 1;
+    S.flags[r] = active ? TRM_INNER : f & TRM_STOP;
+    S.iters[r] += active ? 1 : 0;
+    budgets[r] = B;
+    any |= active ? 1 : 0;
+  }
+  trm_block_or(any, S.gate);
+  if (threadIdx.x == 0) {
+    *S.any_active = *S.gate;
+    *S.any_copy = 0;
+  }
+}
+
+// end of an inner iteration, multi-trust.jl:117-158 for every restart still inside its inner loop: pred with the
+// outer iteration's TV_old, ared and the decision (the reference's expressions, as k_trm_decide), obj.x = the
+// trial (copied by k_trm_copy), accept (u_old = trial, J_old = J = J_new, TV_old = TV_new), halve Δᵏ, or stop
+// (J = J_old); k += 1; the next budget floor(Δᵏ/Δt) after a halving; the gate stays open while any restart is
+// inside its inner loop (k <= kmax, no accept, no stop)
+__global__ __launch_bounds__(1024) void k_trm_inner_end(int K, TrmState S, double beta, double sigma, int kmax,
+                                                        double tau, int B, const double *int_val, const double *tv_new,
+                                                        const double *J_new, double *J_old, double *J, double *tv_u,
+                                                        int32_t *budgets, int32_t *decision) {
+  int any_inner = 0, any_act = 0, any_cp = 0;
+  for (int r = threadIdx.x; r < K; r += blockDim.x) {
+    int f = S.flags[r] & ~(TRM_COPY_U | TRM_COPY_UOLD);
+    if (f & TRM_INNER) {
+      const double tvo = S.tv_old[r], tvn = tv_new[r];
+      const double pred = int_val[r] + beta * (tvo - tvn);                 // multi-trust.jl:126
+      const double ared = (J_old[r] - J_new[r]) + beta * (tvo - tvn);      // :128
+      const int d = (pred <= 0.0) ? 2 : (ared < sigma * pred) ? 1 : 0;     // :130, :140
+      if (decision) decision[r] = d;
+      f |= TRM_COPY_U;                                                     // obj.x = the trial, accepted or not
+      tv_u[r] = tvn;
+      if (d == 2) {                                                        // stop, J = J_old, :130-138
+        J[r] = J_old[r];
+        f |= TRM_STOP;
+        f &= ~TRM_INNER;
+      } else if (d == 0) {                                                 // accept, :148-154
+        f |= TRM_COPY_UOLD;
+        J_old[r] = J_new[r];
+        J[r] = J_new[r];
+        S.tv_old[r] = tvn;
+        f &= ~TRM_INNER;
+      } else {                                                             // halve Δᵏ, :140-146
+        S.Dk[r] = S.Dk[r] / 2;
+        f |= TRM_HALVED;
+      }
+      const int k = S.k[r] + 1;
+      S.k[r] = k;
+      if (k > kmax) f &= ~TRM_INNER;
+      budgets[r] = (f & TRM_HALVED) ? (int)floor(S.Dk[r] / tau) : B;      // B_new = floor(Δᵏ/Δt), :109
+      any_cp = 1;
+    } else if (decision) {
+      decision[r] = -1;
+    }
+    S.flags[r] = f;
+    any_inner |= (f & TRM_INNER) ? 1 : 0;
+    any_act |= (f & TRM_STOP) ? 0 : 1;
+  }
+  trm_block_or(any_cp, S.any_copy);
+  trm_block_or(any_act, S.any_active);
+  trm_block_or(any_inner, S.gate);
+}
+
+// the trial into u (every restart of the inner iteration) and into u_old (accepted ones); grid (chunks, K)
+__global__ __launch_bounds__(256) void k_trm_copy(TrmState S, size_t n, const double *trial, double *u, double *u_old) {
+  if (*S.any_copy == 0) return;
+  const int r = blockIdx.y;
+  const int f = S.flags[r];
+  if (!(f & (TRM_COPY_U | TRM_COPY_UOLD))) return;
+  const size_t base = (size_t)r * n;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const double v = trial[base + e];
+    if (f & TRM_COPY_U) u[base + e] = v;
+    if (f & TRM_COPY_UOLD) u_old[base + e] = v;
+  }
+}
+
 }  // namespace
+
+size_t trm_state_bytes(int K) { return 16 + (size_t)K * (2 * sizeof(double) + 3 * sizeof(int32_t)); }
+
+hipError_t launch_trm_outer_begin(hipStream_t s, int K, void *state, const double *tv_u, double D0, int B,
+                                  int32_t *budgets) {
+  hipLaunchKernelGGL(k_trm_outer_begin, dim3(1), dim3(1024), 0, s, K, trm_state_layout(state, K), tv_u, D0, B,
+                     budgets);
+  return hipGetLastError();
+}
+
+hipError_t launch_trm_inner_end(hipStream_t s, int K, void *state, double beta, double sigma, int kmax, double tau,
+                                int B, const double *int_val, const double *tv_new, const double *J_new,
+                                double *J_old, double *J, double *tv_u, int32_t *budgets, int32_t *decision,
+                                size_t n, const double *trial, double *u, double *u_old) {
+  const TrmState S = trm_state_layout(state, K);
+  hipLaunchKernelGGL(k_trm_inner_end, dim3(1), dim3(1024), 0, s, K, S, beta, sigma, kmax, tau, B, int_val, tv_new,
+                     J_new, J_old, J, tv_u, budgets, decision);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const unsigned chunks = (unsigned)std::min<size_t>((n + 255) / 256, 64);
+  hipLaunchKernelGGL(k_trm_copy, dim3(chunks, (unsigned)K), dim3(256), 0, s, S, n, trial, u, u_old);
+  return hipGetLastError();
+}
 
 hipError_t launch_trm_pred(hipStream_t s, const TrmDev &T) {
   hipLaunchKernelGGL(k_trm_pred, dim3(T.K), dim3(kTrmThreads), 0, s, T);

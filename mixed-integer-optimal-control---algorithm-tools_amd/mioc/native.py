@@ -43,6 +43,8 @@ EXPORTED = [
     "mioc_pred", "mioc_pred_batch_device", "mioc_tv_device", "mioc_trm_decide_device", "mioc_batch_multi",
     "mioc_ode_eval_device", "mioc_rand_start_device", "mioc_backtrack_batch_budgets_device",
     "mioc_heat_setup", "mioc_heat_eval_device", "mioc_heat_eval",
+    "mioc_trm_state_bytes", "mioc_trm_attach", "mioc_trm_outer_begin_device", "mioc_trm_inner_end_device",
+    "mioc_trm_poll",
 ]
 
 
@@ -109,6 +111,12 @@ def load_library(path=None):
         "mioc_heat_setup": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, vp, vp, vp, vp, vp]),
         "mioc_heat_eval_device": (i32, [vp, i64, vp, vp, vp]),
         "mioc_heat_eval": (i32, [vp, i64, vp, vp, vp]),
+        "mioc_trm_state_bytes": (i64, [i64]),
+        "mioc_trm_attach": (i32, [vp, vp]),
+        "mioc_trm_outer_begin_device": (i32, [vp, i64, vp, vp, dbl, i64, vp]),
+        "mioc_trm_inner_end_device": (i32, [vp, i64, vp, dbl, i64, dbl, i64, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp,
+                                            vp, vp]),
+        "mioc_trm_poll": (i32, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -174,6 +182,7 @@ class Context:
         if rc != MIOC_OK:
             raise MiocNativeError(rc, f"mioc_create(device={device}) failed (no visible HIP device?)")
         self.h = h
+        self.device = int(device)
         self.levels = None
         self.M = None
         self.nt = None
@@ -193,10 +202,11 @@ class Context:
         self.close()
         return False
 
-    def __del__(self):
+    def __del__(self, _finalizing=sys.is_finalizing):
         # an unreferenced context is destroyed while the program runs; at shutdown the atexit handler has
         # already closed it, and a HIP call from a finaliser that runs after the runtime's teardown is unsafe
-        if sys.is_finalizing():
+        # (the default argument keeps the check usable after the sys module is torn down)
+        if _finalizing():
             return
         try:
             self.close()
@@ -336,6 +346,53 @@ class Context:
         K, nt, nx = u.shape
         self._check(self.lib.mioc_tv_device(self.h, K, ctypes.c_void_p(u.data_ptr()), nx, nt,
                                             ctypes.c_void_p(out.data_ptr())))
+
+    # ---- device-resident TRM control (multi-trust.jl:92-163; include/mioc.h) ----------------------------------
+    def trm_state_tensor(self, K):
+        """A zero-initialised device state block for K restarts (uint8 CUDA tensor)."""
+        import torch
+        n = int(self.lib.mioc_trm_state_bytes(int(K)))
+        if n < 0:
+            raise ValueError("K must be in [1, 4096]")
+        return torch.zeros(n, dtype=torch.uint8, device=f"cuda:{self.device}")
+
+    def trm_attach(self, state):
+        """Gate the inner-loop kernels by the state's gate word (None detaches)."""
+        self._check(self.lib.mioc_trm_attach(self.h, ctypes.c_void_p(state.data_ptr()) if state is not None else None))
+
+    def trm_outer_begin(self, state, tv_u, D0, B, budgets):
+        K = tv_u.numel()
+        self._check(self.lib.mioc_trm_outer_begin_device(self.h, K, ctypes.c_void_p(state.data_ptr()),
+                                                          ctypes.c_void_p(tv_u.data_ptr()), float(D0), int(B),
+                                                          ctypes.c_void_p(budgets.data_ptr())))
+
+    def trm_inner_end(self, state, sigma, kmax, tau, B, int_val, tv_new, J_new, J_old, J, tv_u, budgets, trial, u,
+                      u_old, decision=None):
+        K = J.numel()
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        self._check(self.lib.mioc_trm_inner_end_device(
+            self.h, K, p(state), float(sigma), int(kmax), float(tau), int(B), p(int_val), p(tv_new), p(J_new),
+            p(J_old), p(J), p(tv_u), p(budgets), p(decision) if decision is not None else None,
+            u[0].numel(), p(trial), p(u), p(u_old)))
+
+    def trm_state_arrays(self, state, K):
+        """The state block on the host: Δᵏ, TV_old, k, flags (1 inner, 2 halved, 4 stopped), outer iterations."""
+        self.synchronize()
+        b = state.cpu().numpy()
+        o = 16
+        out = {}
+        for name, dt in (("Dk", np.float64), ("tv_old", np.float64), ("k", np.int32), ("flags", np.int32),
+                         ("iters", np.int32)):
+            n = K * np.dtype(dt).itemsize
+            out[name] = b[o:o + n].view(dt).copy()
+            o += n
+        return out
+
+    def trm_poll(self, state):
+        """Synchronise once; (any restart inside its inner loop, any restart not stopped)."""
+        out = np.zeros(2, dtype=np.int32)
+        self._check(self.lib.mioc_trm_poll(self.h, ctypes.c_void_p(state.data_ptr()), _p(out)))
+        return bool(out[0]), bool(out[1])
 
     def trm_decide_tensors(self, J_old, J_new, tv_old, tv_new, pred, sigma, decision, ared=None):
         """multi-trust.jl:127-158 per subproblem: decision (K,) int32 = 2 stop / 1 halve / 0 accept."""

@@ -23,10 +23,15 @@ par = mioc.TRM_parameters(beta=1e-2, Delta0=2.0, p=1, maxiter=maxiter, kmax=10)
 TRM_batch(hp, par, K=16, seed=1)  # warm-up (setup, code objects)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-log = []
-vals, u, iters = TRM_batch(hp, par, K=K, seed=2, log=log)
+stats = {}
+vals, u, iters = TRM_batch(hp, par, K=K, seed=2, stats=stats)  # the product path: no per-trial log
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 print(f"heat TRM_batch: K={K} N={hp.N} nt={nt} maxiter={maxiter}: {dt:.3f} s = {K / dt:.1f} restarts/s; "
-      f"outer iterations mean {iters.mean():.2f}, inner iterations {len(log)}; J+beta*TV min {np.min(vals):.6g} "
-      f"median {np.median(vals):.6g}", flush=True)
+      f"outer iterations {stats['outer']} (per restart mean {iters.mean():.2f}); host read-backs of the control "
+      f"flags {stats['polls']} = {stats['polls'] / max(1, stats['outer']):.2f} per outer iteration; "
+      f"J+beta*TV min {np.min(vals):.6g} median {np.median(vals):.6g}", flush=True)
+log = []
+vals2, _, iters2 = TRM_batch(hp, par, K=K, seed=2, log=log)  # the same run with a per-trial log (debugging)
+print(f"  with the per-trial log: {len(log)} inner iterations, same values: {bool(np.array_equal(vals, vals2))}, "
+      f"same iterations: {bool(np.array_equal(iters, iters2))}", flush=True)
