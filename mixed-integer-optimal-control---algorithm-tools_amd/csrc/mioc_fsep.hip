@@ -372,17 +372,23 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
         kv[x0] = Ks[x0 * ND + Ds[x0 * L + jx]];
         pv[x0] = Frow[jx];
       }
+      // targets of this line inside the trust region: |ν0 - u0| <= room - |ν1 - u1| = -1 - rr is an interval of
+      // x0 around u0 - base0 (wave-uniform), so the line's mask is a bit range
+      {
+        const int thr = -1 - rr, uc = su0 - A.base0;
+        const int x0lo = max(uc - thr, 0), x0hi = min(uc + thr, N0 - 1);
+        const unsigned lm = thr >= 0 && x0lo <= x0hi ? ((2u << x0hi) - (1u << x0lo)) : 0u;
+        vmask |= lm << (N0 * s);
+      }
 #pragma unroll
       for (int x0 = 0; x0 < N0; ++x0) {
         const int t = x0 + N0 * s;
         const unsigned av = a[t];
-        // the mask bits as integer arithmetic (shift-or with an inline shift count; a condition would become a
-        // select between 0 and a materialised 1 << t in a register per bit)
-        const unsigned vb = (unsigned)(rr + abs(A.base0 + x0 - su0)) >> 31;  // b̃_l <= room
+        // flagged and finite (below 2^30): bit 6 set, bit 30 clear -- integer arithmetic, a shift-or per target
+        // (a condition would become a select between 0 and a materialised 1 << t per bit)
+        const unsigned sb = ((av >> 6) & ~(av >> 30)) & 1u;
+        smask |= sb << t;
         const bool fin = av < 0x40000000u;
-        const unsigned gb = (av >> 6) & 1u;                                  // near-tie flag
-        vmask |= vb << t;
-        smask |= (vb & (dirb | (fin ? gb : 0u))) << t;
         const double sum = kv[x0] + pv[x0];
         o[t] = fin ? sum : INFINITY;
         jw[t >> 2] |= (av & 63u) << (8 * (t & 3));
@@ -390,6 +396,8 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
       __builtin_amdgcn_sched_barrier(0);  // one line's gathers at a time (all in flight would need 4·V VGPRs)
     }
     FS_T(q3);
+    // flagged targets count only inside the trust region; a row outside the fixed-point range scans them all
+    smask = dirb ? vmask : smask & vmask;
     // the masks stay VGPR words: seen through, the compiler keeps one 64-bit lane mask per target in SGPRs
     // through the barrier (and spills them)
     asm volatile("" : "+v"(vmask), "+v"(smask));
