@@ -51,8 +51,8 @@ __device__ __forceinline__ double fs_min(double a, double b) {
   return r;
 }
 
-// merge of two candidate sets in 32-bit fixed point (finite values < 2^29, +Inf = 2^30, so every operand and sum
-// stays below 2^31): the smaller, flagged (bit 6) when the two are within tolerance.  ntol = -(tolq + 1):
+// merge of two candidate sets in 32-bit fixed point (finite candidates < 2^30, +Inf = 2^30, so every operand and
+// sum stays below 2^31): the smaller, flagged (bit 6) when the two are within tolerance.  ntol = -(tolq + 1):
 // |a - t| + ntol has bit 31 set exactly when |a - t| <= tolq.  Five VALU ops.
 __device__ __forceinline__ unsigned fs_qmerge(unsigned a, unsigned nb, unsigned d, unsigned ntol) {
   const unsigned t = nb + d;
@@ -281,12 +281,12 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
       pmx = fs_max(m2, fs_swap(m2));
     }
     // ---- 32-bit fixed point: A_j = trunc((Ψ_j - Ψmin)/β · 2^Fb) << 7 | j (rank), +Inf = 2^30 -----------------
-    // (β units, grid g = 2^-Fb; every finite candidate value A + d·2^(Fb+7) stays below 2^29, so unit steps are
-    // exact integer additions; +Inf plus any distance stays in [2^30, 2^31))
+    // (β units, grid g = 2^-Fb with 2^(Fb+7) · rs < 2^30: every finite candidate value A + d·2^(Fb+7) stays below
+    // 2^30, so unit steps are exact integer additions; +Inf plus any distance stays in [2^30, 2^31))
     const double rs = (pmx - pmn) * inv + (double)SMAX;  // scaled range of every candidate value
     const bool scale_ok = rs < 0x1p17;
     const int E = ilogb(fmin(rs, 0x1p17) * (1.0 + 0x1p-20) + 1.0) + 1;  // 2^E > rs
-    const int Fb = 22 - E;
+    const int Fb = 23 - E;
     const double g = ldexp(1.0, -Fb);
     const double qmax = beta * (double)SMAX + fmax(fabs(pmn), fabs(pmx)) + fabs(a0) * numx0 + fabs(a1) * numx1;
     // 2 x stamping error (< g, the fma's rounding included) + 2 x the reference's rounding (<= 4u·qmax per

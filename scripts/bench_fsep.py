@@ -48,6 +48,7 @@ for K in Ks:
         same = "" if ref is None else ("  same" if all(np.array_equal(a, b) for a, b in zip(out, ref)) else "  DIFF")
         ref = ref or out
         print(f"K={K:5d} seg={seg:2d} {name:10s} {ms / n:9.3f} ms/launch = {K * n / ms * 1e3:9.1f} subproblems/s "
-              f"({1e3 * ms / n / (cfg.nt - 1):.3f} us/step) segments={d[8]} occupancy={d[7]} redo={d[6]}{same}",
+              f"({1e3 * ms / n / (cfg.nt - 1):.3f} us/step) segments={d[8]} occupancy={d[7]} redo={d[6]} "
+              f"near-tie scans={d[0]} other scans={d[1]}{same}",
               flush=True)
         ctx.close()
