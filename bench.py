@@ -618,6 +618,9 @@ def main():
                    "unit": "subproblems/s", "ms_per_step": round(1e3 * r2["elapsed"] / r2["steps"], 3),
                    "algorithm": native_name(r2["algo"]), "roofline": roof2, "roofline_valu": valu2,
                    "backtrack_ms": round(r2["walk_ms"] / max(1, r2["steps"]), 3)}
+        if args.solver == "native" and len(r2.get("diag", [])) > 9:  # mioc_diagnostics[9]
+            variant["walk"] = "serial" if r2["diag"][9] < 0 else "segmented"
+            variant["walk_serial_fallbacks"] = max(0, int(r2["diag"][9]))
     def batch_line(cfg_name, total=None):
         r3 = run(args, cfg_name, args.batch_size, None, None, rank, world, device, dist, torch,
                  max(args.steps, 3), args.warmup, total=total)

@@ -76,6 +76,9 @@ extern "C" {
                                     (0, default: chosen from the batch size -- more than one only when the
                                     batch alone cannot fill the GPU; 1..8: forced; -1: the one-lane-per-row
                                     kernel of mioc_fused.hip) */
+#define MIOC_OPT_PINF_WALK 8 /* p=Inf backtrack: 0 (default) the segmented walk -- one subproblem's path spread
+                                over many workgroups -- for batches of at most 64 subproblems with >= 512 steps,
+                                else one serial walk per subproblem; 1: segmented walk forced; -1: serial walk */
 
 typedef struct mioc_ctx mioc_ctx;
 
@@ -283,7 +286,8 @@ int32_t mioc_last_algo(mioc_ctx *ctx);
  * DP, [6] instead counts this context's persistent DPs redone with per-step launches: cooperative launch refused, or
  * a dependency wait timed out -- 0 on a healthy run; after a fused separable DP, the segmented launches redone with
  * one workgroup per subproblem); [7] fused DP: resident workgroups per CU (occupancy query); [8] fused separable DP:
- * row segments per subproblem (0: the one-lane-per-row kernel).  n may be up to 9.
+ * row segments per subproblem (0: the one-lane-per-row kernel); [9] p=Inf segmented walk: subproblems whose path
+ * met a state-dependent step and were walked serially (-1: the serial walk ran for all).  n may be up to 10.
  */
 int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n);
 

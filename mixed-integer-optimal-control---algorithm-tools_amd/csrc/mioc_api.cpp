@@ -101,6 +101,7 @@ void free_all(mioc_ctx *ctx) {
   void *ptrs[] = {ctx->d_nuval, ctx->d_nuint,  ctx->d_gidx,      ctx->d_numin,       ctx->d_numax,
                   ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
+                  ctx->pinf.kabs, ctx->pinf.ftab, ctx->pinf.fseg, ctx->pinf.fneed,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
                   ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm,
                   ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own, ctx->d_ode_state};
@@ -457,6 +458,7 @@ int run_bellman(mioc_ctx *ctx) {
     ctx->pinf_cap_k = std::min(cap_km, std::min(cap_k2, cap_kf));
     pinf_plan((int)RP, (int)nt, D);
     rc = grow(ctx, &D.R, &ctx->pinf_cap_R, K * nt * RP * sizeof(double), "row minima R");
+    if (!rc) rc = grow(ctx, &D.kabs, &ctx->pinf_cap_kabs, K * nt * sizeof(double), "level value bounds");
     if (rc) return rc;
     ev_begin(ctx, 2, "k_pinf_prep");
     HIP_TRY(ctx, launch_pinf_prep(ctx->stream, P, Lv, D));
@@ -516,9 +518,30 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
     ev_end(ctx, 1, 1);
   } else {
     HIP_TRY(ctx, launch_pinf_start(ctx->stream, P, Lv, ctx->pinf, (int)B_use, ctx->d_start));
-    ev_begin(ctx, 1, "k_pinf_walk");
-    HIP_TRY(ctx, launch_pinf_walk(ctx->stream, P, Lv, ctx->pinf, ctx->d_start, ctx->d_ranks, ctx->d_flags + 2));
-    ev_end(ctx, 1, 1);
+    // the segmented walk spreads one subproblem's path over many workgroups: for batches too small to fill the GPU
+    // with one serial walk each (auto: K <= 64 and at least 512 steps)
+    const bool fwalk = ctx->opt_pinf_walk > 0 || (ctx->opt_pinf_walk == 0 && K <= 64 && nt >= 512);
+    ctx->last_pinf_fwalk = fwalk;
+    PinfDev &D = ctx->pinf;
+    if (fwalk) {
+      int G, nseg;
+      pinf_fplan((int)nt, &G, &nseg);
+      rc = grow(ctx, &D.ftab, &ctx->pinf_cap_ftab, K * nt * (size_t)ctx->RP, "segmented walk class table");
+      if (!rc) rc = grow(ctx, &D.fseg, &ctx->pinf_cap_fseg, K * (size_t)nseg * ctx->RP * sizeof(int32_t),
+                         "segmented walk segment maps");
+      if (!rc) rc = grow(ctx, &D.fneed, &ctx->pinf_cap_fneed, (K + 1) * sizeof(int32_t), "segmented walk flags");
+      if (rc) return rc;
+      HIP_TRY(ctx, hipMemsetAsync(D.fneed, 0, (K + 1) * sizeof(int32_t), ctx->stream));
+      ev_begin(ctx, 1, "k_pinf_fwalk");
+      HIP_TRY(ctx, launch_pinf_fwalk(ctx->stream, P, Lv, D, ctx->d_start, ctx->d_ranks));
+      // subproblems whose chain met a state-dependent row: the serial walk (the others return at once)
+      HIP_TRY(ctx, launch_pinf_walk(ctx->stream, P, Lv, D, ctx->d_start, ctx->d_ranks, ctx->d_flags + 2, D.fneed));
+      ev_end(ctx, 1, 1);
+    } else {
+      ev_begin(ctx, 1, "k_pinf_walk");
+      HIP_TRY(ctx, launch_pinf_walk(ctx->stream, P, Lv, D, ctx->d_start, ctx->d_ranks, ctx->d_flags + 2, nullptr));
+      ev_end(ctx, 1, 1);
+    }
   }
   HIP_TRY(ctx, launch_expand(ctx->stream, P, Lv, ctx->d_start, ctx->d_ranks, d_u_out, d_phi_star, d_status));
   ctx->have_path = true;
@@ -641,6 +664,11 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   if (option == MIOC_OPT_SDT_BUFFERS) {
     if (value < 4 || value > kSdtMaxBuffers) return fail(ctx, MIOC_EINVAL, "staging buffers must be in [4, 64]");
     ctx->opt_nb = (int)value;
+    return MIOC_OK;
+  }
+  if (option == MIOC_OPT_PINF_WALK) {
+    if (value < -1 || value > 1) return fail(ctx, MIOC_EINVAL, "p=Inf walk option must be -1, 0 or 1");
+    ctx->opt_pinf_walk = (int)value;
     return MIOC_OK;
   }
   if (option == MIOC_OPT_FSEP_SEGMENTS) {
@@ -1209,9 +1237,13 @@ int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
   const int64_t c6 = ctx->algo == MIOC_ALGO_SEPARABLE || ctx->algo == MIOC_ALGO_FUSED_SEPARABLE
                          ? ctx->n_persist_fallbacks
                          : c[6];
-  const int64_t all[9] = {c[0], c[1], f[2], f[3], c[4], c[5], c6, ctx->occupancy,
-                          ctx->algo == MIOC_ALGO_FUSED_SEPARABLE ? ctx->last_fsep_seg : 0};
-  for (int32_t q = 0; q < n && q < 9; ++q) counters[q] = all[q];
+  // slot 9: after a p=Inf segmented walk, its subproblems left to the serial walk (-1: the serial walk ran alone)
+  int32_t fserial = -1;
+  if (ctx->algo == MIOC_ALGO_PINF && ctx->last_pinf_fwalk && ctx->pinf.fneed)
+    HIP_TRY(ctx, hipMemcpy(&fserial, ctx->pinf.fneed + ctx->K, sizeof fserial, hipMemcpyDeviceToHost));
+  const int64_t all[10] = {c[0], c[1], f[2], f[3], c[4], c[5], c6, ctx->occupancy,
+                           ctx->algo == MIOC_ALGO_FUSED_SEPARABLE ? ctx->last_fsep_seg : 0, fserial};
+  for (int32_t q = 0; q < n && q < 10; ++q) counters[q] = all[q];
   return MIOC_OK;
 }
 

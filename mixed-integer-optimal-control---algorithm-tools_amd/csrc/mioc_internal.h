@@ -146,7 +146,12 @@ struct PinfDev {
   double *k2 = nullptr;            // [K][nt][BWP] second-smallest distinct value in the class
   int32_t *kfirst = nullptr;       // [K][nt][BWP] first rank attaining kmin
   double *R = nullptr;             // [K][nt][RP] row minima R_i[c] = min_r Φ_i[c, r]
+  double *kabs = nullptr;          // [K][nt] max |K_l(i)| over the levels of classes < BW (rounding bound)
   int CH = 0, W = 0;               // the walk's staged steps per chunk and LDS row width (pinf_plan)
+  // segmented walk (mioc_pinf.hip): the step's winning class per row, when it does not depend on the state
+  uint8_t *ftab = nullptr;         // [K][nt][RP] class b* of row c' at step j, 0xFF: state-dependent / +Inf
+  int32_t *fseg = nullptr;         // [K][nseg][RP] row after the G steps of segment g entered at row c' (-1: none)
+  int32_t *fneed = nullptr;        // [K + 1] 1: subproblem left to the serial walk; [K]: their count
 };
 // the walk's chunk and band for a p = Inf problem (mioc_pinf.hip)
 void pinf_plan(int RP, int nt, PinfDev &D);
@@ -155,7 +160,11 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
 hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D, int Bu,
                              Start *start);
 hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
-                            const Start *start, int32_t *ranks, int32_t *nfallback);
+                            const Start *start, int32_t *ranks, int32_t *nfallback, const int32_t *need);
+// segmented walk: steps per segment and segment count for nt steps
+void pinf_fplan(int nt, int *G, int *nseg);
+hipError_t launch_pinf_fwalk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
+                             const Start *start, int32_t *ranks);
 
 
 // ---- trust-region quantities around the DP (mioc_trm.hip) ---------------------------------------
@@ -290,7 +299,9 @@ struct mioc_ctx {
 
   // p = Inf buffers
   mioc::PinfDev pinf;
-  size_t pinf_cap_k = 0, pinf_cap_R = 0;
+  size_t pinf_cap_k = 0, pinf_cap_R = 0, pinf_cap_kabs = 0, pinf_cap_ftab = 0, pinf_cap_fseg = 0, pinf_cap_fneed = 0;
+  int opt_pinf_walk = 0;           // p = Inf backtrack: 0 auto, 1 segmented walk, -1 serial (MIOC_OPT_PINF_WALK)
+  bool last_pinf_fwalk = false;    // the last p = Inf backtrack ran the segmented walk
 
   // backtrack scratch
   bool have_path = false;          // d_ranks holds the controls of the last backtrack

@@ -65,7 +65,10 @@ __global__ __launch_bounds__(256) void k_pinf_prep(ProblemDev P, LevelsDev Lv, P
   const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
   const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
   const bool term = (i == P.nt - 1);
+  __shared__ unsigned long long s_kab;  // max |K| as the bits of a non-negative double (ordered as integers)
+  if (threadIdx.x == 0) s_kab = 0ull;
   __syncthreads();
+  unsigned long long kab = 0ull;
   for (int r = threadIdx.x; r < Lv.L; r += blockDim.x) {
     const double *nuv = Lv.nuval + (size_t)r * M;
     const int b = p_bt(nuv, uoi, M);
@@ -73,8 +76,12 @@ __global__ __launch_bounds__(256) void k_pinf_prep(ProblemDev P, LevelsDev Lv, P
     const double t1 = p_t1(nuv, dfi, M, P.dt);
     const double v = term ? t1 : t1 + Lv.beta;  // fl(T1 + β·1.0)
     atomicMin(reinterpret_cast<unsigned long long *>(&skmin[b]), (unsigned long long)okey(v));
+    const unsigned long long av = (unsigned long long)__double_as_longlong(fabs(v));
+    kab = av > kab ? av : kab;
   }
+  atomicMax(&s_kab, kab);
   __syncthreads();
+  if (threadIdx.x == 0) D.kabs[(size_t)k * P.nt + i] = __longlong_as_double((long long)s_kab);
   for (int r = threadIdx.x; r < Lv.L; r += blockDim.x) {
     const double *nuv = Lv.nuval + (size_t)r * M;
     const int b = p_bt(nuv, uoi, M);
@@ -114,12 +121,15 @@ __global__ __launch_bounds__(256) void k_pinf_prep_small(ProblemDev P, LevelsDev
   int kf[BWP];
 #pragma unroll
   for (int b = 0; b < BWP; ++b) km[b] = ~0ull, k2[b] = ~0ull, kf[b] = -1;
+  double kab = 0.0;
   for (int r = 0; r < Lv.L; ++r) {
     const double *nuv = Lv.nuval + (size_t)r * M;
     const int b = p_bt(nuv, uov, M);
     if (b >= BW) continue;
     const double t1 = p_t1(nuv, dfv, M, P.dt);
-    const uint64_t key = okey(term ? t1 : t1 + Lv.beta);
+    const double v = term ? t1 : t1 + Lv.beta;
+    kab = fmax(kab, fabs(v));
+    const uint64_t key = okey(v);
 #pragma unroll
     for (int q = 0; q < BWP; ++q) {
       if (q != b) continue;
@@ -133,6 +143,7 @@ __global__ __launch_bounds__(256) void k_pinf_prep_small(ProblemDev P, LevelsDev
     }
   }
   const size_t row = ((size_t)k * P.nt + i) * BWP;
+  D.kabs[(size_t)k * P.nt + i] = kab;
 #pragma unroll
   for (int q = 0; q < BWP; ++q) {
     D.kmin[row + q] = from_okey(km[q]);
@@ -419,8 +430,9 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 }
 
 __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, PinfDev D, const Start *start,
-                                                   int32_t *ranks, int32_t *nfallback) {
+                                                   int32_t *ranks, int32_t *nfallback, const int32_t *need) {
   if (gate_closed(P.gate)) return;
+  if (need && need[blockIdx.x] == 0) return;  // walked by the segmented walk
   extern __shared__ __attribute__((aligned(16))) double wsm[];
   const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
   const int M = P.M, nt = P.nt, RP = P.RP, BWP = D.BWP, CH = D.CH, W = D.W;
@@ -605,6 +617,158 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
   if (tid == 0 && fallbacks) atomicAdd(nfallback, fallbacks);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Segmented walk (many CUs for one subproblem).  The walker's decision at step j depends on its state
+// (K_l of the level it stands on, Φ_i[c, l]) only through rounding: the target is Φ_i[c, l] =
+// fl(K_l + R_j[c']) with c' = c - b̃_l, so a class b matches iff fl(K_l + V_b) == fl(K_l + R_j[c']) with
+// V_b = fl(Kmin_j[b] + R_{j+1}[c' - b]) and R_j[c'] = min_b V_b.  Every class with V_b == R_j[c'] matches for
+// any K_l; a class with V_b > R_j[c'] matches for none once V_b - R_j[c'] exceeds the rounding unit of
+// |K_l| + max(|V_b|, |R|) (bounded with kabs_{j-1} >= |K_l|), and the same bound on the class's second value
+// V2_b excludes the exact-scan case.  Where all classes of row c' are that clear, the winner -- the first
+// rank among the classes at the minimum -- is a function of (j, c') alone: the class table ftab.  The path
+// then is the chain c'_{j+1} = c'_j - b*(j, c'_j), which composes over segments of G steps in parallel
+// (k_pinf_fseg: every entry row of every segment), is chained serially over the nseg segments, and is
+// expanded per segment (k_pinf_fexpand).  A chain that meets a state-dependent row leaves its subproblem to
+// the serial walk (k_pinf_walk gated by fneed), so the ranks equal the serial walk's always.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pinf_ftab(ProblemDev P, PinfDev D) {
+  if (gate_closed(P.gate)) return;
+  extern __shared__ __attribute__((aligned(16))) double fsm[];
+  const int j = blockIdx.x + 1, k = blockIdx.y, nt = P.nt, RP = P.RP, B = P.B, BWP = D.BWP;
+  const bool term = (j == nt - 1);
+  double *Rn = fsm, *km = Rn + RP, *k2 = km + BWP;  // R_{j+1} row, class minima / second values of step j
+  int *kf = reinterpret_cast<int *>(k2 + BWP);
+  const size_t crow = ((size_t)k * nt + j) * BWP;
+  for (int q = threadIdx.x; q < BWP; q += blockDim.x) {
+    km[q] = D.kmin[crow + q];
+    k2[q] = D.k2[crow + q];
+    kf[q] = D.kfirst[crow + q];
+  }
+  if (!term)
+    for (int c = threadIdx.x; c < RP; c += blockDim.x) Rn[c] = D.R[((size_t)k * nt + j + 1) * RP + c];
+  const double kab = D.kabs[(size_t)k * nt + j - 1];
+  __syncthreads();
+  uint8_t *out = D.ftab + ((size_t)k * nt + j) * RP;
+  for (int cp = threadIdx.x; cp < RP; cp += blockDim.x) {
+    unsigned res = 0xFFu;
+    if (cp <= B) {
+      double R = INFINITY;
+      for (int b = 0; b < BWP; ++b) {
+        const double x = term ? (b == cp ? 0.0 : INFINITY) : (cp - b >= 0 ? Rn[cp - b] : INFINITY);
+        if (km[b] < INFINITY && x < INFINITY) R = fmin(R, term ? km[b] : km[b] + x);
+      }
+      if (R < INFINITY) {
+        bool safe = true;
+        int best = INT_MAX, bb = -1;
+        for (int b = 0; b < BWP; ++b) {
+          const double x = term ? (b == cp ? 0.0 : INFINITY) : (cp - b >= 0 ? Rn[cp - b] : INFINITY);
+          if (!(km[b] < INFINITY && x < INFINITY)) continue;
+          const double V = term ? km[b] : km[b] + x;
+          if (V == R) {
+            if (kf[b] < best) best = kf[b], bb = b;
+            if (k2[b] < INFINITY) {  // a level of the class with a larger K must not round onto the target
+              const double V2 = term ? k2[b] : k2[b] + x;
+              if (!(V2 - R > (kab + fmax(fabs(R), fabs(V2))) * 0x1p-50)) safe = false;
+            }
+          } else if (!(V - R > (kab + fmax(fabs(R), fabs(V))) * 0x1p-50)) {
+            safe = false;
+          }
+        }
+        if (safe && bb >= 0 && best >= 0) res = (unsigned)bb;
+      }
+    }
+    out[cp] = (uint8_t)res;
+  }
+}
+
+// composed map of segment g: the row after steps j0 .. j1 for every entry row (one thread per entry row)
+__global__ __launch_bounds__(256) void k_pinf_fseg(ProblemDev P, PinfDev D, int G, int nseg) {
+  if (gate_closed(P.gate)) return;
+  const int g = blockIdx.x, k = blockIdx.z, nt = P.nt, RP = P.RP;
+  const int cp0 = blockIdx.y * blockDim.x + threadIdx.x;
+  if (cp0 > P.B) return;
+  const int j0 = 1 + g * G, j1 = (j0 + G - 1 < nt - 1 ? j0 + G - 1 : nt - 1);
+  const uint8_t *tab = D.ftab + (size_t)k * nt * RP;
+  int c = cp0;
+  for (int j = j0; j <= j1; ++j) {
+    const unsigned b = tab[(size_t)j * RP + c];
+    if (b == 0xFFu) {
+      c = -1;
+      break;
+    }
+    if (j < nt - 1) c -= (int)b;
+  }
+  D.fseg[((size_t)k * nseg + g) * RP + cp0] = c;
+}
+
+// one workgroup per subproblem: thread 0 chains the segment maps from the start cell, then every thread expands
+// its segments into ranks; fneed[k] = 1 hands the subproblem to the serial walk
+__global__ __launch_bounds__(1024) void k_pinf_fexpand(ProblemDev P, LevelsDev Lv, PinfDev D, const Start *start,
+                                                       int32_t *ranks, int G, int nseg) {
+  if (gate_closed(P.gate)) return;
+  extern __shared__ int sent[];  // [nseg] entry row of each segment
+  __shared__ int s_ok;
+  const int k = blockIdx.x, nt = P.nt, RP = P.RP, M = P.M;
+  const Start st = start[k];
+  if (st.status != MIOC_OK || nt == 1) {  // nothing to walk: the serial walk returns at once as well
+    if (threadIdx.x == 0) {
+      D.fneed[k] = 0;
+      if (st.status == MIOC_OK) ranks[(size_t)k * nt] = st.r;
+    }
+    return;
+  }
+  if (threadIdx.x == 0) {
+    int cp = st.c - p_bt(Lv.nuval + (size_t)st.r * M, P.uold + (size_t)k * nt * M, M);
+    int ok = cp >= 0 && cp <= P.B;
+    for (int g = 0; ok && g < nseg; ++g) {
+      sent[g] = cp;
+      cp = D.fseg[((size_t)k * nseg + g) * RP + cp];
+      ok = cp >= 0;
+    }
+    s_ok = ok;
+    D.fneed[k] = !ok;
+    if (!ok) atomicAdd(D.fneed + P.K, 1);
+    else ranks[(size_t)k * nt] = st.r;
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  const uint8_t *tab = D.ftab + (size_t)k * nt * RP;
+  const int32_t *kfk = D.kfirst + (size_t)k * nt * D.BWP;
+  int32_t *rk = ranks + (size_t)k * nt;
+  for (int g = threadIdx.x; g < nseg; g += blockDim.x) {
+    const int j0 = 1 + g * G, j1 = (j0 + G - 1 < nt - 1 ? j0 + G - 1 : nt - 1);
+    int c = sent[g];
+    for (int j = j0; j <= j1; ++j) {
+      const int b = (int)tab[(size_t)j * RP + c];  // not 0xFF: the chain through this segment exists
+      rk[j] = kfk[(size_t)j * D.BWP + b];
+      c -= b;
+    }
+  }
+}
+
+void pinf_fplan(int nt, int *G, int *nseg) {
+  const int steps = nt > 1 ? nt - 1 : 1;
+  int g = 256;
+  while ((steps + g - 1) / g > 4096) g *= 2;
+  *G = g;
+  *nseg = (steps + g - 1) / g;
+}
+
+hipError_t launch_pinf_fwalk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
+                             const Start *start, int32_t *ranks) {
+  if (D.BWP > 64 || P.B + 1 > P.RP) return hipErrorInvalidValue;
+  int G, nseg;
+  pinf_fplan(P.nt, &G, &nseg);
+  if (P.nt > 1) {
+    const size_t lds = ((size_t)P.RP + 2 * D.BWP) * sizeof(double) + (size_t)D.BWP * sizeof(int);
+    hipLaunchKernelGGL(k_pinf_ftab, dim3(P.nt - 1, P.K), dim3(256), lds, s, P, D);
+    hipLaunchKernelGGL(k_pinf_fseg, dim3(nseg, (P.B + 256) / 256, P.K), dim3(256), 0, s, P, D, G, nseg);
+  }
+  hipLaunchKernelGGL(k_pinf_fexpand, dim3(P.K), dim3(1024), (size_t)nseg * sizeof(int), s, P, Lv, D, start, ranks,
+                     G, nseg);
+  return hipGetLastError();
+}
+
 // The walk's chunk and LDS row width: a band covering two chunks of budget descent plus one class window when that
 // is at most half a row (the narrow class windows of SOS1 problems: C1-C3 have BW = 4, W = 106 of RP = 832), else
 // whole rows with the largest chunk that fits 96 KB.
@@ -623,10 +787,10 @@ void pinf_plan(int RP, int nt, PinfDev &D) {
 }
 
 hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
-                            const Start *start, int32_t *ranks, int32_t *nfallback) {
+                            const Start *start, int32_t *ranks, int32_t *nfallback, const int32_t *need) {
   if (D.BWP > 64 || D.CH < 1 || D.W < 2) return hipErrorInvalidValue;
   size_t lds = (size_t)2 * D.CH * ((size_t)D.W * 8 + (size_t)D.BWP * 20) + 32;
-  hipLaunchKernelGGL(k_pinf_walk, dim3(P.K), dim3(256), lds, s, P, Lv, D, start, ranks, nfallback);
+  hipLaunchKernelGGL(k_pinf_walk, dim3(P.K), dim3(256), lds, s, P, Lv, D, start, ranks, nfallback, need);
   return hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ MIOC_ENONFINITE = -7
 
 MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
 MIOC_OPT_ALGO, MIOC_OPT_TIMING, MIOC_OPT_PERSIST, MIOC_OPT_PRED_FMA = 1, 2, 3, 4
-MIOC_OPT_SPIN_LIMIT, MIOC_OPT_SDT_BUFFERS, MIOC_OPT_FSEP_SEGMENTS = 5, 6, 7
+MIOC_OPT_SPIN_LIMIT, MIOC_OPT_SDT_BUFFERS, MIOC_OPT_FSEP_SEGMENTS, MIOC_OPT_PINF_WALK = 5, 6, 7, 8
 MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID, MIOC_ALGO_SEPARABLE = 0, 1, 2, 3, 4
 MIOC_ALGO_FUSED, MIOC_ALGO_FUSED_SEPARABLE = 5, 6
 MIOC_ODE_FISHING, MIOC_ODE_DOUBLETANK, MIOC_ODE_VANDERPOL = 1, 2, 3
@@ -509,9 +509,10 @@ class Context:
         """[value-collision targets scanned, multi-level targets scanned, p=Inf walk fallbacks or U-table walk
         run-ahead rounds, errors,
         hash-overflow rows, targets whose value was not found, values flagged colliding (persistent / segmented DPs
-        redone), occupancy, fused separable row segments] (include/mioc.h)."""
-        out = np.zeros(9, dtype=np.int64)
-        self._check(self.lib.mioc_diagnostics(self.h, _p(out), 9))
+        redone), occupancy, fused separable row segments, p=Inf segmented walk: subproblems walked serially]
+        (include/mioc.h)."""
+        out = np.zeros(10, dtype=np.int64)
+        self._check(self.lib.mioc_diagnostics(self.h, _p(out), 10))
         return out.tolist()
 
 
