@@ -1,7 +1,9 @@
 """Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into HBM bytes per kernel launch.
 
-Usage: python scripts/pmc_traffic.py OUT.json [CFG:]LABEL=DIR/NAME_counter_collection.csv ...
+Usage: python scripts/pmc_traffic.py OUT.json [--qualify KERNEL@CFG:MIN_WGS ...] [CFG:]LABEL=DIR/NAME_counter_collection.csv ...
 A CFG: prefix (a pass over one bench config, e.g. `bench.py --config C2 ...`) stores the kernels as "name@CFG".
+--qualify KERNEL@CFG:MIN_WGS stores the dispatches of KERNEL with at least MIN_WGS workgroups as "KERNEL@CFG" (one
+pass over the default bench holds both the single-subproblem C4 line and the 1024-restart batch lines).
 FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE
 reports half the bytes of wide reads, so it is doubled; WRITE_SIZE is taken as is.  Both counters
 count Infinity-Cache hits as memory-side traffic.
@@ -19,16 +21,28 @@ def short(name):
 
 def main():
     out = sys.argv[1]
+    args = sys.argv[2:]
+    qual = {}
+    while args and args[0] == "--qualify":
+        kc, mw = args[1].rsplit(":", 1)
+        kname, kcfg = kc.split("@")
+        qual[kname] = (kcfg, int(mw))
+        args = args[2:]
     res = {}
-    for spec in sys.argv[2:]:
+    for spec in args:
         label, path = spec.split("=", 1)
         cfg = label.split(":", 1)[0] if ":" in label else None
         acc = defaultdict(lambda: defaultdict(list))
         with open(path) as f:
             for row in csv.DictReader(f):
-                acc[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                name = short(row["Kernel_Name"])
+                if name in qual:
+                    wgs = int(row["Grid_Size"]) // max(1, int(row["Workgroup_Size"]))
+                    if wgs >= qual[name][1]:
+                        name = f"{name}@{qual[name][0]}"
+                acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
         for k, d in acc.items():
-            e = res.setdefault(f"{k}@{cfg}" if cfg else k, {})
+            e = res.setdefault(f"{k}@{cfg}" if cfg and "@" not in k else k, {})
             for cname, vals in d.items():
                 scale = 1024.0 * (2.0 if cname == "FETCH_SIZE" else 1.0)
                 e[cname.lower() + "_bytes_per_launch"] = scale * sum(vals) / len(vals)
