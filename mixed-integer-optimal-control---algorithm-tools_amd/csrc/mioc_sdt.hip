@@ -50,6 +50,9 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_PASS_SPLIT
 #define SDT_PASS_SPLIT 0                 // passes as two independent half-chains + a combine (experiment)
 #endif
+#ifndef SDT_WAVE_LOCAL
+#define SDT_WAVE_LOCAL 1                 // passes over the low M-1 dimensions sync per wave; outputs in their own buffer
+#endif
 #ifndef SDT_PREFETCH
 #define SDT_PREFETCH 1                   // load the sphere orders ahead of the dependency wait
 #endif
@@ -137,6 +140,11 @@ __device__ __forceinline__ double sd_min(double a, double b) {
   asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+__device__ __forceinline__ double sd_max(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 // The thread index as a value the compiler cannot hoist out of the persistent driver's row loop: everything the
 // row body derives from it (LDS addresses of the passes, swizzles, store offsets) is recomputed per row instead of
@@ -174,17 +182,15 @@ __device__ __forceinline__ double sd_dpp_d(double x) {
 __device__ __forceinline__ double sd_rdl(double x, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l), __builtin_amdgcn_readlane(__double2loint(x), l));
 }
-__device__ __forceinline__ void sd_wave_stats(double &mn, double &mx, int &n) {
+// (min and max without llvm.minnum's canonicalisation: the operands are finite or ±Inf, never NaN)
+__device__ __forceinline__ void sd_wave_stats(double &mn, double &mx) {
 #define SD_STEP(C)                             \
-  mn = fmin(mn, sd_dpp_d<C>(mn));              \
-  mx = fmax(mx, sd_dpp_d<C>(mx));              \
-  n += sd_dpp_i<C>(n);
+  mn = sd_min(mn, sd_dpp_d<C>(mn));            \
+  mx = sd_max(mx, sd_dpp_d<C>(mx));
   SD_STEP(0xB1) SD_STEP(0x4E) SD_STEP(0x141) SD_STEP(0x140)
 #undef SD_STEP
-  mn = fmin(fmin(sd_rdl(mn, 0), sd_rdl(mn, 16)), fmin(sd_rdl(mn, 32), sd_rdl(mn, 48)));
-  mx = fmax(fmax(sd_rdl(mx, 0), sd_rdl(mx, 16)), fmax(sd_rdl(mx, 32), sd_rdl(mx, 48)));
-  n = (__builtin_amdgcn_readlane(n, 0) + __builtin_amdgcn_readlane(n, 16)) +
-      (__builtin_amdgcn_readlane(n, 32) + __builtin_amdgcn_readlane(n, 48));
+  mn = sd_min(sd_min(sd_rdl(mn, 0), sd_rdl(mn, 16)), sd_min(sd_rdl(mn, 32), sd_rdl(mn, 48)));
+  mx = sd_max(sd_max(sd_rdl(mx, 0), sd_rdl(mx, 16)), sd_max(sd_rdl(mx, 32), sd_rdl(mx, 48)));
 }
 
 // LDS position of rank r (3 bits per dimension): XOR swizzle so that each 32-lane half of a pass reads
@@ -370,6 +376,19 @@ template <int M>
 __host__ __device__ constexpr size_t sd_dfuo_offset() {  // then df(:, i), u_old(:, i) per wave (persistent driver)
   return sd_slot_offset<M>() + 2 * ((size_t)1 << (3 * M)) * sizeof(uint32_t);
 }
+template <int M>
+__host__ __device__ constexpr size_t sd_out_offset() {  // then the row's outputs (natural order), SDT_WAVE_LOCAL
+  return sd_dfuo_offset<M>() + ((2 * M * sizeof(double) * (((size_t)1 << (3 * M - 3)) / 64) + 255) & ~(size_t)255);
+}
+template <int M>
+__host__ __device__ constexpr size_t sd_lds_total() {
+  return SDT_WAVE_LOCAL ? sd_out_offset<M>() + ((size_t)1 << (3 * M)) * sizeof(double)
+                        : sd_dfuo_offset<M>() + 2 * M * sizeof(double) * (((size_t)1 << (3 * M - 3)) / 64);
+}
+
+// Wave-local LDS ordering: this wave's LDS stores are complete before its next LDS reads (LDS instructions of one
+// wave execute in order; the wait also keeps the compiler from moving accesses across)
+__device__ __forceinline__ void sd_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // The sphere orders a step reads (step i+1, for the sources) and writes (step i, for the output row), as the
 // position pairs 2(tid + T·q) + {0, 1} of this thread, plus both heads (position 0).  Loaded at the start of
@@ -419,8 +438,11 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
                                          const double *__restrict__ uo_all) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
   double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
-  double *dtv = psi + L;                                // [L] transform values (swizzled), then outputs (natural)
+  double *dtv = psi + L;                                // [L] transform values (swizzled)
   uint16_t *uu = reinterpret_cast<uint16_t *>(dtv + L);  // [L] the U row (natural order)
+  // [L] the outputs (natural order): a buffer of their own, so that the winners of one wave need not wait for every
+  // other wave's last pass (SDT_WAVE_LOCAL); else the transform buffer after a barrier
+  double *outv = SDT_WAVE_LOCAL ? reinterpret_cast<double *>(sds + sd_out_offset<M>()) : dtv;
   uint16_t *list = uu + L;                              // [SD_LCAP] targets for the exact scan
   const int tid = sd_tid(), lane = tid & 63, w = tid >> 6;
   const int B = P.B;
@@ -452,10 +474,16 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     pre = pre + a[m] * (double)nu;  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
     bpre += abs(nu - uo[m]);
   }
-  const unsigned ptid = sd_bytes((unsigned)tid);  // the thread's first M-1 coordinates, one byte each
   unsigned valid = 0;  // target inside the trust region: c' + b̃_l(i) <= B
+  // targets in the trust region (low 16 bits) + finite sources (high 16 bits) of the wave: ballots counted on the
+  // scalar unit
+  int nv = 0;
 #pragma unroll
-  for (int x = 0; x < 8; ++x) valid |= (unsigned)(bpre + abs(lb[M - 1] + x - uo[M - 1]) <= B - cp) << x;
+  for (int x = 0; x < 8; ++x) {
+    const bool in = bpre <= B - cp - abs(lb[M - 1] + x - uo[M - 1]);  // right side wave-uniform
+    valid |= (unsigned)in << x;
+    nv += __popcll(__ballot(in));
+  }
 
   if (tid == 0) sh.nlist = 0;
   double pmn = INFINITY, pmx = -INFINITY;
@@ -465,15 +493,12 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     for (int h = 0; h < 2; ++h) {
       const double x = v[2 * q + h];
       psi[(h ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
-      if (x < INFINITY) {
-        pmn = fmin(pmn, x);
-        pmx = fmax(pmx, x);
-      }
+      const bool fin = x < INFINITY;
+      nv += __popcll(__ballot(fin)) << 16;
+      pmn = sd_min(pmn, x);  // +Inf is neutral
+      pmx = sd_max(pmx, __hiloint2double(fin ? __double2hiint(x) : (int)0xFFF00000, __double2loint(x)));  // +Inf -> -Inf
     }
-  int nv = __popc(valid);  // targets in the trust region (low 16 bits) + finite sources (high 16 bits)
-#pragma unroll
-  for (int q = 0; q < 8; ++q) nv += (v[q] < INFINITY) << 16;
-  sd_wave_stats(pmn, pmx, nv);
+  sd_wave_stats(pmn, pmx);
   if (lane == 0) {
     sh.rmn[w] = pmn;
     sh.rmx[w] = pmx;
@@ -483,8 +508,8 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   h.early();
 #pragma unroll
   for (int q = 0; q < NW; ++q) {
-    pmn = fmin(pmn, sh.rmn[q]);
-    pmx = fmax(pmx, sh.rmx[q]);
+    pmn = sd_min(pmn, sh.rmn[q]);
+    pmx = sd_max(pmx, sh.rmx[q]);
   }
   nv = 0;
 #pragma unroll
@@ -596,7 +621,17 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
 #pragma unroll
         for (int x = 0; x < 8; ++x) dtv[pos[x]] = o[x];
       }
+#if SDT_WAVE_LOCAL
+      // the lines of passes 0 .. M-2 keep the top grid coordinate (rank bits 3(M-1)..) = the wave index (the swizzle
+      // leaves those bits alone): a wave reads only what it wrote itself, so only the last pass, which runs along
+      // that coordinate, needs every wave's values
+      if (m + 2 < M)
+        sd_wave_sync();
+      else if (m + 1 < M)
+        sd_bar();
+#else
       sd_bar();  // last pass: every read of dtv is done before it becomes the output buffer
+#endif
       SD_STAMP(3 + m);
     }
   }
@@ -617,12 +652,15 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
         const int r = tid | (x << (3 * (M - 1))), j = jx[x];
         const bool fin = (valid >> x & 1) && o[x] < INFINITY;
         const bool flg = (__double2loint(o[x]) & SD_FLAG) != 0;
-        const unsigned d = sd_l1(sd_bytes(j), ptid | (unsigned)x << (8 * (M - 1)));
+        // d(l, j*) exactly: an unflagged finite o[x] is V_j* + d with V_j* = the stamp of Ψ_j* (the same expression
+        // as the stamping above, payload j*), every term exact in the binade (garbage, unused, otherwise)
+        const double y = (pv[x] - pmn) * inv + base;
+        const double dd = o[x] - __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | j);
         const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
-        const double val = (t1 + beta * (double)d) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
+        const double val = (t1 + beta * dd) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
         listed |= (unsigned)(fin && flg) << x;
         uu[r] = (uint16_t)(fin && !flg ? j : 0xFFFF);  // 0xFFFF: unwritten (Φ = +Inf) or not yet known (listed)
-        dtv[r] = fin ? (flg ? __longlong_as_double(0x7FF8000000000000ll) : val) : INFINITY;
+        outv[r] = fin ? (flg ? __longlong_as_double(0x7FF8000000000000ll) : val) : INFINITY;
       }
     } else {
 #pragma unroll
@@ -641,7 +679,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
             for (int e = 0; e < SD_SPARSE; ++e) {
               if (e < nf) {
                 const int j = spj[e];
-                const unsigned d = sd_l1(sd_bytes(j), ptid | (unsigned)x << (8 * (M - 1)));
+                const unsigned d = sd_l1(sd_bytes(j), sd_bytes((unsigned)tid) | (unsigned)x << (8 * (M - 1)));
                 const double val = (t1 + beta * (double)d) + spv[e];
                 if (val < bv || (val == bv && j < bj)) {
                   bv = val;
@@ -654,7 +692,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
           }
         }
         uu[r] = (uint16_t)uj;
-        dtv[r] = (listed >> x & 1) ? __longlong_as_double(0x7FF8000000000000ll) : ov;
+        outv[r] = (listed >> x & 1) ? __longlong_as_double(0x7FF8000000000000ll) : ov;
       }
     }
     if (listed) {
@@ -671,18 +709,18 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     const int nl = sh.nlist;
     if (nl) {
       if (nl <= SD_COOP)
-        sd_scan<M, true>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
+        sd_scan<M, true>(list, nl, psi, a, lb, beta, uu, outv, sh.redv, sh.redj);
       else if (nl <= SD_LCAP)
-        sd_scan<M, false>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
+        sd_scan<M, false>(list, nl, psi, a, lb, beta, uu, outv, sh.redv, sh.redj);
       else
-        sd_scan<M, false>(nullptr, L, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);  // every NaN-marked rank
+        sd_scan<M, false>(nullptr, L, psi, a, lb, beta, uu, outv, sh.redv, sh.redj);  // every NaN-marked rank
       sd_bar();
       if (tid == 0) sh.cnt[direct ? 1 : 0] += nl;
     }
   }
   if (empty) {  // uniform: the row is +Inf, U unwritten -- through LDS, so that the stores below take one path
 #pragma unroll
-    for (int x = 0; x < 8; ++x) dtv[tid | (x << (3 * (M - 1)))] = INFINITY;
+    for (int x = 0; x < 8; ++x) outv[tid | (x << (3 * (M - 1)))] = INFINITY;
     reinterpret_cast<ulonglong2 *>(uu)[tid] = make_ulonglong2(~0ull, ~0ull);
     sd_bar();
   }
@@ -691,8 +729,8 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const uint2 e = *reinterpret_cast<const uint2 *>(pout + 2 * (tid + T * q));
-    sd_store16<PERSIST>(Sout, L * 8, 2 * (tid + T * q), __double_as_longlong(dtv[e.x & 0xFFFFu]),
-                        __double_as_longlong(dtv[e.y & 0xFFFFu]));
+    sd_store16<PERSIST>(Sout, L * 8, 2 * (tid + T * q), __double_as_longlong(outv[e.x & 0xFFFFu]),
+                        __double_as_longlong(outv[e.y & 0xFFFFu]));
   }
   {
     const ulonglong2 t = reinterpret_cast<const ulonglong2 *>(uu)[tid];
@@ -909,9 +947,7 @@ struct SdHooksNone {
 
 // LDS bytes of the row body: Ψ by rank, the transform / output values, the U row, the scan list, and two
 // sphere-order slots (steps i+1 and i)
-size_t sdt_lds_bytes(const PyrGeom &G) {
-  return G.M == 4 ? sd_dfuo_offset<4>() + 2 * 4 * sizeof(double) * 8 : sd_dfuo_offset<3>() + 2 * 3 * sizeof(double);
-}
+size_t sdt_lds_bytes(const PyrGeom &G) { return G.M == 4 ? sd_lds_total<4>() : sd_lds_total<3>(); }
 
 // copy one step's sphere order (L uint32) into an LDS slot with LDS-DMA (1 KiB per wave-instruction, no VGPRs);
 // lands asynchronously (vmcnt), visible to the other waves after their wait and a barrier
@@ -1143,7 +1179,11 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa[q], 0, 16);
+#ifndef SDT_EXP_NOB64  // timing experiment only (wrong results): without the straddle loads
     w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob[q], 0, 16);
+#else
+    w.b[q] = sd_u32x2{0u, 0u};
+#endif
   }
   w.mask = mask;
 }
@@ -1266,7 +1306,9 @@ struct SdPipe {
     if (has_next) {
       sd_issue_pipe<M>(raw, rs, slot + ((ni + 1) & 1) * L, ncp, (unsigned)((ni + 1) % NB) * bufb,
                        r0b + (unsigned)(ni + 1) * rowb, rowb);
+#ifndef SDT_EXP_NOPERM  // timing experiment only (wrong results): the sphere order of the first step for every step
       if (ni != i) sd_perm_dma_asm<M>(pk + (size_t)ni * L, slot + (ni & 1) * L);
+#endif
       sd_dfuo_dma<M>(dfa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + ni) * M, sds);
     }
     SD_TL_AT(g0, i, nt, 5);
@@ -1292,7 +1334,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   const int base = B / W, extra = B - base * W;  // rows 1..B, the longer chunks highest
   const int lo = 1 + wl * base + max(0, wl - (W - extra)), hi = lo + base + (wl >= W - extra ? 1 : 0);
   uint32_t *slot = reinterpret_cast<uint32_t *>(sds + sd_slot_offset<M>());
-  double *dtv = reinterpret_cast<double *>(sds) + L;  // the row body's outputs (natural order) after a row
+  // the row body's outputs (natural order) after a row
+  double *dtv = SDT_WAVE_LOCAL ? reinterpret_cast<double *>(sds + sd_out_offset<M>()) : reinterpret_cast<double *>(sds) + L;
   auto pslot = [&](int step) { return slot + (step & 1) * L; };  // sphere order of `step`
   // this subproblem's region: NB staging buffers of R rows, then row 0 of every step (k_sdt_row0); one buffer
   // resource over all of it (the host checks it is below 4 GiB)
