@@ -817,17 +817,21 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
 // Sphere order of u_old(i) for every step (one workgroup per (step, subproblem)): the ranks j grouped by
 // their L1 distance b̃_j(i) = Σ_m |ν_jm - u_old[m,i]| (HelpFunctions.jl:53-57), perm[p] = j | b̃_j << 16.
 // Staging rows of step i are stored in this order, so the L sources a workgroup of step i-1 reads from
-// row c' - s of S_i (the sphere s) form one contiguous run per sphere.  The order inside a sphere is
-// whatever the LDS atomics produce: producer and consumer read the same table.
+// row c' - s of S_i (the sphere s) form one contiguous run per sphere.  Inside a sphere the ranks ascend (a
+// stable counting sort), so the order is a function of u_old(i) alone: steps with equal u_old share one table,
+// which the persistent separable-transform driver uses to skip reloading it.
 __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all) {
-  __shared__ int hist[64];
+  __shared__ int start[64];     // the next free position of each sphere (distances >= 63 share the last)
+  __shared__ int wcnt[4][65];   // ranks of the current chunk per wave and sphere (65: the inactive lanes)
   const int i = blockIdx.x, k = blockIdx.y, L = G.ncol * G.n[0], M = G.M;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const double *uo = P.uold + ((size_t)k * P.nt + i) * M;
   uint32_t *perm = perm_all + ((size_t)k * P.nt + i) * L;
   int u[kMaxM];
 #pragma unroll
   for (int m = 0; m < kMaxM; ++m) u[m] = m < M ? (int)uo[m] : 0;
-  if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+  if (tid < 64) start[tid] = 0;
+  for (int e = tid; e < 4 * 65; e += blockDim.x) (&wcnt[0][0])[e] = 0;
   __syncthreads();
   auto dist = [&](int j) {
     int d = 0;
@@ -838,20 +842,44 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
     }
     return min(d, 0xFFFF);
   };
-  for (int j = threadIdx.x; j < L; j += blockDim.x) atomicAdd(&hist[min(dist(j), 63)], 1);
+  for (int j = tid; j < L; j += blockDim.x) atomicAdd(&start[min(dist(j), 63)], 1);
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     int run = 0;
     for (int b = 0; b < 64; ++b) {
-      const int c = hist[b];
-      hist[b] = run;
+      const int c = start[b];
+      start[b] = run;
       run += c;
     }
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < L; j += blockDim.x) {
-    const int d = dist(j);
-    perm[atomicAdd(&hist[min(d, 63)], 1)] = (uint32_t)j | ((uint32_t)d << 16);
+  // chunks of 256 consecutive ranks in order; inside a chunk, a rank's place among its sphere's ranks is the number of
+  // lower lanes of its wave with the same sphere (7 ballots) plus those of the lower waves
+  for (int c = 0; c < L; c += 256) {
+    const int j = c + tid;
+    const bool act = j < L;
+    const int d = act ? dist(j) : 0, b = act ? min(d, 63) : 64;
+    unsigned long long same = ~0ull;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const unsigned long long m = __ballot((b >> q) & 1);
+      same &= ((b >> q) & 1) ? m : ~m;
+    }
+    const int below = __popcll(same & ((1ull << lane) - 1ull));
+    if (below == 0) wcnt[w][b] = __popcll(same);
+    __syncthreads();
+    if (act) {
+      int pos = start[b] + below;
+      for (int q = 0; q < w; ++q) pos += wcnt[q][b];
+      perm[pos] = (uint32_t)j | ((uint32_t)d << 16);
+    }
+    __syncthreads();
+    if (tid < 64) {
+      start[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+      wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+    }
+    if (tid == 64) wcnt[0][64] = wcnt[1][64] = wcnt[2][64] = wcnt[3][64] = 0;
+    __syncthreads();
   }
 }
 

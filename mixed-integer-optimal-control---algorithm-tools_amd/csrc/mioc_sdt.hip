@@ -53,6 +53,9 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_WAVE_LOCAL
 #define SDT_WAVE_LOCAL 1                 // passes over the low M-1 dimensions sync per wave; outputs in their own buffer
 #endif
+#ifndef SDT_PERM_SKIP
+#define SDT_PERM_SKIP 1                  // persistent driver: no sphere-order reload where u_old repeats (see go())
+#endif
 #ifndef SDT_PREFETCH
 #define SDT_PREFETCH 1                   // load the sphere orders ahead of the dependency wait
 #endif
@@ -983,6 +986,36 @@ __device__ __forceinline__ void sd_perm_dma_asm(const uint32_t *src, uint32_t *s
   }
 }
 
+// u_old(:, a) and u_old(:, b) bit for bit, by scalar loads in one asm statement with its own lgkmcnt wait (a plain C++
+// load here becomes a vector load whose vmcnt(0) wait would also wait for the row loads just issued)
+typedef unsigned int sd_s32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int sd_s32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int sd_s32x2 __attribute__((ext_vector_type(2)));
+template <int M>
+__device__ __forceinline__ bool sd_same_uold(const double *a, const double *b) {
+  static_assert(M == 3 || M == 4, "sd_same_uold: M = 3 or 4");
+  if constexpr (M == 4) {
+    sd_s32x8 x, y;
+    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx8 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(x), "=&s"(y)
+                 : "s"(a), "s"(b)
+                 : "memory");
+    bool same = true;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) same &= x[e] == y[e];
+    return same;
+  } else {
+    sd_s32x4 x0, y0;
+    sd_s32x2 x1, y1;
+    asm volatile("s_load_dwordx4 %0, %4, 0x0\n\ts_load_dwordx2 %1, %4, 0x10\n\ts_load_dwordx4 %2, %5, 0x0\n\t"
+                 "s_load_dwordx2 %3, %5, 0x10\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(x0), "=&s"(x1), "=&s"(y0), "=&s"(y1)
+                 : "s"(a), "s"(b)
+                 : "memory");
+    return x0[0] == y0[0] && x0[1] == y0[1] && x0[2] == y0[2] && x0[3] == y0[3] && x1[0] == y1[0] && x1[1] == y1[1];
+  }
+}
+
 // df(:, i) and u_old(:, i) (M doubles each) into this wave's LDS words: lanes 0..4M-1 move one dword each
 // (global_load_lds_dword, LDS-DMA, inline asm for the same reason as sd_perm_dma_asm)
 template <int M>
@@ -1306,9 +1339,14 @@ struct SdPipe {
     if (has_next) {
       sd_issue_pipe<M>(raw, rs, slot + ((ni + 1) & 1) * L, ncp, (unsigned)((ni + 1) % NB) * bufb,
                        r0b + (unsigned)(ni + 1) * rowb, rowb);
-#ifndef SDT_EXP_NOPERM  // timing experiment only (wrong results): the sphere order of the first step for every step
-      if (ni != i) sd_perm_dma_asm<M>(pk + (size_t)ni * L, slot + (ni & 1) * L);
+#ifdef SDT_TL_ISSUE  // timeline diagnostic: point 7 = the next row's loads issued (else: this row's loads consumed)
+      SD_TL_AT(g0, i, nt, 7);
 #endif
+      // the sphere order of step ni into the slot of step i+1 -- unless u_old(ni) = u_old(i+1): the order is a function of
+      // u_old alone (k_pyr_order), so the slot already holds it (by induction, every slot holds the order of the last
+      // step assigned to it)
+      if (ni != i && !(SDT_PERM_SKIP && sd_same_uold<M>(uoa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + i + 1) * M)))
+        sd_perm_dma_asm<M>(pk + (size_t)ni * L, slot + (ni & 1) * L);
       sd_dfuo_dma<M>(dfa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + ni) * M, sds);
     }
     SD_TL_AT(g0, i, nt, 5);
@@ -1382,7 +1420,9 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       double v[8];
       sd_take(v, h.raw);
+#ifndef SDT_TL_ISSUE
       SD_TL(7);
+#endif
       // one row per workgroup: a sphere-0 source at distance 0 (u_old(i+1) on the level grid: position 0 with b̃ = 0)
       // is this workgroup's own output of the previous row, still in LDS (the loaded copy predates it); an off-grid
       // u_old(i+1) has b̃ >= 1 everywhere and no such source
