@@ -6,6 +6,10 @@
 //     slots s = 0..H-1, lane 2r+1 holds x1 = N1-1..H in the same slots (mirrored), which makes the cross-half
 //     step of the x1 pass the same instruction on both lanes: take the partner's slot H-1 (DPP swap) and merge
 //     it into slot H-1-t at cost t+1.
+//   * Four lanes per row (LN = 4, the row-segment launches of small batches): the lane quad also splits x0 into
+//     mirrored halves, with the same cross-half step in the x0 pass (partner lane ^ 2).  A wave then carries 16
+//     rows, so a segment of 128 rows fills 8 waves, two per SIMD, where two lanes per row leave one wave per SIMD
+//     with nothing to hide its dependency chains behind.
 //   * The front Φ is updated IN PLACE: read phase (every lane reads its row, runs the transform, gathers its
 //     results into registers), barrier, write phase (results, the inbox of the segment below, +Inf cells, the
 //     next step's K table), barrier.  One copy of the front (~79 KB at C5) lets two subproblems share a CU.
@@ -42,6 +46,9 @@ namespace {
 
 constexpr int FS2_FLAG = 64;  // near-tie flag (payload bit 6)
 constexpr int FS2_MAXT = 512;  // threads per workgroup: 256 budget rows + row B (larger B: mioc_fused.hip)
+#ifndef FSEP_LANES4
+#define FSEP_LANES4 1  // row segments with four lanes per row where they fit (A/B builds: 0)
+#endif
 
 __device__ __forceinline__ void fs_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -129,12 +136,25 @@ struct FsepArgs {
   int base0, base1;
 };
 
-template <int N0, int N1, bool SEG>
+// the partner lane's (tid ^ 2) value: DPP quad_perm [2, 3, 0, 1]
+__device__ __forceinline__ unsigned fs_swap2_u(unsigned x) {
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+}
+__device__ __forceinline__ double fs_swap2(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0x4E, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0x4E, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// LN lanes per source row (2: x1 halves; 4: x1 and x0 halves).  A lane's slot t = s·H0 + u holds the level
+// x0 = h0 ? N0-1-u : u, x1 = h1 ? N1-1-s : s (h1 = lane bit 0, h0 = lane bit 1 for LN = 4, else 0).
+template <int N0, int N1, bool SEG, int LN>
 __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG && N0 * N1 <= 36 ? 4 : 2))) void k_fsep2(
     ProblemDev P, LevelsDev Lv, FsepArgs A) {
-  constexpr int L = N0 * N1, H = N1 / 2, V = N0 * H, SMAX = N0 + N1 - 2, ND = SMAX + 1;
+  constexpr int L = N0 * N1, H = N1 / 2, H0 = LN == 4 ? N0 / 2 : N0, V = H0 * H, SMAX = N0 + N1 - 2, ND = SMAX + 1;
+  constexpr int LSH = LN == 4 ? 2 : 1, RPW = 64 / LN;  // lanes per row (log2), rows per wave
   constexpr int FS = (L + 1) | 1;  // odd row stride (8-byte words)
-  static_assert(N1 % 2 == 0 && N0 <= 8 && N1 <= 8 && V <= 32, "grid shape");
+  static_assert(N1 % 2 == 0 && (LN == 2 || N0 % 2 == 0) && N0 <= 8 && N1 <= 8 && V <= 32, "grid shape");
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
   __shared__ int s_stop;
   const int S = SEG ? A.S : 1, k = (int)blockIdx.x / S, q = (int)blockIdx.x - k * S;
@@ -146,7 +166,7 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
   double *const Kt = F + A.koff;
   // d(l, j), the L1 distance of two levels, one byte each (static: built once)
   unsigned char *const Dt = reinterpret_cast<unsigned char *>(Kt + L * ND);
-  const int cx = lo + (nthr >> 1);  // past the lane pairs: the extra row (row B) when cx < hi
+  const int cx = lo + (nthr >> LSH);  // past the lane groups: the extra row (row B) when cx < hi
   const double beta = Lv.beta, inv = Lv.inv_beta;
   const double numx0 = (double)max(abs(A.base0), abs(A.base0 + N0 - 1)),
                numx1 = (double)max(abs(A.base1), abs(A.base1 + N1 - 1));
@@ -223,6 +243,10 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
   __syncthreads();
   uint8_t *Uk = A.U + (size_t)k * A.u_stride_k;
   int nflag = 0, nscan = 0;
+  // the inbox flag of the segment below, polled one step ahead: the value a step checks was loaded during the step
+  // before, so the inbox copy issues at the start of the read phase and its latency hides behind the transform
+  int vin_next = 0;
+  if (SEG && q > 0) vin_next = __hip_atomic_load(fl - 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if defined(MIOC_STAMPS)
   unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -232,15 +256,18 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
     // step loop, the per-target constants (LDS offsets, U offsets) would take more registers than the row itself
     int tido = tid;
     asm volatile("" : "+v"(tido));
-    const int hf = tido & 1;
-    const int cp = lo + (tido >> 1);  // this lane pair's source row
+    const int hf = tido & 1, h0 = LN == 4 ? (tido >> 1) & 1 : 0;
+    const int cp = lo + (tido >> LSH);  // this lane group's source row
     const bool act = cp < hi;
     const int room = act ? B - cp : -1;  // target l of this row is inside the trust region iff b̃_l <= room
     const int cl = act ? cp - lo : 0;
-    const int lb = cl * FS + (hf ? N0 * (N1 - 1) : 0), ls = hf ? -N0 : N0;  // slot s, x0 at F[lb + ls·s + x0]
-    int x1v[H];
+    // slot (s, u) at F[lb + ls·s + lu·u]
+    const int lb = cl * FS + (hf ? N0 * (N1 - 1) : 0) + (h0 ? N0 - 1 : 0), ls = hf ? -N0 : N0, lu = h0 ? -1 : 1;
+    int x1v[H], x0v[H0];
 #pragma unroll
     for (int s = 0; s < H; ++s) x1v[s] = hf ? N1 - 1 - s : s;
+#pragma unroll
+    for (int u = 0; u < H0; ++u) x0v[u] = h0 ? N0 - 1 - u : u;
     const int su0 = __builtin_amdgcn_readfirstlane(cu0), su1 = __builtin_amdgcn_readfirstlane(cu1);
     auto btl = [&](int x0, int x1) { return abs(A.base0 + x0 - su0) + abs(A.base1 + x1 - su1); };
     // U_i[l][c] through a buffer resource (bounds-checked to the step's L·R bytes: a store past them is dropped)
@@ -252,19 +279,35 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
     // the segment above has consumed the ring slot this step's outbox overwrites (WAR)
     const int need_in = SEG && q > 0 ? nt - 1 - i : INT_MIN;
     const int need_cons = SEG && q < S - 1 && i + NB <= nt - 2 ? nt - 1 - (i + NB) : INT_MIN;
-    int vin = 0, vcons = 0;
-    if (SEG && q > 0) vin = __hip_atomic_load(fl - 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int vin = vin_next, vcons = 0;
     if (SEG && need_cons != INT_MIN) vcons = __hip_atomic_load(fl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // ================= read phase: Φ_{i+1} rows into registers, the transform, results into registers ========
     FS_T(q0);
+    // ---- the segment below has published this step's outbox: load it (consumed in the write phase) --------
+    if (SEG && q > 0 && wait_flag(fl - 2, vin, need_in)) {
+      if (i >= 1) vin_next = vin >= need_in + 1 ? vin : __hip_atomic_load(fl - 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // LDS-DMA of the slot, 1 KiB chunks by wave (inline asm: the compiler does not make later LDS accesses
+      // wait for it; the drain before barrier 1 completes it, the barrier publishes it)
+      const char *slot = ring_in + (size_t)(i % NB) * A.slot_bytes;
+      const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)(fsm)) + A.stg * 8u;
+      for (int c = w; c < A.slot_bytes / 1024; c += nw) {
+        const char *gsrc = slot + c * 1024 + lane * 16;
+        const unsigned m0 = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)c * 1024u);
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(gsrc), "s"(m0)
+                     : "memory");
+      }
+    }
     double o[V];
 #pragma unroll
     for (int s = 0; s < H; ++s)
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) o[x0 + N0 * s] = F[lb + ls * s + x0];
+      for (int u = 0; u < H0; ++u) o[u + H0 * s] = F[lb + ls * s + lu * u];
     const double a0 = ca0, a1 = ca1;
-    // ---- row statistics over the finite sources (both lanes of the pair) ----------------------------------
+    // ---- row statistics over the finite sources (every lane of the group) ---------------------------------
     double pmn = o[0], pmx = o[0];
 #pragma unroll
     for (int j = 1; j < V; ++j) {
@@ -273,12 +316,18 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
     }
     pmn = fs_min(pmn, fs_swap(pmn));
     pmx = fs_max(pmx, fs_swap(pmx));
+    if constexpr (LN == 4) {
+      pmn = fs_min(pmn, fs_swap2(pmn));
+      pmx = fs_max(pmx, fs_swap2(pmx));
+    }
     const bool infrow = !(pmx < INFINITY);
     if (__ballot(infrow && pmn < INFINITY)) {  // some sources unreachable: the maximum over the finite ones
       double m2 = pmn;
 #pragma unroll
       for (int j = 0; j < V; ++j) m2 = fs_max(m2, o[j] < INFINITY ? o[j] : pmn);
-      pmx = fs_max(m2, fs_swap(m2));
+      m2 = fs_max(m2, fs_swap(m2));
+      if constexpr (LN == 4) m2 = fs_max(m2, fs_swap2(m2));
+      pmx = m2;
     }
     // ---- 32-bit fixed point: A_j = trunc((Ψ_j - Ψmin)/β · 2^Fb) << 7 | j (rank), +Inf = 2^30 -----------------
     // (β units, grid g = 2^-Fb with 2^(Fb+7) · rs < 2^30: every finite candidate value A + d·2^(Fb+7) stays below
@@ -303,54 +352,47 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
 #pragma unroll
     for (int s = 0; s < H; ++s)
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
-        const int t = x0 + N0 * s;
+      for (int u = 0; u < H0; ++u) {
+        const int t = u + H0 * s;
         // +Inf converts to 0xFFFFFFFF (clamped), which the min turns into 2^30
-        const unsigned q0 = (unsigned)__builtin_fma(o[t], sc, c0) << 7 | (unsigned)(x0 + N0 * x1v[s]);
+        const unsigned q0 = (unsigned)__builtin_fma(o[t], sc, c0) << 7 | (unsigned)(x0v[u] + N0 * x1v[s]);
         a[t] = min(q0, 0x40000000u);
       }
     __builtin_amdgcn_sched_barrier(0);
     FS_T(q1);
-    // ---- pass along x0: this lane's H lines are whole --------------------------------------------------------
+    // ---- pass along x0: this lane's H line pieces (orientation-free), then (LN = 4) the partner's boundary ----
 #pragma unroll
     for (int s = 0; s < H; ++s) {
 #pragma unroll
-      for (int x0 = 1; x0 < N0; ++x0) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[s * N0 + x0 - 1], U1, ntol);
+      for (int u = 1; u < H0; ++u) a[s * H0 + u] = fs_qmerge(a[s * H0 + u], a[s * H0 + u - 1], U1, ntol);
 #pragma unroll
-      for (int x0 = N0 - 2; x0 >= 0; --x0) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[s * N0 + x0 + 1], U1, ntol);
+      for (int u = H0 - 2; u >= 0; --u) a[s * H0 + u] = fs_qmerge(a[s * H0 + u], a[s * H0 + u + 1], U1, ntol);
+    }
+    if constexpr (LN == 4) {
+#pragma unroll
+      for (int s = 0; s < H; ++s) {
+        const unsigned pb = fs_swap2_u(a[s * H0 + H0 - 1]);
+#pragma unroll
+        for (int t = 0; t < H0; ++t)
+          a[s * H0 + H0 - 1 - t] = fs_qmerge(a[s * H0 + H0 - 1 - t], pb, (t + 1) * U1, ntol);
+      }
     }
     // ---- pass along x1: this lane's H slots (orientation-free), then the partner's boundary slot ------------
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
+    for (int u = 0; u < H0; ++u) {
 #pragma unroll
-      for (int s = 1; s < H; ++s) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[(s - 1) * N0 + x0], U1, ntol);
+      for (int s = 1; s < H; ++s) a[s * H0 + u] = fs_qmerge(a[s * H0 + u], a[(s - 1) * H0 + u], U1, ntol);
 #pragma unroll
-      for (int s = H - 2; s >= 0; --s) a[s * N0 + x0] = fs_qmerge(a[s * N0 + x0], a[(s + 1) * N0 + x0], U1, ntol);
+      for (int s = H - 2; s >= 0; --s) a[s * H0 + u] = fs_qmerge(a[s * H0 + u], a[(s + 1) * H0 + u], U1, ntol);
     }
 #pragma unroll
-    for (int x0 = 0; x0 < N0; ++x0) {
-      const unsigned pb = fs_swap_u(a[(H - 1) * N0 + x0]);
+    for (int u = 0; u < H0; ++u) {
+      const unsigned pb = fs_swap_u(a[(H - 1) * H0 + u]);
 #pragma unroll
-      for (int t = 0; t < H; ++t) a[(H - 1 - t) * N0 + x0] = fs_qmerge(a[(H - 1 - t) * N0 + x0], pb, (t + 1) * U1, ntol);
+      for (int t = 0; t < H; ++t) a[(H - 1 - t) * H0 + u] = fs_qmerge(a[(H - 1 - t) * H0 + u], pb, (t + 1) * U1, ntol);
     }
     __builtin_amdgcn_sched_barrier(0);
     FS_T(q2);
-    // ---- the segment below has published this step's outbox: load it (consumed in the write phase) --------
-    if (SEG && q > 0 && wait_flag(fl - 2, vin, need_in)) {
-      // LDS-DMA of the slot, 1 KiB chunks by wave (inline asm: the compiler does not make later LDS accesses
-      // wait for it; the drain before barrier 1 completes it, the barrier publishes it)
-      const char *slot = ring_in + (size_t)(i % NB) * A.slot_bytes;
-      const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)(fsm)) + A.stg * 8u;
-      for (int c = w; c < A.slot_bytes / 1024; c += nw) {
-        const char *gsrc = slot + c * 1024 + lane * 16;
-        const unsigned m0 = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)c * 1024u);
-        unsigned keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(gsrc), "s"(m0)
-                     : "memory");
-      }
-    }
     // ---- winners: R(l, j*) = fl(K_l[d(l, j*)] + Ψ_j*) for the certified winner j* ----------------------------
     // b̃_l = |ν0 - u0| + |ν1 - u1| splits into a wave-uniform x0 part (SGPRs) and this lane's x1 part per slot
     unsigned vmask = 0, smask = 0;
@@ -365,31 +407,38 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
       const int rr = abs(A.base1 + x1 - su1) - room - 1;  // + |ν0 - u0| < 0  <=>  b̃_l <= room
       const double *const Ks = Kt + N0 * x1 * ND;         // K_l[·] of l = x0 + N0·x1 at Ks + x0·ND
       const unsigned char *const Ds = Dt + N0 * x1 * L;   // d(l, ·) at Ds + x0·L
-      double kv[N0], pv[N0];
+      double kv[H0], pv[H0];
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
-        const unsigned jx = a[x0 + N0 * s] & 63u;
-        kv[x0] = Ks[x0 * ND + Ds[x0 * L + jx]];
-        pv[x0] = Frow[jx];
+      for (int u = 0; u < H0; ++u) {
+        const unsigned jx = a[u + H0 * s] & 63u;
+        kv[u] = Ks[x0v[u] * ND + Ds[x0v[u] * L + jx]];
+        pv[u] = Frow[jx];
       }
       // targets of this line inside the trust region: |ν0 - u0| <= room - |ν1 - u1| = -1 - rr is an interval of
       // x0 around u0 - base0 (wave-uniform), so the line's mask is a bit range
       {
         const int thr = -1 - rr, uc = su0 - A.base0;
         const int x0lo = max(uc - thr, 0), x0hi = min(uc + thr, N0 - 1);
-        const unsigned lm = thr >= 0 && x0lo <= x0hi ? ((2u << x0hi) - (1u << x0lo)) : 0u;
-        vmask |= lm << (N0 * s);
+        if constexpr (LN == 4) {  // this lane's half of the line, slot u = x0 (h0 = 0) or N0-1-x0 (mirrored)
+          const int ulo = h0 ? N0 - 1 - x0hi : x0lo, uhi = h0 ? N0 - 1 - x0lo : x0hi;
+          const int a0s = max(ulo, 0), a1s = min(uhi, H0 - 1);
+          const unsigned lm = thr >= 0 && a0s <= a1s ? ((2u << a1s) - (1u << a0s)) : 0u;
+          vmask |= lm << (H0 * s);
+        } else {
+          const unsigned lm = thr >= 0 && x0lo <= x0hi ? ((2u << x0hi) - (1u << x0lo)) : 0u;
+          vmask |= lm << (N0 * s);
+        }
       }
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
-        const int t = x0 + N0 * s;
+      for (int u = 0; u < H0; ++u) {
+        const int t = u + H0 * s;
         const unsigned av = a[t];
         // flagged and finite (below 2^30): bit 6 set, bit 30 clear -- integer arithmetic, a shift-or per target
         // (a condition would become a select between 0 and a materialised 1 << t per bit)
         const unsigned sb = ((av >> 6) & ~(av >> 30)) & 1u;
         smask |= sb << t;
         const bool fin = av < 0x40000000u;
-        const double sum = kv[x0] + pv[x0];
+        const double sum = kv[u] + pv[u];
         o[t] = fin ? sum : INFINITY;
         jw[t >> 2] |= (av & 63u) << (8 * (t & 3));
       }
@@ -406,10 +455,10 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
 #pragma unroll
       for (int s = 0; s < H; ++s)
 #pragma unroll
-        for (int x0 = 0; x0 < N0; ++x0) {
-          const int t = x0 + N0 * s;
+        for (int u = 0; u < H0; ++u) {
+          const int t = u + H0 * s;
           if ((smask >> t) & 1u) {
-            const int x1 = x1v[s], l = x0 + N0 * x1;
+            const int x0 = x0v[u], x1 = x1v[s], l = x0 + N0 * x1;
             double best = INFINITY;
             int bj = 0;
 #pragma unroll 4
@@ -461,8 +510,8 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
     // it, they would stay live through the whole read phase
     int tidw = tid;
     asm volatile("" : "+v"(tidw));
-    const int hfw = tidw & 1, cpw = lo + (tidw >> 1);
-    double *const padw = F + (cpw < hi ? cpw - lo : 0) * FS + L;  // this lane pair's pad word (never read)
+    const int hfw = tidw & 1, h0w = LN == 4 ? (tidw >> 1) & 1 : 0, cpw = lo + (tidw >> LSH);
+    double *const padw = F + (cpw < hi ? cpw - lo : 0) * FS + L;  // this lane group's pad word (never read)
 #pragma unroll
     for (int s = 0; s < H; ++s) {
       const int x1 = hfw ? N1 - 1 - s : s;
@@ -473,8 +522,8 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
       int ub = (int)__umul24((unsigned)(N0 * x1), (unsigned)R) + cb;
       asm volatile("" : "+v"(ub));
 #pragma unroll
-      for (int x0 = 0; x0 < N0; ++x0) {
-        const int t = x0 + N0 * s, bx0 = abs(A.base0 + x0 - su0);
+      for (int u = 0; u < H0; ++u) {
+        const int x0 = h0w ? N0 - 1 - u : u, t = u + H0 * s, bx0 = abs(A.base0 + x0 - su0);
         const bool v = (vmask >> t) & 1u;
         // branch-free: a target outside the trust region writes this row's pad word (column L) instead
         double *const dst = v ? Fw + (bx0 * FS + x0) : padw;
@@ -485,15 +534,15 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
     }
     FS_T(w1);
     // the outbox: targets above hi (only waves whose rows reach within SMAX of hi), sc1 stores into the ring
-    if (SEG && q < S - 1 && lo + 32 * (w + 1) + SMAX > hi) {
+    if (SEG && q < S - 1 && lo + RPW * (w + 1) + SMAX > hi) {
       const unsigned slot0 = (unsigned)(i % NB) * (unsigned)A.slot_bytes;
 #pragma unroll
       for (int s = 0; s < H; ++s) {
         const int x1 = hfw ? N1 - 1 - s : s;
         const int cb = cpw + abs(A.base1 + x1 - su1);
 #pragma unroll
-        for (int x0 = 0; x0 < N0; ++x0) {
-          const int t = x0 + N0 * s, c = cb + abs(A.base0 + x0 - su0);
+        for (int u = 0; u < H0; ++u) {
+          const int x0 = h0w ? N0 - 1 - u : u, t = u + H0 * s, c = cb + abs(A.base0 + x0 - su0);
           const bool v = ((vmask >> t) & 1u) && c >= hi;
           const double ov = o[t];
           __builtin_amdgcn_raw_buffer_store_b64(
@@ -597,14 +646,16 @@ bool fsep2_shape(const PyrGeom &G) {
   const int n0 = G.n[0], n1 = G.n[1];
   return G.M == 2 && ((n0 == 6 && n1 == 6) || (n0 == 4 && n1 == 4) || (n0 == 8 && n1 == 8) || (n0 == 8 && n1 == 4));
 }
-template <bool SEG>
+template <bool SEG, int LN>
 const void *fsep2_fn_t(const PyrGeom &G) {
-  return G.n[0] == 6 ? (const void *)k_fsep2<6, 6, SEG>
-         : G.n[0] == 4 ? (const void *)k_fsep2<4, 4, SEG>
-         : G.n[1] == 8 ? (const void *)k_fsep2<8, 8, SEG>
-                       : (const void *)k_fsep2<8, 4, SEG>;
+  return G.n[0] == 6 ? (const void *)k_fsep2<6, 6, SEG, LN>
+         : G.n[0] == 4 ? (const void *)k_fsep2<4, 4, SEG, LN>
+         : G.n[1] == 8 ? (const void *)k_fsep2<8, 8, SEG, LN>
+                       : (const void *)k_fsep2<8, 4, SEG, LN>;
 }
-const void *fsep2_fn(const PyrGeom &G, int S) { return S > 1 ? fsep2_fn_t<true>(G) : fsep2_fn_t<false>(G); }
+const void *fsep2_fn(const PyrGeom &G, const FsepPlan &p) {
+  return p.S == 1 ? fsep2_fn_t<false, 2>(G) : p.lanes == 4 ? fsep2_fn_t<true, 4>(G) : fsep2_fn_t<true, 2>(G);
+}
 }  // namespace
 
 bool fsep2_plan(const PyrGeom &G, int B, int S, FsepPlan *out) {
@@ -613,12 +664,20 @@ bool fsep2_plan(const PyrGeom &G, int B, int S, FsepPlan *out) {
   FsepPlan p;
   p.S = S;
   if (S == 1) {
+    p.lanes = 2;
     p.W = std::max(1, (R - 1 + 31) / 32);  // lane pairs for rows 0 .. 32W-1; row B beyond them is the extra row
     p.RS = 32 * p.W;
     p.rows = R;
   } else {
-    p.RS = 32 * std::max(1, (R - 1 + 32 * S - 1) / (32 * S));
-    p.W = p.RS / 32;
+    // segments: four lanes per row (16 rows per wave) where the segment still fits one workgroup, else two
+    p.lanes = 2;
+    if (FSEP_LANES4 && G.n[0] % 2 == 0) {
+      const int rs4 = 16 * std::max(1, (R - 1 + 16 * S - 1) / (16 * S));
+      if (64 * (rs4 / 16) <= FS2_MAXT) p.lanes = 4;
+    }
+    const int rpw = 64 / p.lanes;
+    p.RS = rpw * std::max(1, (R - 1 + rpw * S - 1) / (rpw * S));
+    p.W = p.RS / rpw;
     if ((S - 1) * p.RS >= R || p.RS < SMAX + 1) return false;  // an empty last segment / a halo past the next one
     p.rows = std::min(R, p.RS + 1 + SMAX);
   }
@@ -636,7 +695,7 @@ bool fsep2_plan(const PyrGeom &G, int B, int S, FsepPlan *out) {
 
 int fsep2_blocks_per_cu(const PyrGeom &G, const FsepPlan &p) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fsep2_fn(G, p.S), p.threads, p.lds) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fsep2_fn(G, p), p.threads, p.lds) != hipSuccess) return 0;
   return n;
 }
 
@@ -666,10 +725,10 @@ hipError_t launch_fsep2(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv,
   const dim3 grid((unsigned)(P.K * p.S)), block((unsigned)p.threads);
   if (p.S > 1) {  // the segments of a subproblem wait for each other: every workgroup must be resident
     void *args[] = {&Pc, &Lc, &A};
-    return hipLaunchCooperativeKernel(fsep2_fn(G, p.S), grid, block, args, (unsigned)p.lds, s);
+    return hipLaunchCooperativeKernel(fsep2_fn(G, p), grid, block, args, (unsigned)p.lds, s);
   }
   void *args[] = {&Pc, &Lc, &A};
-  return hipLaunchKernel(fsep2_fn(G, p.S), grid, block, args, p.lds, s);
+  return hipLaunchKernel(fsep2_fn(G, p), grid, block, args, p.lds, s);
 }
 
 #if defined(MIOC_STAMPS)

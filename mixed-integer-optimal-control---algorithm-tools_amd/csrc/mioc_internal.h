@@ -130,6 +130,7 @@ struct FsepPlan {
   int rows = 0, koff = 0;    // LDS front rows, K table offset (doubles)
   int stg = 0, slot_bytes = 0;  // S > 1: inbox staging offset (doubles), ring slot bytes
   int threads = 0;
+  int lanes = 2;  // lanes per budget row (4: row segments of small batches)
   size_t lds = 0;
 };
 bool fsep2_plan(const PyrGeom &G, int B, int S, FsepPlan *out);

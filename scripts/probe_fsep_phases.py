@@ -50,7 +50,7 @@ with native.Context(0) as ctx:
     buf = (ctypes.c_ulonglong * (nw * 8))()
     assert f(buf, nw) == 0
 a = np.array(buf, dtype=np.float64).reshape(nw, 8) / (nt - 1)
-wpb = 8 if d[8] <= 1 else max(1, 8 // d[8])  # waves per workgroup (B = 256)
+wpb = int(os.environ.get("FS_WPB", 8 if d[8] <= 1 else max(1, 8 // d[8])))  # waves per workgroup (B = 256; FS_WPB: four lanes per row)
 per_wave = a[: (len(a) // wpb) * wpb].reshape(-1, wpb, 8)
 a = a[a[:, 7] > 0]
 us = 1e3 * ms / (nt - 1)
