@@ -77,8 +77,8 @@ __device__ __forceinline__ double fs_max(double a, double b) {  // v_max_f64 wit
 
 template <int CTRL>
 __device__ __forceinline__ double fs_dpp(double x) {
-  return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false),
-                          __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false));
+  return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, true),
+                          __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, true));
 }
 __device__ __forceinline__ double fs_rdl(double x, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l), __builtin_amdgcn_readlane(__double2loint(x), l));
@@ -96,13 +96,13 @@ __device__ __forceinline__ double fs_wave_min(double v) {
 typedef unsigned fs_u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ unsigned fs_swap_u(unsigned x) {
-  return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
 }
 
 // the partner lane's (tid ^ 1) value: DPP quad_perm [1, 0, 3, 2], no LDS round trip
 __device__ __forceinline__ double fs_swap(double x) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0xB1, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0xB1, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0xB1, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0xB1, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
 
@@ -138,11 +138,11 @@ struct FsepArgs {
 
 // the partner lane's (tid ^ 2) value: DPP quad_perm [2, 3, 0, 1]
 __device__ __forceinline__ unsigned fs_swap2_u(unsigned x) {
-  return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);
 }
 __device__ __forceinline__ double fs_swap2(double x) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0x4E, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0x4E, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0x4E, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0x4E, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
 

@@ -10,11 +10,13 @@
 // In real arithmetic min_j (Ψ_j + β·d(l,j)) is an L1 distance transform, separable over the grid
 // dimensions: M one-dimensional passes, each a forward and a backward sweep along the 8 levels of one
 // dimension.  The transform runs in exact fixed-point arithmetic inside one binade of doubles:
-//   - each finite Ψ_j becomes V_j = base + (Ψ_j - Ψmin)/β, truncated to the grid g = 2^13 ulp(base), with
-//     the source rank j in the 12 low mantissa bits (the payload) and bit 12 as the "near tie" flag;
+//   - each finite Ψ_j becomes V_j = base + (Ψ_j - Ψmin)/β, truncated to the grid g = 2^18 ulp(base), with
+//     the source rank j in mantissa bits 6..17 and a near-tie count in bits 0..5 (the payload);
 //   - a unit step costs exactly 1.0 (a multiple of g), so every sum is exact and keeps its payload, and
 //     v_min_f64 carries the winner's rank through every pass for free;
-//   - every merge of two disjoint candidate sets whose values differ by <= tol sets the flag.
+//   - every merge of two disjoint candidate sets whose values differ by <= tol adds one to the count of its result
+//     (one v_addc on the low word: a value passes at most 14 merges per pass, 56 in all, so the count never reaches
+//     the rank bits); a nonzero count is the "near tie" flag.
 // Invariant: an unflagged result's rank j* beats every other source by more than tol in the exact
 // fixed-point values.  tol covers twice the stamping error (< g) plus twice the reference's own rounding
 // error (<= 4u·|T1 + β·d + Ψ|), so then R(l, j) > R(l, j*) for all j != j*: j* is the reference's unique
@@ -38,8 +40,10 @@
 namespace mioc {
 
 constexpr int SD_RB = 12;                // payload rank bits (L <= 4096)
-constexpr int SD_FLAG = 1 << SD_RB;      // near-tie flag (payload bit 12)
-constexpr int SD_PAY = 2 * SD_FLAG - 1;  // payload mask: 13 low mantissa bits
+constexpr int SD_CB = 6;                 // payload near-tie count bits, below the rank (at most 56 merges per value)
+constexpr int SD_CNT = (1 << SD_CB) - 1; // near-tie count mask: nonzero = flagged
+constexpr int SD_PAY = (1 << (SD_CB + SD_RB)) - 1;  // payload mask: 18 low mantissa bits
+constexpr int SD_GRID = 52 - SD_CB - SD_RB;         // g = 2^(E - SD_GRID) for the binade [2^E, 2^(E+1))
 constexpr int SD_COOP = 8;               // listed targets up to this many: whole-workgroup scans, else one wave each
 constexpr int SD_FEW = 4;                // rows with at most this many targets go straight to the exact scan
 constexpr int SD_SPARSE = 4;             // rows with at most this many finite sources: direct minimum over them
@@ -163,20 +167,21 @@ __device__ __forceinline__ int sd_tid() {
 // the wave, which the persistent driver keeps in flight across the row body on purpose
 __device__ __forceinline__ void sd_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// merge two disjoint candidate sets (their minima a, b): the smaller keeps its payload; a near tie sets
-// the flag.  |a - b| is exact (one binade), +Inf - +Inf is NaN and never flags.
+// merge two disjoint candidate sets (their minima a, b): the smaller keeps its payload; a near tie counts
+// one.  |a - b| is exact (one binade), +Inf - +Inf is NaN and never flags.
 __device__ __forceinline__ double sd_merge(double a, double b, double tol) {
   const double m = sd_min(a, b);
   const bool close = fabs(a - b) <= tol;
-  return __hiloint2double(__double2hiint(m), __double2loint(m) | (close ? SD_FLAG : 0));
+  return __hiloint2double(__double2hiint(m), (int)((unsigned)__double2loint(m) + (close ? 1u : 0u)));  // v_addc
 }
 
 // Wave-wide reductions through DPP (no LDS round trip, unlike __shfl_xor's ds_bpermute): four steps leave every
 // lane with its 16-lane row's result (quad_perm xor 1, xor 2, row_half_mirror, row_mirror), then the four row
-// results are read as scalars.
+// results are read as scalars.  bound_ctrl: every lane has a source under these controls, so no old value is
+// needed (and no register initialised for it).
 template <int CTRL>
 __device__ __forceinline__ int sd_dpp_i(int x) {
-  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ double sd_dpp_d(double x) {
@@ -523,12 +528,12 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
   const bool empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || !(pmn < INFINITY))) != 0;  // uniform
 
-  // ---- the binade: values base + (Ψ - Ψmin)/β + d lie in [base, 2·base), grid g = 2^13 ulp ----------
+  // ---- the binade: values base + (Ψ - Ψmin)/β + d lie in [base, 2·base), grid g = 2^18 ulp ----------
   const double inv = Lv.inv_beta;                      // fl(1/β), host-computed
   const double rs = (pmx - pmn) * inv + (double)Smax;  // scaled range of every transform value
-  const bool scale_ok = rs < 0x1p36;                   // else unit steps are not on the grid: exact scans
-  const int E = ilogb(fmin(rs, 0x1p36) * (1.0 + 0x1p-20) + 1.0) + 2;  // 2^E >= 2·rs
-  const double base = ldexp(1.0, E), g = ldexp(1.0, E - 39);
+  const bool scale_ok = rs < 0x1p31;                   // else unit steps are not on the grid: exact scans
+  const int E = ilogb(fmin(rs, 0x1p31) * (1.0 + 0x1p-20) + 1.0) + 2;  // 2^E >= 2·rs (E <= SD_GRID: g <= 1)
+  const double base = ldexp(1.0, E), g = ldexp(1.0, E - SD_GRID);
   double qmax = beta * (double)Smax + fmax(fabs(pmn), fabs(pmx));  // >= |T1 + β·d + Ψ| for every candidate
 #pragma unroll
   for (int m = 0; m < M; ++m) qmax += fabs(a[m]) * (double)max(abs(lb[m]), abs(lb[m] + 7));
@@ -572,7 +577,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
         double V = INFINITY;
         if (x < INFINITY) {
           const double y = (x - pmn) * inv + base;
-          V = __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | j);
+          V = __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | (j << SD_CB));
         }
         dtv[sd_swz(j)] = V;
       }
@@ -647,18 +652,18 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       int jx[8];
       double pv[8];
 #pragma unroll
-      for (int x = 0; x < 8; ++x) jx[x] = __double2loint(o[x]) & (SD_FLAG - 1);  // +Inf carries payload 0
+      for (int x = 0; x < 8; ++x) jx[x] = (__double2loint(o[x]) >> SD_CB) & ((1 << SD_RB) - 1);  // +Inf: payload 0
 #pragma unroll
       for (int x = 0; x < 8; ++x) pv[x] = psi[jx[x]];
 #pragma unroll
       for (int x = 0; x < 8; ++x) {
         const int r = tid | (x << (3 * (M - 1))), j = jx[x];
         const bool fin = (valid >> x & 1) && o[x] < INFINITY;
-        const bool flg = (__double2loint(o[x]) & SD_FLAG) != 0;
+        const bool flg = (__double2loint(o[x]) & SD_CNT) != 0;
         // d(l, j*) exactly: an unflagged finite o[x] is V_j* + d with V_j* = the stamp of Ψ_j* (the same expression
         // as the stamping above, payload j*), every term exact in the binade (garbage, unused, otherwise)
         const double y = (pv[x] - pmn) * inv + base;
-        const double dd = o[x] - __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | j);
+        const double dd = o[x] - __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | (j << SD_CB));
         const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
         const double val = (t1 + beta * dd) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
         listed |= (unsigned)(fin && flg) << x;
