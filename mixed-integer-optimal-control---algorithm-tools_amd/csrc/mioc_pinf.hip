@@ -206,7 +206,16 @@ __device__ __forceinline__ double pvmin(double a, double b) {
 // read.  Class rows for CH steps at a time are staged into LDS by LDS-DMA one chunk ahead; the barrier
 // per step waits only on LDS (lgkmcnt), so the streamed R_i stores and the next chunk's DMA stay in
 // flight.  Four independent min accumulators per output keep the dependency chain short.
+// G > 1 (few subproblems, so one workgroup per subproblem leaves most of the CU idle): G adjacent lanes share a row
+// pair, each taking BWP/G of the classes over a window of BWP/G + 1 values; their partial minima combine by DPP
+// (min is exact, so the result is the same whatever the grouping, and every candidate fl(Kmin_i[b] + R_{i+1}[c-b])
+// is the same expression).  C4 at p = Inf: 10 waves instead of 3, each with a quarter of the chain.
 // ---------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double pv_dpp(double x) {
+  return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xF, 0xF, true),
+                          __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xF, 0xF, true));
+}
 #ifdef MIOC_STAMPS
 // diagnostic build: per-wave phase cycles of workgroup 0 (s_memtime): [0] window + class reads waited,
 // [1] min-plus VALU + stores, [2] barrier, [3] steps, [4] total
@@ -216,18 +225,21 @@ __device__ unsigned long long g_pinf_stamps[16][8];
 #define PI_T(v)
 #endif
 
-template <int BWP>
-__global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int CH) {
+template <int BWP, int G>
+__global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P, PinfDev D, int CH) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  constexpr int NP = BWP / 2 + 1;  // 16-byte pieces of a window
-  const int RP = P.RP, B = P.B, nt = P.nt, k = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  constexpr int CB = BWP / G;     // classes per lane
+  constexpr int NP = CB / 2 + 1;  // 16-byte pieces of a lane's window
+  static_assert(G == 1 || (G == 4 && CB % 2 == 0), "k_pinf_recur: G = 1 or 4");
+  const int RP = P.RP, B = P.B, nt = P.nt, k = blockIdx.x, nthr = blockDim.x / G;
+  const int tid = (int)threadIdx.x / G, h = (int)threadIdx.x % G;  // row pair slot, class quarter
   const int AW = RP + BWP;                     // even: RP is a multiple of 64
   double *A = sm, *Kbuf = sm + 2 * AW;         // A: [2 parities][AW]; Kbuf: [2][CH][BWP]
   const double *kmin = D.kmin + (size_t)k * nt * BWP;
   double *R = D.R + (size_t)k * nt * RP;
   {
     const int pt = (nt - 1) & 1;  // terminal row R_{n-1}[c] = Kmin_{n-1}[c] (class minima of T1, no β)
-    for (int q = tid; q < 2 * AW; q += nthr) {
+    for (int q = (int)threadIdx.x; q < 2 * AW; q += (int)blockDim.x) {
       const int par = q / AW, kk = q % AW, c = kk + 1 - BWP;
       double v = INFINITY;
       if (par == pt && c >= 0 && c < BWP) v = kmin[(size_t)(nt - 1) * BWP + c];
@@ -237,21 +249,23 @@ __global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int
   }
   if (nt < 2) return;
   int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
-  glds_copy(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, tid, nthr);
+  glds_copy(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, (int)threadIdx.x, (int)blockDim.x);
   vm_drain();
   lds_barrier();
   for (int q = 0; hi >= 0; ++q) {
     const double *Kc = Kbuf + (size_t)(q & 1) * CH * BWP;
     const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
     if (nhi >= 0)
-      glds_copy(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8, tid,
-                nthr);
+      glds_copy(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
+                (int)threadIdx.x, (int)blockDim.x);
     for (int i = hi; i >= lo; --i) {
       PI_T(t0);
       for (int c0 = 2 * tid; c0 < RP; c0 += 2 * nthr) {
-        const double2 *win = reinterpret_cast<const double2 *>(A + (size_t)((i + 1) & 1) * AW + c0);
-        const double2 *kr = reinterpret_cast<const double2 *>(Kc + (size_t)(i - lo) * BWP);
-        double w[2 * NP], kv[BWP];
+        // this lane's classes b = h·CB + bb: row 2t reads R_{i+1}[c0 - b] = A[c0 + BWP - 1 - b], a window of CB + 1
+        // values from A[c0 + BWP - (h + 1)·CB] (even: 16-byte aligned)
+        const double2 *win = reinterpret_cast<const double2 *>(A + (size_t)((i + 1) & 1) * AW + c0 + BWP - (h + 1) * CB);
+        const double2 *kr = reinterpret_cast<const double2 *>(Kc + (size_t)(i - lo) * BWP + h * CB);
+        double w[2 * NP], kv[CB];
 #pragma unroll
         for (int p2 = 0; p2 < NP; ++p2) {
           const double2 x = win[p2];
@@ -259,7 +273,7 @@ __global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int
           w[2 * p2 + 1] = x.y;
         }
 #pragma unroll
-        for (int p2 = 0; p2 < BWP / 2; ++p2) {
+        for (int p2 = 0; p2 < CB / 2; ++p2) {
           const double2 y = kr[p2];
           kv[2 * p2] = y.x;
           kv[2 * p2 + 1] = y.y;
@@ -267,29 +281,39 @@ __global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int
 #ifdef MIOC_STAMPS
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PI_T(t1);
-        if (blockIdx.x == 0 && (tid & 63) == 0 && c0 == 2 * tid) g_pinf_stamps[tid >> 6][0] += t1 - t0;
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && c0 == 2 * tid) g_pinf_stamps[threadIdx.x >> 6][0] += t1 - t0;
 #endif
-        // row 2t:   R_{i+1}[2t - b]   = w[BWP - 1 - b];   row 2t+1: R_{i+1}[2t + 1 - b] = w[BWP - b]
+        // row 2t:   R_{i+1}[2t - b]   = w[CB - 1 - bb];   row 2t+1: R_{i+1}[2t + 1 - b] = w[CB - bb]
         double m0[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, m1[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
 #pragma unroll
-        for (int b2 = 0; b2 < BWP; ++b2) {
-          m0[b2 & 3] = pvmin(m0[b2 & 3], kv[b2] + w[BWP - 1 - b2]);
-          m1[b2 & 3] = pvmin(m1[b2 & 3], kv[b2] + w[BWP - b2]);
+        for (int b2 = 0; b2 < CB; ++b2) {
+          m0[b2 & 3] = pvmin(m0[b2 & 3], kv[b2] + w[CB - 1 - b2]);
+          m1[b2 & 3] = pvmin(m1[b2 & 3], kv[b2] + w[CB - b2]);
         }
-        const double r0 = pvmin(pvmin(m0[0], m0[1]), pvmin(m0[2], m0[3]));
-        const double r1 = pvmin(pvmin(m1[0], m1[1]), pvmin(m1[2], m1[3]));
+        double r0 = pvmin(pvmin(m0[0], m0[1]), pvmin(m0[2], m0[3]));
+        double r1 = pvmin(pvmin(m1[0], m1[1]), pvmin(m1[2], m1[3]));
+        if constexpr (G == 4) {  // the four class quarters of the lane quad (quad_perm xor 1, xor 2)
+          r0 = pvmin(r0, pv_dpp<0xB1>(r0));
+          r1 = pvmin(r1, pv_dpp<0xB1>(r1));
+          r0 = pvmin(r0, pv_dpp<0x4E>(r0));
+          r1 = pvmin(r1, pv_dpp<0x4E>(r1));
+        }
         double *Aout = A + (size_t)(i & 1) * AW;
-        Aout[c0 + BWP - 1] = r0;
-        Aout[c0 + BWP] = r1;
-        R[(size_t)i * RP + c0] = c0 <= B ? r0 : INFINITY;
-        R[(size_t)i * RP + c0 + 1] = c0 + 1 <= B ? r1 : INFINITY;
+        if (G == 1 || h == 0) {
+          Aout[c0 + BWP - 1] = r0;
+          R[(size_t)i * RP + c0] = c0 <= B ? r0 : INFINITY;
+        }
+        if (G == 1 || h == 1) {
+          Aout[c0 + BWP] = r1;
+          R[(size_t)i * RP + c0 + 1] = c0 + 1 <= B ? r1 : INFINITY;
+        }
       }
       PI_T(t2);
       lds_barrier();
 #ifdef MIOC_STAMPS
       PI_T(t3);
-      if (blockIdx.x == 0 && (tid & 63) == 0) {
-        unsigned long long *g = g_pinf_stamps[tid >> 6];
+      if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {
+        unsigned long long *g = g_pinf_stamps[threadIdx.x >> 6];
         g[1] += t2 - t0;  // minus slot 0 afterwards
         g[2] += t3 - t2;
         g[3] += 1;
@@ -305,19 +329,36 @@ __global__ __launch_bounds__(512) void k_pinf_recur(ProblemDev P, PinfDev D, int
 }
 
 int pinf_chunk_recur(int BWP) { return BWP <= 16 ? 64 : 32; }
+#ifndef PINF_RECUR_SPLIT
+#define PINF_RECUR_SPLIT 1  // few subproblems: four lanes per row pair (A/B builds: 0)
+#endif
 
 hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D) {
-  int threads = ((P.RP / 2 + 63) / 64) * 64;  // one thread per two budget rows
-  if (threads > 512) threads = 512;
+  int pairs = ((P.RP / 2 + 63) / 64) * 64;  // one thread (G = 1) or lane quad (G = 4) per two budget rows
+  if (pairs > 512) pairs = 512;
+  // few subproblems (fewer workgroups than a quarter of the CUs): four lanes per row pair; a batch keeps one lane
+  // (its workgroups already fill the CUs, and the recursion is then bound by the R stores)
+  int ncu = 0, dev = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int G = PINF_RECUR_SPLIT && P.K * 4 <= ncu && D.BWP >= 8 ? 4 : 1;
+  if (G == 4 && pairs > 256) pairs = 256;
+  const int threads = pairs * G;
   const int CH = pinf_chunk_recur(D.BWP);
   size_t lds = (size_t)(2 * (D.BWP + P.RP) + 2 * CH * D.BWP) * sizeof(double);
+#define PINF_RECUR(BW)                                                                                    \
+  if (G == 4)                                                                                             \
+    hipLaunchKernelGGL((k_pinf_recur<BW, 4>), dim3(P.K), dim3(threads), lds, s, P, D, CH);                \
+  else                                                                                                    \
+    hipLaunchKernelGGL((k_pinf_recur<BW, 1>), dim3(P.K), dim3(threads), lds, s, P, D, CH);
   switch (D.BWP) {
-    case 8: hipLaunchKernelGGL(k_pinf_recur<8>, dim3(P.K), dim3(threads), lds, s, P, D, CH); break;
-    case 16: hipLaunchKernelGGL(k_pinf_recur<16>, dim3(P.K), dim3(threads), lds, s, P, D, CH); break;
-    case 32: hipLaunchKernelGGL(k_pinf_recur<32>, dim3(P.K), dim3(threads), lds, s, P, D, CH); break;
-    case 64: hipLaunchKernelGGL(k_pinf_recur<64>, dim3(P.K), dim3(threads), lds, s, P, D, CH); break;
+    case 8: PINF_RECUR(8) break;
+    case 16: PINF_RECUR(16) break;
+    case 32: PINF_RECUR(32) break;
+    case 64: PINF_RECUR(64) break;
     default: return hipErrorInvalidValue;
   }
+#undef PINF_RECUR
   return hipGetLastError();
 }
 
