@@ -230,7 +230,7 @@ __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int CB = BWP / G;     // classes per lane
   constexpr int NP = CB / 2 + 1;  // 16-byte pieces of a lane's window
-  static_assert(G == 1 || (G == 4 && CB % 2 == 0), "k_pinf_recur: G = 1 or 4");
+  static_assert(G == 1 || ((G == 2 || G == 4) && CB % 2 == 0), "k_pinf_recur: G = 1, 2 or 4");
   const int RP = P.RP, B = P.B, nt = P.nt, k = blockIdx.x, nthr = blockDim.x / G;
   const int tid = (int)threadIdx.x / G, h = (int)threadIdx.x % G;  // row pair slot, class quarter
   const int AW = RP + BWP;                     // even: RP is a multiple of 64
@@ -292,9 +292,11 @@ __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P
         }
         double r0 = pvmin(pvmin(m0[0], m0[1]), pvmin(m0[2], m0[3]));
         double r1 = pvmin(pvmin(m1[0], m1[1]), pvmin(m1[2], m1[3]));
-        if constexpr (G == 4) {  // the four class quarters of the lane quad (quad_perm xor 1, xor 2)
+        if constexpr (G >= 2) {  // the class parts of the lane group (quad_perm xor 1, then xor 2)
           r0 = pvmin(r0, pv_dpp<0xB1>(r0));
           r1 = pvmin(r1, pv_dpp<0xB1>(r1));
+        }
+        if constexpr (G == 4) {
           r0 = pvmin(r0, pv_dpp<0x4E>(r0));
           r1 = pvmin(r1, pv_dpp<0x4E>(r1));
         }
@@ -330,7 +332,10 @@ __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P
 
 int pinf_chunk_recur(int BWP) { return BWP <= 16 ? 64 : 32; }
 #ifndef PINF_RECUR_SPLIT
-#define PINF_RECUR_SPLIT 1  // few subproblems: four lanes per row pair (A/B builds: 0)
+#define PINF_RECUR_SPLIT 1  // few subproblems: G lanes per row pair (A/B builds: 0)
+#endif
+#ifndef PINF_RECUR_G
+#define PINF_RECUR_G 4      // lanes per row pair when split (2 or 4)
 #endif
 
 hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D) {
@@ -341,14 +346,16 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
   int ncu = 0, dev = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  const int G = PINF_RECUR_SPLIT && P.K * 4 <= ncu && D.BWP >= 8 ? 4 : 1;
-  if (G == 4 && pairs > 256) pairs = 256;
+  const int G = PINF_RECUR_SPLIT && P.K * 4 <= ncu && D.BWP >= 8 ? PINF_RECUR_G : 1;
+  if (G * pairs > 1024) pairs = 1024 / G;
   const int threads = pairs * G;
   const int CH = pinf_chunk_recur(D.BWP);
   size_t lds = (size_t)(2 * (D.BWP + P.RP) + 2 * CH * D.BWP) * sizeof(double);
 #define PINF_RECUR(BW)                                                                                    \
   if (G == 4)                                                                                             \
     hipLaunchKernelGGL((k_pinf_recur<BW, 4>), dim3(P.K), dim3(threads), lds, s, P, D, CH);                \
+  else if (G == 2)                                                                                        \
+    hipLaunchKernelGGL((k_pinf_recur<BW, 2>), dim3(P.K), dim3(threads), lds, s, P, D, CH);                \
   else                                                                                                    \
     hipLaunchKernelGGL((k_pinf_recur<BW, 1>), dim3(P.K), dim3(threads), lds, s, P, D, CH);
   switch (D.BWP) {
