@@ -74,22 +74,31 @@ __global__ void k_validate(ProblemDev P, const double *__restrict__ numin, const
                            int32_t *flags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
-  if (i >= P.nt) return;
-  const double *dfi = P.df + ((size_t)k * P.nt + i) * P.M;
-  const double *uoi = P.uold + ((size_t)k * P.nt + i) * P.M;
-  int bad = 0;
-  long long bmax = 0;
-  for (int m = 0; m < P.M; ++m) {
-    double d = dfi[m];
-    if (!(fabs(d) <= 1.7976931348623157e308)) bad |= 1;
-    double u = uoi[m];
-    if (!(u == floor(u)) || !(fabs(u) < 4.0e15)) bad |= 2;
-    double e = fmax(fabs(numax[m] - u), fabs(numin[m] - u));
-    bmax += (e > 1.0e9 || e != e) ? 1000000000LL : (long long)e;
+  int bad = 0, bm = 0;
+  if (i < P.nt) {
+    const double *dfi = P.df + ((size_t)k * P.nt + i) * P.M;
+    const double *uoi = P.uold + ((size_t)k * P.nt + i) * P.M;
+    long long bmax = 0;
+    for (int m = 0; m < P.M; ++m) {
+      double d = dfi[m];
+      if (!(fabs(d) <= 1.7976931348623157e308)) bad |= 1;
+      double u = uoi[m];
+      if (!(u == floor(u)) || !(fabs(u) < 4.0e15)) bad |= 2;
+      double e = fmax(fabs(numax[m] - u), fabs(numin[m] - u));
+      bmax += (e > 1.0e9 || e != e) ? 1000000000LL : (long long)e;
+    }
+    bm = bmax > (long long)P.B ? P.B : (int)bmax;
   }
-  if (bad) atomicOr(&flags[0], bad);
-  int bm = bmax > (long long)P.B ? P.B : (int)bmax;
-  atomicMax(&flags[1], bm);
+  // one pair of atomics per wave (one per thread serialised on the two flag words: 0.4 ms at 1024 x 4096 steps)
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    bad |= __shfl_xor(bad, off);
+    bm = max(bm, __shfl_xor(bm, off));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (bad) atomicOr(&flags[0], bad);
+    if (bm > 0) atomicMax(&flags[1], bm);
+  }
 }
 
 hipError_t launch_validate(hipStream_t s, const ProblemDev &P, const double *numin, const double *numax,
