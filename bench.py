@@ -671,7 +671,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded N(0,1) df, rand_func_int-shaped u_old; SURVEY §8 d)",
             "config": {"workload": workload(res),
-                       "parallelism": f"dp{world} (independent subproblems, RCCL broadcast + gather of results)"},
+                       "parallelism": f"dp{world} (independent subproblems" +
+                                      ("; one GPU, no collective)" if world == 1 else
+                                       "; RCCL broadcast of the problem, gather of the controls)")},
             "algorithm": {native_name(res["algo"]): res["dom_name"]},
             "checksum": res.get("gathered_checksum"),
         }
