@@ -440,7 +440,8 @@ __device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restr
 // caller's outstanding loads or stores.
 template <int M, bool PERSIST, class Hooks>
 __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int k, int cp,
-                                         int i, double (&v)[8], const uint32_t *pin, const uint32_t *pout,
+                                         int i, double (&v)[8], const uint2 (&ein_in)[4], const uint32_t *pin,
+                                         const uint32_t *pout,
                                          double *Sout, uint16_t *UU, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
                                          unsigned char *sds, Hooks &h, const double *__restrict__ df_all,
                                          const double *__restrict__ uo_all) {
@@ -462,9 +463,11 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   const double *uoi = PERSIST ? dfi + M : uo_all + ((size_t)k * P.nt + i) * M;
   SD_RSTAMP(13);
   SD_STAMP(0);
+  // this thread's sphere-order entries (rank | b̃ << 16 at its eight positions of step i+1): read by the caller (the
+  // persistent driver kept them from issuing this row's loads, so no LDS round trip starts the row)
   uint2 ein[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) ein[q] = *reinterpret_cast<const uint2 *>(pin + 2 * (tid + T * q));
+  for (int q = 0; q < 4; ++q) ein[q] = ein_in[q];
   // ---- this thread's targets: ranks tid | x << 3(M-1) (the lines of the last pass) -----------------
   double a[M];
   int lb[M], uo[M];
@@ -1070,7 +1073,10 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
     sd_issue_loads<M, false>(v, slot, cp, Sin_all + (size_t)k * s_stride, (P.B + 1) * L * (int)sizeof(double),
                              nullptr);
     SdHooksNone hooks;
-    sdt_body<M, false>(P, Lv, G, k, cp, i, v, slot, slot + L, Sout_all + (size_t)k * s_stride + (size_t)cp * L,
+    uint2 ein[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ein[q] = *reinterpret_cast<const uint2 *>(slot + 2 * (tid + (L / 8) * q));
+    sdt_body<M, false>(P, Lv, G, k, cp, i, v, ein, slot, slot + L, Sout_all + (size_t)k * s_stride + (size_t)cp * L,
                        UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(P.B + 1) * L) + (size_t)cp * L, sh,
                        sds, hooks, P.df, P.uold);
     if (tid == 0) {
@@ -1189,6 +1195,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_row0(ProblemDev P, Lev
 struct SdRaw {
   sd_u32x4 a[4];
   sd_u32x2 b[4];
+  uint2 e[4];     // the sphere-order entries the offsets came from (the row body's `ein`)
   unsigned mask;  // per pair q: bit 3q the first element has no source row, 3q+1 the second, 3q+2 it straddles
 };
 template <int M>
@@ -1199,6 +1206,8 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
   uint2 e[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) e[q] = *reinterpret_cast<const uint2 *>(pin + 2 * (tid + T * q));  // reads first
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w.e[q] = e[q];
   // an offset beyond the resource's range drops the access (the load returns 0 without touching memory): rows
   // below 0, and the second element wherever the pair does not straddle (it came with the first)
   constexpr unsigned OOB = 0xFFFFFFF0u;
@@ -1433,7 +1442,10 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       // u_old(i+1) has b̃ >= 1 everywhere and no such source
       if (hi - lo == 1 && h.pcp >= 0 && tid == 0 && (pslot(i + 1)[0] >> 16) == 0)
         v[0] = status == 1 ? INFINITY : dtv[pslot(i + 1)[0] & 0xFFFFu];
-      status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, pslot(i + 1), pslot(i),
+      uint2 ein[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ein[q] = h.raw.e[q];
+      status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, ein, pslot(i + 1), pslot(i),
                                  reg + (size_t)(i % NB) * R * L + (size_t)cp * L,
                                  UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L, sh,
                                  sds, h, df_all, uo_all);
