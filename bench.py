@@ -318,9 +318,10 @@ def roofline_of(res):
         # k_sdt_run is one persistent launch over all nt - 1 steps
         steps = (nt - 1) if name == "k_sdt_run" else 1
         bytes_per_launch = steps * K * (B + 1) * L * (8 + 8 + 2)
-        # per pass and 8-point line: 14 merges (7 forward, 7 backward), each add + min + sub + cmp (4 FP64 ops)
-        ops = 1.0 * steps * K * (B + 1) * L * M * (14 / 8) * 4
-        note = "separable transform FP64 ops (4 per merge); brute-force-equivalent candidates/s = " \
+        # per pass and 8-point line: 14 merges (7 forward, 7 backward), each add + min + sub + cmp (4 FP64 ops) and the
+        # near-tie count's v_addc
+        ops = 1.0 * steps * K * (B + 1) * L * M * (14 / 8) * 5
+        note = "separable transform VALU ops (5 per merge, 4 of them FP64); brute-force-equivalent candidates/s = " \
                f"{steps * K * ncand_step / avg_s:.4g}"
     elif name in ("k_fused_run", "k_fsep_run", "k_fsep2"):
         # one launch = every step of K subproblems; the value fronts never leave the CU's LDS, so the HBM bytes
@@ -377,7 +378,35 @@ def roofline_of(res):
             "frac": round(ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS, 6)}
     if note:
         valu["note"] = note
+    if name == "k_sdt_run":
+        per_item, src = pmc_valu_per_wave_item(name)
+        if per_item:
+            # two waves per SIMD (512 threads, one workgroup per CU), 4 cycles per wave64 VALU instruction, 2.4 GHz
+            valu["pmc_valu_instructions_per_wave_item"] = round(per_item, 1)
+            valu["pmc_valu_issue_frac"] = round(2 * per_item * 4 / (avg_s / steps * 2.4e9), 3)
+            valu["pmc_source"] = src
     return roof, valu
+
+
+def pmc_valu_per_wave_item(kernel):
+    """SQ_INSTS_VALU / SQ_WAVES / items per wave of `kernel` from the newest committed PMC pass
+    (profiles/roundN_*_pmc_valu_*_ntT.csv, scripts/gpu_pmc_valu.sh: one DP row item per wave and step), or None."""
+    import csv
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*_pmc_valu_*_nt*.csv")))
+    if not files:
+        return None, None
+    f = files[-1]
+    nt = int(re.search(r"_nt(\d+)", f).group(1))
+    v = {}
+    with open(f) as fh:
+        for r in csv.DictReader(fh):
+            if kernel in r["Kernel_Name"]:
+                v[r["Counter_Name"]] = float(r["Counter_Value"])
+    if not v.get("SQ_INSTS_VALU") or not v.get("SQ_WAVES"):
+        return None, None
+    return v["SQ_INSTS_VALU"] / v["SQ_WAVES"] / (nt - 1), os.path.relpath(f, ROOT)
 
 
 def _cpu_info():
