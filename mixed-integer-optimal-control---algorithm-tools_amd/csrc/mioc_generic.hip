@@ -89,7 +89,8 @@ __global__ void k_validate(ProblemDev P, const double *__restrict__ numin, const
     }
     bm = bmax > (long long)P.B ? P.B : (int)bmax;
   }
-  // one pair of atomics per wave (one per thread serialised on the two flag words: 0.4 ms at 1024 x 4096 steps)
+  // at most one pair of atomics per wave, and the maximum only when it raises the value already there: same-address
+  // atomics serialise at the L2 (one per thread, or even one per wave, took 0.4-0.75 ms at 1024 x 4096 steps)
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     bad |= __shfl_xor(bad, off);
@@ -97,7 +98,7 @@ __global__ void k_validate(ProblemDev P, const double *__restrict__ numin, const
   }
   if ((threadIdx.x & 63) == 0) {
     if (bad) atomicOr(&flags[0], bad);
-    if (bm > 0) atomicMax(&flags[1], bm);
+    if (bm > 0 && bm > __hip_atomic_load(&flags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&flags[1], bm);
   }
 }
 
