@@ -140,7 +140,8 @@ int32_t mioc_backtrack_batch_device(mioc_ctx *ctx, int64_t B_use, double *d_u_ou
                                     int32_t *d_status);
 /* The same with one budget per subproblem: d_B_use[k] (device, K int32, each 0 <= B_use[k] <= B) -- the
  * per-restart trust-region radii after halving (multi-trust.jl:108-110, B_new = floor(Δᵏ/Δt) per restart).
- * Reads the K budgets back once to validate them. */
+ * The budgets are validated on the device (no host read-back): a B_use[k] outside [0, B] makes d_status[k] =
+ * MIOC_ESTATE and leaves subproblem k's u row NaN; the call itself returns MIOC_OK. */
 int32_t mioc_backtrack_batch_budgets_device(mioc_ctx *ctx, const int32_t *d_B_use, double *d_u_out, double *d_phi_star,
                                             int32_t *d_status);
 int32_t mioc_synchronize(mioc_ctx *ctx);

@@ -858,12 +858,9 @@ int32_t mioc_backtrack_batch_budgets_device(mioc_ctx *ctx, const int32_t *d_B_us
   if (rc) return rc;
   if (!d_u_out || !d_B_use) return fail(ctx, MIOC_EINVAL, "null pointer");
   if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "backtrack called before bellman");
-  // the per-subproblem budgets must lie in [0, B]; checked on the device copy (a few bytes per subproblem)
-  std::vector<int32_t> hb(ctx->K);
-  HIP_TRY(ctx, hipMemcpyAsync(hb.data(), d_B_use, ctx->K * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  for (int32_t b : hb)
-    if (b < 0 || b > ctx->B) return fail(ctx, MIOC_ESTATE, "every B_use[k] must satisfy 0 <= B_use[k] <= B");
+  // the per-subproblem budgets must lie in [0, B]: checked by the start kernels on the device (start_budget), which
+  // report an out-of-range B_use[k] as status[k] = MIOC_ESTATE -- no host read-back, so the device TRM loop
+  // (trm_batch.py) enqueues its trials without a synchronisation
   ctx->Bvec = d_B_use;
   rc = run_backtrack(ctx, ctx->B, d_u_out, d_phi_star, d_status);
   ctx->Bvec = nullptr;

@@ -322,7 +322,8 @@ __global__ __launch_bounds__(1024) void k_generic_argmin0(ProblemDev P, LevelsDe
                                                           size_t front_stride, int Bu, Start *start) {
   if (gate_closed(P.gate)) return;
   const int k = blockIdx.x;
-  if (P.Bvec) Bu = P.Bvec[k];
+  Bu = start_budget(P, k, Bu, start);
+  if (Bu < 0) return;  // uniform: an out-of-range B'_k (status MIOC_ESTATE)
   const double *f = front0 + (size_t)k * front_stride;
   ArgKey best;
   best.v = ~0ull;
@@ -526,7 +527,8 @@ __global__ __launch_bounds__(1024) void k_stage_argmin0(ProblemDev P, LevelsDev 
                                                         const double *S0_all, size_t s_stride, int Bu, Start *start) {
   if (gate_closed(P.gate)) return;
   const int k = blockIdx.x, L = Lv.L;
-  if (P.Bvec) Bu = P.Bvec[k];
+  Bu = start_budget(P, k, Bu, start);
+  if (Bu < 0) return;  // uniform: an out-of-range B'_k (status MIOC_ESTATE)
   const double *S0 = S0_all + (size_t)k * s_stride;
   const uint32_t *perm = perm_all + (size_t)k * P.nt * L;  // sphere order of u_old(0): rank | b̃ << 16
   ArgKey best;

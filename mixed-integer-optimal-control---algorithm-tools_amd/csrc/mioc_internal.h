@@ -67,6 +67,26 @@ struct Start {                      // backtrack start cell per subproblem
   int32_t pad;
 };
 
+// The backtrack budget of subproblem k: the per-subproblem B'_k when the call passed a device vector
+// (mioc_backtrack_batch_budgets_device), else the call's B'.  A B'_k outside [0, B] is checked here, on the device,
+// so that the call needs no host read-back of the budgets: the start kernel records MIOC_ESTATE as the
+// subproblem's status (its u row becomes NaN in k_expand, the walk skips it) and returns -1.
+__device__ __forceinline__ int start_budget(const ProblemDev &P, int k, int Bu, Start *start) {
+  if (!P.Bvec) return Bu;
+  const int b = P.Bvec[k];
+  if (b >= 0 && b <= P.B) return b;
+  if (threadIdx.x == 0) {
+    Start st;
+    st.phi = __builtin_nan("");
+    st.c = 0;
+    st.r = -1;
+    st.status = MIOC_ESTATE;
+    st.pad = 0;
+    start[k] = st;
+  }
+  return -1;
+}
+
 // ---- kernel launchers (mioc_generic.hip) ------------------------------------------------------
 hipError_t launch_validate(hipStream_t s, const ProblemDev &P, const double *numin, const double *numax,
                            int32_t *flags);

@@ -386,7 +386,8 @@ __global__ __launch_bounds__(1024) void k_pinf_start(ProblemDev P, LevelsDev Lv,
   extern __shared__ __attribute__((aligned(16))) double sR1[];
   __shared__ PKey red[16];
   const int k = blockIdx.x, M = P.M, nt = P.nt;
-  if (P.Bvec) Bu = P.Bvec[k];  // <= the launch's Bu, which sized sR1
+  Bu = start_budget(P, k, Bu, start);  // <= the launch's Bu, which sized sR1
+  if (Bu < 0) return;                  // uniform: an out-of-range B'_k (status MIOC_ESTATE)
   const double *R1 = D.R + ((size_t)k * nt + 1) * P.RP;
   if (nt >= 2)
     for (int c = threadIdx.x; c <= Bu; c += blockDim.x) sR1[c] = R1[c];

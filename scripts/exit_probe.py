@@ -1,6 +1,8 @@
 """Control for the rocprofv3 exit SIGSEGV: a minimal GPU program (torch tensor on the device, optionally a libmioc
 context created, used and destroyed) that writes /proc/self/maps at interpreter exit to $MIOC_EXIT_MAPS.
-Usage: python scripts/exit_probe.py [torch|mioc]"""
+Usage: python scripts/exit_probe.py [torch|mioc|mioc_nocoop]
+(mioc: C5 at K = 1 runs k_fsep2 in row segments, a cooperative launch; mioc_nocoop: the same DP as one ordinary
+launch)"""
 import atexit
 import os
 import sys
@@ -21,7 +23,8 @@ import torch  # noqa: E402
 
 x = torch.ones(1024, device="cuda")
 print("torch sum", float(x.sum()))
-if len(sys.argv) > 1 and sys.argv[1] == "mioc":
+mode = sys.argv[1] if len(sys.argv) > 1 else "torch"
+if mode.startswith("mioc"):
     from mioc import native  # noqa: E402
     from mioc.synth import CONFIGS, make_inputs  # noqa: E402
     cfg = CONFIGS["C5"]
@@ -29,6 +32,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "mioc":
     with native.Context(0) as ctx:
         ctx.set_levels(lt)
         ctx.set_cost(cfg.p, cfg.beta)
+        if mode == "mioc_nocoop":  # one workgroup per subproblem: an ordinary launch, no cooperative one
+            ctx.set_option(native.MIOC_OPT_FSEP_SEGMENTS, 1)
         ctx.bellman(df, uo, cfg.B, cfg.dt)
         ctx.synchronize()
         print("mioc algo", ctx.last_algo())

@@ -134,3 +134,28 @@ def test_c4_chunked_rows_vs_oracle(oracle_c):
         u, ps, _ = ctx.backtrack(Bp)
         assert np.array_equal(u, ou) and ps == ops, f"B=300 B'={Bp}"
     ctx.close()
+
+
+def test_c4_nt64_fixture_wait_timeout_redoes_dp():
+    """The headline kernel's timeout path: with a spin limit of one poll, the persistent k_sdt_run gives up at its
+    first dependency wait that is not already satisfied, every workgroup leaves, and the host redoes the DP with
+    per-step launches (check_run, counted in diagnostics [6]) before anything reads the tables -- so every step's U
+    hash, u and Φ* still equal the oracle fixture."""
+    z = np.load(os.path.join(HERE, "golden", "hashed", "c4_4096lv_p1_nt64_uhash.npz"), allow_pickle=False)
+    lt = CONFIGS["C4"].levels()
+    algo = native.MIOC_ALGO_SEPARABLE
+    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=1)
+    ctx.set_option(native.MIOC_OPT_SPIN_LIMIT, 1)
+    df, uo = z["df"], z["u_old"]
+    ctx.bellman(df, uo, int(z["B"][0]), float(z["dt"][0]))
+    assert ctx.last_algo() == algo
+    nt = df.shape[1]
+    bad = [i for i in range(nt - 1) if not np.array_equal(_hash(ctx.argmin_table(i)), z["u_hash"][i])]
+    assert not bad, f"U differs from the oracle at steps {bad[:10]}"
+    for q, Bp in enumerate(z["budgets"]):
+        u, ps, _ = ctx.backtrack(int(Bp))
+        assert np.array_equal(u, z["u"][q]), f"B'={Bp}"
+        assert ps == z["phi_star"][q], f"B'={Bp}: {ps!r} vs {z['phi_star'][q]!r}"
+    diag = ctx.diagnostics()
+    assert diag[6] >= 1, diag  # the persistent launch was abandoned and redone
+    ctx.close()

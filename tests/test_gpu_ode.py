@@ -255,3 +255,37 @@ def test_trm_batch_equals_sequential_trm(name, p, nt):
         assert np.array_equal(obj.x, ub[k].T), k
     print(f"{name}: iterations per restart {iters.tolist()}, halvings {halvings}")
     ctx.close()
+
+
+@pytest.mark.parametrize("chunk", [1, 2, 3])
+def test_trm_batch_production_path_equals_logged_and_sequential(chunk):
+    """The production path of TRM_batch (log=None: no decision array, several trials enqueued between two read-backs
+    of the control flags, gated kernels skipped by restarts that left their inner loop) against the logged path
+    (one synchronisation per trial) and against the host TRM loop run restart by restart: identical values,
+    controls and iteration counts.  kmax = 3 with chunks of 1, 2 and 3 trials: an inner loop ends at every position
+    of a chunk (mid-chunk for chunk 2, at a chunk end for 1 and 3)."""
+    import torch
+    from mioc.trm_batch import TRM_batch
+    K, nt, name = 12, 240, "doubletank"
+    par = mioc.TRM_parameters(beta=1e-3, Delta0=1.0, p=math.inf, maxiter=6, kmax=3)
+    ctx = native.Context(0)
+    ctx.set_levels(LevelTable([[0, 1]] * 3, mioc.bounded_sum_iterator([[0, 1]] * 3, 1, 1)))
+    x0 = torch.empty(K, nt, 3, dtype=torch.float64, device="cuda")
+    ctx.rand_start_tensor(x0, seed=1234)
+    ctx.synchronize()
+    log = []
+    vl, ul, il = TRM_batch(name, par, x0=x0, log=log)
+    stats = {}
+    vals, u, iters = TRM_batch(name, par, x0=x0, inner_chunk=chunk, stats=stats)
+    assert np.array_equal(vals, vl) and np.array_equal(iters, il)
+    assert torch.equal(u, ul)
+    halvings = sum(int(np.sum(d == 1)) for *_, d, _inner in log)
+    assert halvings >= 1, "no restart halved its radius: the chunked inner loop was not exercised"
+    assert stats["polls"] <= stats["outer"] * -(-par.kmax // chunk)
+    ub = u.cpu().numpy()
+    for k in range(K):
+        obj = _DeviceODE(name, nt, ctx)
+        J = mioc.TRM(obj, par, x0=x0[k].cpu().numpy().T.copy())
+        assert J == vals[k], (k, J, vals[k])
+        assert np.array_equal(obj.x, ub[k].T), k
+    ctx.close()

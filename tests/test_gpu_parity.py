@@ -176,6 +176,67 @@ def test_full_size_c5_restart_vs_oracle(oracle_c):
         assert np.array_equal(u, ou) and ps == ops, f"algo={algo}"
 
 
+def test_full_size_c5_p2_restart_vs_oracle(oracle_c):
+    """The reference's heat configuration uses p = 2 (multi-trust.jl:193-195, weights (Σ|Δ|²)^(1/2),
+    HelpFunctions.jl:63-67): one C5-shape restart at the full nt = 4096, B = 256 with the integer-key LUT
+    (MIOC_P_INTLUT; host weights from Python's pow, so parity with Julia's own ^ is unpinned -- DESIGN §4) against
+    the oracle: u, Φ* and U on 64 sampled steps, generic sweep and fused DP."""
+    cfg = CONFIGS["C5"]
+    lt, df, uo = make_inputs(cfg, k=5)
+    lv = _oracle_levels(lt)
+    k, pint, tab = native.cost_spec(2, levels=lt)
+    phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_INTLUT, cfg.beta, cfg.dt, p_int=2, wtab=tab)
+    steps = sorted(set(np.linspace(0, cfg.nt - 2, 64).astype(int).tolist()))
+    for algo in (native.MIOC_ALGO_FUSED, native.MIOC_ALGO_GENERIC):
+        ctx = _ctx(lt, k, cfg.beta, algo, p_int=pint, table=tab)
+        ctx.bellman(df, uo, cfg.B, cfg.dt)
+        assert ctx.last_algo() == algo
+        for Bp in (cfg.B, cfg.B // 3):
+            ou, ops = oracle_c.backtrack(lv, uo, phi, U, cfg.B, Bp)
+            u, ps, _ = ctx.backtrack(Bp)
+            assert np.array_equal(u, ou) and ps == ops, f"algo={algo} B'={Bp}"
+        for i in steps:
+            d, o = ctx.argmin_table(i), U[:, :, i]
+            m = o >= 0
+            assert np.array_equal(d[m], o[m]), f"algo={algo} step {i}"
+        ctx.close()
+
+
+def test_backtrack_budgets_device_vs_single():
+    """eval_u_TRM! with one budget per subproblem (mioc_backtrack_batch_budgets_device, the halving path of
+    multi-trust.jl:108-110 per restart) equals a separate backtrack at each budget; a budget outside [0, B] is
+    caught on the device (no host read-back): that subproblem's status is MIOC_ESTATE and its u row NaN."""
+    import torch
+    cfg = CONFIGS["C5"]
+    K, nt = 6, 200
+    subs = [make_inputs(cfg, k=k, nt=nt)[1:] for k in range(K)]
+    lt = cfg.levels()
+    ddf = torch.tensor(np.ascontiguousarray(np.stack([d.T for d, _ in subs])), dtype=torch.float64, device="cuda")
+    duo = torch.tensor(np.ascontiguousarray(np.stack([u.T for _, u in subs])), dtype=torch.float64, device="cuda")
+    budgets = [cfg.B, 0, 77, -1, cfg.B + 1, 5]
+    for algo in (native.MIOC_ALGO_FUSED_SEPARABLE, native.MIOC_ALGO_FUSED, native.MIOC_ALGO_GENERIC):
+        ctx = _ctx(lt, P_ONE, cfg.beta, algo)
+        torch.cuda.synchronize()
+        ctx.bellman_batch_tensors(ddf, duo, cfg.B, cfg.dt)
+        du = torch.empty_like(ddf)
+        dphi = torch.empty(K, dtype=torch.float64, device="cuda")
+        dst = torch.empty(K, dtype=torch.int32, device="cuda")
+        bv = torch.tensor(budgets, dtype=torch.int32, device="cuda")
+        ctx.backtrack_batch_budgets_tensors(bv, du, dphi, dst)
+        ctx.synchronize()
+        ub, st = du.cpu().numpy(), dst.cpu().numpy()
+        for k, Bp in enumerate(budgets):
+            if not 0 <= Bp <= cfg.B:
+                assert st[k] == native.MIOC_ESTATE and np.all(np.isnan(ub[k])), (algo, k, Bp)
+                continue
+            single = _ctx(lt, P_ONE, cfg.beta, algo)
+            single.bellman(*subs[k], cfg.B, cfg.dt)
+            u, ps, _ = single.backtrack(Bp)
+            assert st[k] == 0 and np.array_equal(ub[k].T, u) and dphi[k].item() == ps, (algo, k, Bp)
+            single.close()
+        ctx.close()
+
+
 def _path_objective(lt, df, u, dt, beta, p_kind):
     """Φ* recomputed along a control in the reference's rounding order (HelpFunctions.jl:52-71)."""
     M, n = u.shape

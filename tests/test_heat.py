@@ -262,3 +262,41 @@ def test_trm_batch_heat_equals_sequential_trm():
         obj.ctx.close()
     print(f"heat: iterations per restart {iters.tolist()}, values {vals.tolist()}")
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_trm_batch_heat_reference_config_p2():
+    """The reference's own heat run, main("heat") (multi-trust.jl:193-195, example_heat.jl:39,42-44): p = 2,
+    β = 1e-3, Δ⁰ = 2, nt = 500 (τ = 0.02, B = 100), 6 x 6 product levels.  TRM_batch (device control, fused DP with
+    the p = 2 weight LUT, production path log=None) against the host TRM loop run restart by restart on HeatObj:
+    identical values and controls.  The LUT's square roots come from Python's pow here (Julia's ^ supplies them
+    through integration/MIOC.jl), so parity with the reference's own floats is unpinned for p = 2."""
+    import math
+
+    import torch
+
+    import mioc
+    from mioc import native
+    from mioc.heat import HeatObj
+    from mioc.iterators import LevelTable
+    from mioc.trm_batch import TRM_batch
+    hp = HeatProblem(n=17, nt=500)
+    K = 4
+    par = mioc.TRM_parameters(beta=1e-3, Delta0=2.0, p=2, maxiter=3, kmax=4)
+    assert math.floor(par.Delta0 / hp.tau) == 100
+    ctx = native.Context(0)
+    ctx.set_levels(LevelTable(hp.levels))
+    x0 = torch.empty(K, hp.nt, 2, dtype=torch.float64, device="cuda")
+    ctx.rand_start_tensor(x0, seed=11)
+    ctx.synchronize()
+    vals, u, iters = TRM_batch(hp, par, x0=x0)
+    ub = u.cpu().numpy()
+    for k in range(K):
+        obj = HeatObj(hp)
+        J = mioc.TRM(obj, par, x0=x0[k].cpu().numpy().T.copy())
+        assert J == vals[k], (k, J, vals[k])
+        assert np.array_equal(obj.x, ub[k].T), k
+        assert math.isfinite(J)
+        obj.ctx.close()
+    print(f"heat p=2: iterations per restart {iters.tolist()}, values {vals.tolist()}")
+    ctx.close()
