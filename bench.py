@@ -63,6 +63,15 @@ def parse(argv=None):
     ap.add_argument("--batch-total", type=int, default=1024,
                     help="strong-scaling batch line (batch_strong): this many subproblems per step in total, split "
                          "over the ranks (0 to skip)")
+    ap.add_argument("--shard8", type=int, default=1,
+                    help="one GPU: also time the 1/8 shard of --batch-total (the per-rank work of the strong-scaling "
+                         "batch at 8 GPUs), as the projection batch_shard8 (0 to skip)")
+    ap.add_argument("--p2-batch-config", default="C5",
+                    help="the batch line at p=2 (the reference's heat configuration, multi-trust.jl:193-195; "
+                         "'none' to skip)")
+    ap.add_argument("--pmc-valu", default=None,
+                    help="a rocprofv3 --pmc CSV (SQ_INSTS_VALU, SQ_WAVES, ...) of THIS build over the same bench "
+                         "command: adds counter-backed VALU figures to each line's roofline_valu")
     ap.add_argument("--pinf-batch-config", default="C2",
                     help="the p=Inf batch line's config (the reference's main() runs C1-C3 at p=Inf; 'none' to skip)")
     ap.add_argument("--heat-restarts", type=int, default=4096,
@@ -378,35 +387,55 @@ def roofline_of(res):
             "frac": round(ops / avg_s / 1e12 / FP64_VALU_PEAK_TOPS, 6)}
     if note:
         valu["note"] = note
-    if name == "k_sdt_run":
-        per_item, src = pmc_valu_per_wave_item(name)
-        if per_item:
-            # two waves per SIMD (512 threads, one workgroup per CU), 4 cycles per wave64 VALU instruction, 2.4 GHz
-            valu["pmc_valu_instructions_per_wave_item"] = round(per_item, 1)
-            valu["pmc_valu_issue_frac"] = round(2 * per_item * 4 / (avg_s / steps * 2.4e9), 3)
-            valu["pmc_source"] = src
+    pmc = pmc_valu_of(name, avg_s, steps)
+    if pmc:
+        valu.update(pmc)
     return roof, valu
 
 
-def pmc_valu_per_wave_item(kernel):
-    """SQ_INSTS_VALU / SQ_WAVES / items per wave of `kernel` from the newest committed PMC pass
-    (profiles/roundN_*_pmc_valu_*_ntT.csv, scripts/gpu_pmc_valu.sh: one DP row item per wave and step), or None."""
+PMC_VALU_FILE = None  # --pmc-valu: a rocprofv3 --pmc CSV of this build over the same bench command
+
+
+def pmc_valu_of(kernel, avg_s, steps):
+    """Counter-backed VALU figures of `kernel` from the --pmc-valu CSV (a separate rocprofv3 --pmc pass of THIS build
+    over the same bench command; no committed file of an older build is ever used): the dispatches of `kernel` whose
+    duration is within 20 % of this line's HIP-event launch time, averaged.  VALU instructions per wave and DP step
+    (SQ_INSTS_VALU / SQ_WAVES / steps) and the SIMDs' VALU-busy fraction (rocprof's gfx950 VALUBusy:
+    ΣSQ_ACTIVE_INST_VALU / (CUs x GRBM_GUI_ACTIVE))."""
     import csv
-    import glob
-    import re
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*_pmc_valu_*_nt*.csv")))
-    if not files:
-        return None, None
-    f = files[-1]
-    nt = int(re.search(r"_nt(\d+)", f).group(1))
-    v = {}
-    with open(f) as fh:
+    path, how = PMC_VALU_FILE, "--pmc-valu (this build)"
+    if not path:
+        # else the newest committed pass (profiles/roundN_pmc_valu_bench.csv, by round number), labelled as such: its
+        # dispatches count only where their duration matches this run's within 20 %
+        import glob
+        import re
+        files = glob.glob(os.path.join(ROOT, "profiles", "round*_pmc_valu_bench.csv"))
+        if not files:
+            return None
+        path = max(files, key=lambda f: int(re.search(r"round(\d+)_", os.path.basename(f)).group(1)))
+        how = "committed pass of this round's final build (duration-matched)"
+    per = {}
+    with open(path) as fh:
         for r in csv.DictReader(fh):
-            if kernel in r["Kernel_Name"]:
-                v[r["Counter_Name"]] = float(r["Counter_Value"])
-    if not v.get("SQ_INSTS_VALU") or not v.get("SQ_WAVES"):
-        return None, None
-    return v["SQ_INSTS_VALU"] / v["SQ_WAVES"] / (nt - 1), os.path.relpath(f, ROOT)
+            if kernel not in r["Kernel_Name"]:
+                continue
+            dur = (float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) * 1e-9
+            if abs(dur - avg_s) > 0.2 * avg_s:
+                continue
+            d = per.setdefault(r["Dispatch_Id"], {})
+            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    if not per:
+        return None
+    avg = {}
+    for d in per.values():
+        for k, v in d.items():
+            avg[k] = avg.get(k, 0.0) + v / len(per)
+    out = {"pmc_source": os.path.relpath(path, ROOT), "pmc_pass": how, "pmc_dispatches": len(per)}
+    if avg.get("SQ_INSTS_VALU") and avg.get("SQ_WAVES"):
+        out["pmc_valu_instructions_per_wave_step"] = round(avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"] / steps, 1)
+    if avg.get("SQ_ACTIVE_INST_VALU") and avg.get("GRBM_GUI_ACTIVE"):
+        out["pmc_valu_busy_frac"] = round(avg["SQ_ACTIVE_INST_VALU"] / (256 * avg["GRBM_GUI_ACTIVE"]), 4)
+    return out
 
 
 def _cpu_info():
@@ -440,6 +469,10 @@ def cpu_baseline(cfg_name, p_over, cpu_steps):
     kind = P_INF if p == math.inf else P_ONE
     model, aff, threads = _cpu_info()
     oc = OracleC()
+    lut = None
+    if p not in (1.0, math.inf):  # integer p: the reference loop with the host weight LUT (oracle_bellman)
+        from mioc.native import cost_spec
+        kind, p_int, lut = cost_spec(p, levels=cfg.levels())
     host = f"host: {model}, {aff} CPUs in the affinity mask, {threads} threads used (this job's CPU share)"
     if cfg.levels().L <= 64:
         # batch config: independent subproblems, one per thread (the reference is single-threaded per subproblem);
@@ -450,6 +483,8 @@ def cpu_baseline(cfg_name, p_over, cpu_steps):
 
         def one(j):
             df, uo = j
+            if lut is not None:
+                return oc.bellman(lv, df, uo, cfg.B, kind, cfg.beta, cfg.dt, p_int=p_int, wtab=lut)[0][0, 0, 0]
             return oc.bellman_steps(lv, df, uo, cfg.B, kind, cfg.beta, cfg.dt, cfg.nt - 1)
 
         t0 = time.perf_counter()
@@ -617,8 +652,10 @@ def _exit_maps():
 
 
 def main():
+    global PMC_VALU_FILE
     _exit_maps()
     args = parse()
+    PMC_VALU_FILE = args.pmc_valu
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args))
     import torch
@@ -650,8 +687,8 @@ def main():
         if args.solver == "native" and len(r2.get("diag", [])) > 9:  # mioc_diagnostics[9]
             variant["walk"] = "serial" if r2["diag"][9] < 0 else "segmented"
             variant["walk_serial_fallbacks"] = max(0, int(r2["diag"][9]))
-    def batch_line(cfg_name, total=None):
-        r3 = run(args, cfg_name, args.batch_size, None, None, rank, world, device, dist, torch,
+    def batch_line(cfg_name, total=None, p_over=None):
+        r3 = run(args, cfg_name, args.batch_size, p_over, None, rank, world, device, dist, torch,
                  max(args.steps, 3), args.warmup, total=total)
         line = {"config": {"workload": workload(r3), "parallelism": f"dp{world} (independent restarts)",
                            "global_batch": r3["G"], "per_rank": r3["K"]},
@@ -667,7 +704,7 @@ def main():
                 line["exact_scan_targets"] = {"near_tie": r3["diag"][0], "out_of_binade_or_few": r3["diag"][1]}
             line["roofline"], line["roofline_valu"] = roofline_of(r3)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(cfg_name, None, args.cpu_steps)
+            line["cpu_baseline"] = cpu_baseline(cfg_name, p_over, args.cpu_steps)
         return line
 
     batch_pinf = heat = None
@@ -682,6 +719,24 @@ def main():
         else:  # fixed total work split over the ranks (C5 x 1024 on 8 GPUs: 128 restarts per GPU)
             strong = batch_line(args.batch_config, total=args.batch_total)
             strong.pop("cpu_baseline", None)
+    shard8 = None
+    if (args.shard8 and world == 1 and args.batch_total >= 8 and args.batch_config not in ("", "none") and
+            args.nt is None):
+        # the per-rank share of the strong-scaling batch on an 8-GPU node, timed on this one GPU: a projection of the
+        # 8-GPU speed-up (the ranks share nothing but the start broadcast and the final gather)
+        shard8 = batch_line(args.batch_config, total=args.batch_total // 8)
+        shard8.pop("cpu_baseline", None)
+        shard8["projection"] = (f"one GPU running the 1/8 shard ({args.batch_total // 8} restarts) of the "
+                                f"{args.batch_total}-restart strong-scaling batch; the 8-GPU speed-up it projects is "
+                                f"the full batch's ms_per_step over this line's")
+        full = strong if strong is not None else batch
+        if full is not None and full["config"]["global_batch"] == args.batch_total:
+            shard8["projected_8gpu_speedup"] = round(full["ms_per_step"] / shard8["ms_per_step"], 3)
+    batch_p2 = None
+    if args.p2_batch_config not in ("", "none") and args.nt is None:
+        batch_p2 = batch_line(args.p2_batch_config, p_over="2")
+        batch_p2["note"] = ("p = 2 weights (Σ|Δ|²)^(1/2) from a host LUT (Python pow; Julia's own ^ through "
+                            "integration/MIOC.jl): the reference's heat configuration (multi-trust.jl:193-195)")
     if args.pinf_batch_config not in ("", "none") and args.nt is None:
         batch_pinf = batch_line(args.pinf_batch_config)
     if rank == 0:
@@ -718,6 +773,10 @@ def main():
             out["batch"] = batch
         if strong:
             out["batch_strong"] = strong
+        if shard8:
+            out["batch_shard8"] = shard8
+        if batch_p2:
+            out["batch_p2"] = batch_p2
         if batch_pinf:
             out["batch_p_inf"] = batch_pinf
         if heat:

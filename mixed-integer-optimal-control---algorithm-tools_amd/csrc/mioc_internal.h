@@ -105,7 +105,8 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
                          const int32_t *ranks, double *u_out, double *phi_star, int32_t *status);
 
 // ---- L1-ball pyramid (mioc_pyramid.hip) + staging-layout backtrack (mioc_generic.hip) -------------
-hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm);
+// slab_shift: 0 = sphere order (pyramid); sdt_slab_shift(G) for the separable transform (slab-major, see k_pyr_order)
+hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int slab_shift);
 hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm, double *S,
                                size_t s_stride);
 hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
@@ -114,6 +115,7 @@ hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
 size_t pyr_lds_bytes(const PyrGeom &G);
 // separable L1 transform (mioc_sdt.hip): same staging layout, 8^M grids (M = 3, 4), beta > 0
 bool sdt_supported(const PyrGeom &G);
+int sdt_slab_shift(const PyrGeom &G);  // the sphere-order mode the separable transform's kernels were built for
 size_t sdt_lds_bytes(const PyrGeom &G);
 constexpr int kSdtMaxBuffers = 64;  // persistent separable transform: staging buffers S_i, step i in buffer i % NB
 hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,

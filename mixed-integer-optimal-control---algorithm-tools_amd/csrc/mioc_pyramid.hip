@@ -820,9 +820,13 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
 // row c' - s of S_i (the sphere s) form one contiguous run per sphere.  Inside a sphere the ranks ascend (a
 // stable counting sort), so the order is a function of u_old(i) alone: steps with equal u_old share one table,
 // which the persistent separable-transform driver uses to skip reloading it.
-__global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all) {
-  __shared__ int start[64];     // the next free position of each sphere (distances >= 63 share the last)
-  __shared__ int wcnt[4][65];   // ranks of the current chunk per wave and sphere (65: the inactive lanes)
+// slab_shift > 0 (separable transform): slab-major -- the ranks are grouped first by their top grid coordinate
+// j >> slab_shift (the slab a row workgroup's wave owns), then by sphere, then ascending; every slab is one contiguous
+// block of L/8 positions, so the wave that owns a slab loads exactly its slab's sources (mioc_sdt.hip).
+__global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all, int slab_shift) {
+  constexpr int NK = 8 * 64;        // bucket keys: slab << 6 | min(distance, 63)
+  __shared__ int start[NK];         // the next free position of each bucket
+  __shared__ int wcnt[4][NK + 1];   // ranks of the current chunk per wave and bucket (NK: the inactive lanes)
   const int i = blockIdx.x, k = blockIdx.y, L = G.ncol * G.n[0], M = G.M;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const double *uo = P.uold + ((size_t)k * P.nt + i) * M;
@@ -830,8 +834,8 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
   int u[kMaxM];
 #pragma unroll
   for (int m = 0; m < kMaxM; ++m) u[m] = m < M ? (int)uo[m] : 0;
-  if (tid < 64) start[tid] = 0;
-  for (int e = tid; e < 4 * 65; e += blockDim.x) (&wcnt[0][0])[e] = 0;
+  for (int e = tid; e < NK; e += blockDim.x) start[e] = 0;
+  for (int e = tid; e < 4 * (NK + 1); e += blockDim.x) (&wcnt[0][0])[e] = 0;
   __syncthreads();
   auto dist = [&](int j) {
     int d = 0;
@@ -842,26 +846,27 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
     }
     return min(d, 0xFFFF);
   };
-  for (int j = tid; j < L; j += blockDim.x) atomicAdd(&start[min(dist(j), 63)], 1);
+  auto key = [&](int j, int d) { return (slab_shift ? (j >> slab_shift) << 6 : 0) | min(d, 63); };
+  for (int j = tid; j < L; j += blockDim.x) atomicAdd(&start[key(j, dist(j))], 1);
   __syncthreads();
   if (tid == 0) {
     int run = 0;
-    for (int b = 0; b < 64; ++b) {
+    for (int b = 0; b < NK; ++b) {
       const int c = start[b];
       start[b] = run;
       run += c;
     }
   }
   __syncthreads();
-  // chunks of 256 consecutive ranks in order; inside a chunk, a rank's place among its sphere's ranks is the number of
-  // lower lanes of its wave with the same sphere (7 ballots) plus those of the lower waves
+  // chunks of 256 consecutive ranks in order; inside a chunk, a rank's place among its bucket's ranks is the number of
+  // lower lanes of its wave with the same key (10 ballots) plus those of the lower waves
   for (int c = 0; c < L; c += 256) {
     const int j = c + tid;
     const bool act = j < L;
-    const int d = act ? dist(j) : 0, b = act ? min(d, 63) : 64;
+    const int d = act ? dist(j) : 0, b = act ? key(j, d) : NK;
     unsigned long long same = ~0ull;
 #pragma unroll
-    for (int q = 0; q < 7; ++q) {
+    for (int q = 0; q < 10; ++q) {
       const unsigned long long m = __ballot((b >> q) & 1);
       same &= ((b >> q) & 1) ? m : ~m;
     }
@@ -874,17 +879,17 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
       perm[pos] = (uint32_t)j | ((uint32_t)d << 16);
     }
     __syncthreads();
-    if (tid < 64) {
-      start[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
-      wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+    for (int e = tid; e < NK; e += blockDim.x) {
+      start[e] += wcnt[0][e] + wcnt[1][e] + wcnt[2][e] + wcnt[3][e];
+      wcnt[0][e] = wcnt[1][e] = wcnt[2][e] = wcnt[3][e] = 0;
     }
-    if (tid == 64) wcnt[0][64] = wcnt[1][64] = wcnt[2][64] = wcnt[3][64] = 0;
+    if (tid == 0) wcnt[0][NK] = wcnt[1][NK] = wcnt[2][NK] = wcnt[3][NK] = 0;
     __syncthreads();
   }
 }
 
-hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm) {
-  hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm);
+hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int slab_shift) {
+  hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm, slab_shift);
   return hipGetLastError();
 }
 

@@ -63,6 +63,13 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_PREFETCH
 #define SDT_PREFETCH 1                   // load the sphere orders ahead of the dependency wait
 #endif
+#ifndef SDT_PRED
+#define SDT_PRED 0                       // persistent driver: stamp with a per-row predicted scale (see sdt_body)
+#endif
+#ifndef SDT_SLAB
+#define SDT_SLAB 0                       // slab-major sphere order: a wave loads and stamps only its own slab (sdt_body)
+#endif
+constexpr int SD_PRED_ROWS = 64;         // rows of a workgroup's chunk that keep a predicted scale (the others: none)
 
 // Diagnostic build only (make stamps -> libmioc_stamps.so): per-workgroup phase clocks of the last launch.
 #if defined(MIOC_STAMPS) && !defined(MIOC_STAMPS_TL)
@@ -204,6 +211,29 @@ __device__ __forceinline__ void sd_wave_stats(double &mn, double &mx) {
 // LDS position of rank r (3 bits per dimension): XOR swizzle so that each 32-lane half of a pass reads
 // 32 distinct 8-byte bank slots in every pass: slot = (x0 ^ x1) + 8·((x1 ^ x2) & 3)
 __device__ __forceinline__ int sd_swz(int r) { return r ^ ((r >> 3) & 7) ^ (((r >> 6) & 3) << 3); }
+
+// The first position of thread tid's q-th position pair (q < 4) in a staging row / sphere order.  SDT_SLAB: the
+// sphere orders are slab-major (k_pyr_order, slab = the top grid coordinate of the rank), so wave w's pairs cover
+// exactly slab w's block of L/8 positions, 128 consecutive positions per q (16 bytes per lane: coalesced); else
+// 2(tid + T·q) (the same for M = 3, one wave).
+template <int M>
+__device__ __forceinline__ int sd_p2(int tid, int q) {
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
+  if constexpr (SDT_SLAB)
+    return (tid >> 6) * (L / NW) + 2 * ((tid & 63) + 64 * q);
+  else
+    return 2 * (tid + T * q);
+}
+// The position of the level at distance 0 from u_old (when u_old is on the grid): the head of the first sphere --
+// position 0 of the sphere order, or (SDT_SLAB) the first position of u_old's slab.  Callers check b̃ == 0 there.
+template <int M>
+__device__ __forceinline__ int sd_headpos(const PyrGeom &G, double uo_top) {
+  constexpr int L = 1 << (3 * M);
+  if constexpr (SDT_SLAB)
+    return min(max((int)uo_top - G.base[M - 1], 0), 7) * (L / 8);
+  else
+    return 0;
+}
 
 // rank of element x of line q in the pass over dimension m (q enumerates the other coordinates, lowest
 // dimension fastest)
@@ -373,7 +403,11 @@ struct SdtShared {
   int nsp;   // sparse rows: the finite sources (rank, Ψ)
   int spj[SD_SPARSE];
   double spv[SD_SPARSE];
-  int cnt[2];  // targets sent to the exact scan (near ties, direct rows), flushed to the global counters once
+  int cnt[3];  // targets sent to the exact scan (near ties, direct rows), rows stamped twice (predicted scale
+              // missed); flushed to the global counters [0], [1], [4] once
+  int rfail[NW];  // per wave: a finite Ψ outside the row's predicted range (SDT_PRED)
+  int arrive;     // SDT_SLAB: waves of the current row past their drain (the last one publishes the row flags)
+  double pred[SD_PRED_ROWS][2];  // per chunk row: the predicted range [lo, hi] of its Ψ (lo = +Inf: none yet)
 };
 
 template <int M>
@@ -404,22 +438,26 @@ __device__ __forceinline__ void sd_wave_sync() { asm volatile("s_waitcnt lgkmcnt
 // latency never sits behind a barrier.
 struct SdPerm {
   uint2 in[4], out[4];
-  uint32_t hin, hout;
+  uint32_t hin, hout;  // the sphere-order entries at the head positions pin_h (step i+1) and pout_h (step i)
+  int pin_h, pout_h;
 };
 template <int M>
-__device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restrict__ perm_all, int nt, int k,
-                                             int i) {
+__device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restrict__ perm_all, const ProblemDev &P,
+                                             const PyrGeom &G, int k, int i) {
   constexpr int T = 1 << (3 * M - 3);
+  const int nt = P.nt;
   const uint32_t *pin = perm_all + ((size_t)k * nt + i + 1) * ((size_t)T * 8);
   const uint32_t *pout = perm_all + ((size_t)k * nt + i) * ((size_t)T * 8);
   const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    pm.in[q] = *reinterpret_cast<const uint2 *>(pin + 2 * (tid + T * q));
-    pm.out[q] = *reinterpret_cast<const uint2 *>(pout + 2 * (tid + T * q));
+    pm.in[q] = *reinterpret_cast<const uint2 *>(pin + sd_p2<M>(tid, q));
+    pm.out[q] = *reinterpret_cast<const uint2 *>(pout + sd_p2<M>(tid, q));
   }
-  pm.hin = pin[0];
-  pm.hout = pout[0];
+  pm.pin_h = sd_headpos<M>(G, P.uold[((size_t)k * nt + i + 1) * M + M - 1]);
+  pm.pout_h = sd_headpos<M>(G, P.uold[((size_t)k * nt + i) * M + M - 1]);
+  pm.hin = pin[pm.pin_h];
+  pm.hout = pout[pm.pout_h];
 }
 
 // One source row c' of step i for subproblem k (the row body shared by both drivers).
@@ -427,12 +465,14 @@ __device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restr
 //            S_{i+1}[c' - b̃_j(i+1)][pos_{i+1}(j)] (+Inf where that row is below 0); loaded by the caller (the
 //            persistent driver issues these loads one row ahead, so they may still be in flight on entry).
 //   pin    : LDS copy of the sphere order of step i+1 (rank | b̃ << 16 by position), pout: of step i.
-//   h      : the driver's pipeline hooks (no-ops for one launch per step): h.early() once every wave has consumed
-//            `v` (publish `loaded`, issue this wave's dependency polls without waiting); h.drain() right before the
-//            first barrier after the last use of `v` and `pin` (this wave's stores of the previous row have landed);
-//            h.go() after that barrier (publish the previous row, check the polls, issue the next row's loads, the
-//            next step's sphere order and df / u_old).  A timed-out wait sets sh.stop, which the driver reads after
-//            the row.
+//   h      : the driver's pipeline hooks (no-ops for one launch per step): h.poll() at the start (SDT_PRED: issue
+//            this wave's dependency polls without waiting); h.early() once every wave has consumed `v` (!SDT_PRED:
+//            publish `loaded`, issue the polls); h.drain() right before the first barrier after the last use of `v`
+//            and `pin` (this wave's stores of the previous row have landed); h.go() after that barrier (publish
+//            `loaded` (SDT_PRED) and the previous row, check the polls, issue the next row's loads, the next step's
+//            sphere order and df / u_old).  A timed-out wait sets sh.stop, which the driver reads after the row.
+//   prow   : (persistent driver, SDT_PRED) this row's predicted Ψ range [lo, hi] in LDS, refreshed here on a miss;
+//            null: none
 // Returns 1 if the row is all +Inf (no target in the trust region or no finite source), else 0.
 // Writes row c' of S_i (sphere order of u_old(i)) and of UU_i: exactly five 16-byte vector-memory stores per
 // thread on every path, the last vector-memory instructions of the row (the persistent driver's counted wait
@@ -444,7 +484,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
                                          const uint32_t *pout,
                                          double *Sout, uint16_t *UU, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
                                          unsigned char *sds, Hooks &h, const double *__restrict__ df_all,
-                                         const double *__restrict__ uo_all) {
+                                         const double *__restrict__ uo_all, double *prow) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
   double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
   double *dtv = psi + L;                                // [L] transform values (swizzled)
@@ -468,6 +508,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   uint2 ein[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) ein[q] = ein_in[q];
+  h.poll();  // (SDT_PRED) this wave's dependency polls, checked after the row's first barrier
   // ---- this thread's targets: ranks tid | x << 3(M-1) (the lines of the last pass) -----------------
   double a[M];
   int lb[M], uo[M];
@@ -475,7 +516,8 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   for (int m = 0; m < M; ++m) {
     a[m] = P.dt * dfi[m];
     lb[m] = G.base[m];
-    uo[m] = (int)uoi[m];
+    // u_old(:, i) is the same for every lane: as a scalar, the trust-region thresholds below are scalar arithmetic
+    uo[m] = __builtin_amdgcn_readfirstlane((int)uoi[m]);
   }
   double pre = 0.0;
   int bpre = 0;
@@ -497,70 +539,243 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   }
 
   if (tid == 0) sh.nlist = 0;
-  double pmn = INFINITY, pmx = -INFINITY;
+  // ---- the binade: values base + (Ψ - ref)/β + d lie in [base, 2·base), grid g = 2^18 ulp ----------------
+  // for Ψ in [lo, hi] (ref = lo): every quantity of the certified transform follows from the range alone
+  const double inv = Lv.inv_beta;  // fl(1/β), host-computed
+  double qa = beta * (double)Smax;  // |T1 + β·d + Ψ| <= qa + max(|lo|, |hi|) for every candidate
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int m = 0; m < M; ++m) qa += fabs(a[m]) * (double)max(abs(lb[m]), abs(lb[m] + 7));
+  double ref, base, g, tol;
+  bool scale_ok;
+  auto scale = [&](double lo, double hi) {
+    const double rs = (hi - lo) * inv + (double)Smax;              // scaled range of every transform value
+    scale_ok = rs < 0x1p31;                                        // else unit steps are not on the grid: exact scans
+    const int E = ilogb(fmin(rs, 0x1p31) * (1.0 + 0x1p-20) + 1.0) + 2;  // 2^E >= 2·rs (E <= SD_GRID: g <= 1)
+    base = ldexp(1.0, E);
+    g = ldexp(1.0, E - SD_GRID);
+    // 2 × stamping error (< g) + 2 × the reference's rounding (<= 4u·qmax per candidate), in units of β
+    tol = 3.0 * g + 0x1p-49 * (qa + fmax(fabs(lo), fabs(hi))) * inv;
+    ref = lo;
+  };
+  // V_j = trunc_g(base + (Ψ_j - ref)/β) | j
+  auto stamp = [&](double x, int j) {
+    const double y = (x - ref) * inv + base;
+    return __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | (j << SD_CB));
+  };
+  // ---- one pass of the transform: forward and backward sweep along the 8 levels of dimension m, unit step 1.0;
+  // this thread's line is read from and (but for the last pass) written back to the swizzled LDS values ---------
+  double o[8];
+  auto pass = [&](int m) {
+    int pos[8];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const double x = v[2 * q + h];
-      psi[(h ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
-      const bool fin = x < INFINITY;
-      nv += __popcll(__ballot(fin)) << 16;
-      pmn = sd_min(pmn, x);  // +Inf is neutral
-      pmx = sd_max(pmx, __hiloint2double(fin ? __double2hiint(x) : (int)0xFFF00000, __double2loint(x)));  // +Inf -> -Inf
+    for (int x = 0; x < 8; ++x) {
+      pos[x] = sd_swz(sd_rank((int)threadIdx.x, m, x));  // tid-only: hoisted out of the row loop
+      o[x] = dtv[pos[x]];
     }
-  sd_wave_stats(pmn, pmx);
-  if (lane == 0) {
-    sh.rmn[w] = pmn;
-    sh.rmx[w] = pmx;
-    sh.rnv[w] = nv;
+#if SDT_PASS_SPLIT
+    // two independent chains (prefix f over sources <= x, strict suffix b over sources > x: disjoint candidate
+    // sets), then one merge per point: half the dependency depth of the in-place sweeps, 20 merges instead of 14
+    {
+      double f[8], b[8];
+      f[0] = o[0];
+      b[7] = o[7];
+#pragma unroll
+      for (int x = 1; x < 8; ++x) {
+        f[x] = sd_merge(o[x], f[x - 1] + 1.0, tol);
+        if (x < 7) b[7 - x] = sd_merge(o[7 - x], b[8 - x] + 1.0, tol);
+      }
+#pragma unroll
+      for (int x = 0; x < 7; ++x) o[x] = sd_merge(f[x], b[x + 1] + 1.0, tol);
+      o[7] = f[7];
+    }
+#else
+    // in place: after the forward sweep o[x] covers the sources at <= x; a backward merge of o[x] with
+    // o[x+1] + 1 compares a source at <= x with itself shifted by >= 2, never within tol, so every
+    // flagged tie is between two distinct sources (as in a merge of disjoint sets)
+#pragma unroll
+    for (int x = 1; x < 8; ++x) o[x] = sd_merge(o[x], o[x - 1] + 1.0, tol);
+#pragma unroll
+    for (int x = 6; x >= 0; --x) o[x] = sd_merge(o[x], o[x + 1] + 1.0, tol);
+#endif
+    if (m + 1 < M) {
+#pragma unroll
+      for (int x = 0; x < 8; ++x) dtv[pos[x]] = o[x];
+    }
+  };
+  // SDT_SLAB: passes 0 .. M-2 run per wave: their lines keep the top grid coordinate (rank bits 3(M-1)..) = the wave
+  // index (the swizzle leaves those bits alone), so a wave reads only what it wrote itself
+  auto wave_passes = [&]() {
+#pragma unroll
+    for (int m = 0; m + 1 < M; ++m) {
+      sd_wave_sync();
+      pass(m);
+    }
+  };
+  int nf;
+  bool empty;
+  constexpr bool PRED = PERSIST && SDT_PRED;
+  constexpr bool SLAB = PRED && SDT_SLAB;
+  if constexpr (PRED) {
+    // Predicted scale (persistent driver): a row's Ψ move little from one step to the next, so the range [lo, hi]
+    // this row saw at an earlier step, widened by its own width, is stamped with at once -- no min/max reduction and
+    // no barrier before the stamps.  Every finite Ψ is checked to lie in [lo, hi]; then every bound of the
+    // certification holds as if (lo, hi) were the row's own min and max (the binade holds [lo, hi] + Smax, tol
+    // covers |Ψ| <= max(|lo|, |hi|)), only the grid is up to ~3x coarser.  A miss (or no prediction yet) redoes the
+    // stamps from the exact min and max below, exactly as the per-step driver does, and refreshes the prediction.
+    const double plo = prow ? prow[0] : INFINITY, phi = prow ? prow[1] : -INFINITY;
+    scale(plo, phi);
+    const bool miss = !(plo <= phi) || !scale_ok || !(tol < base * 0x1p-20);
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
+        const double x = v[2 * q + hh];
+        psi[j] = x;
+        const bool fin = x < INFINITY;
+        nv += __popcll(__ballot(fin)) << 16;
+        bad |= fin && !(x >= plo && x <= phi);
+        dtv[sd_swz(j)] = fin ? stamp(x, j) : INFINITY;
+      }
+    const bool wbad = __ballot(bad) != 0;
+    if (lane == 0) {
+      sh.rnv[w] = nv;
+      sh.rfail[w] = wbad;
+    }
+    if constexpr (SLAB) {
+      // SDT_SLAB: every Ψ this wave loaded lies in its own slab, so its stamps and passes 0 .. M-2 need no other
+      // wave: they run at once, on the predicted stamps (redone below on a miss; discarded if the row takes no
+      // transform); then this wave's share of the pipeline, and the row's first barrier only before the last pass
+      wave_passes();
+      h.arrive();  // this wave's previous stores drained; the last wave to arrive publishes `loaded` and `done`
+      h.go();      // this wave's polls matched -> its share of the next row's loads and of the sphere-order copy
+      sd_bar();    // every wave's passes 0 .. M-2 and counts are in LDS
+    } else {
+      h.drain();
+      sd_bar();  // Ψ by rank and the stamps of every wave are in LDS; every wave has consumed its loads
+      // `v` and `pin` are dead from here on: the driver may reuse the latter
+      h.go();
+    }
+    SD_STAMP(1);
+    nv = 0;
+    bool fail = miss;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      nv += sh.rnv[q];
+      fail |= sh.rfail[q] != 0;
+    }
+    nf = nv >> 16;
+    nv &= 0xFFFF;
+    // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
+    empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || nf == 0)) != 0;  // uniform
+    if (__builtin_amdgcn_readfirstlane((int)(!empty && nf > SD_SPARSE && nv > SD_FEW && fail))) {
+      // the exact range of the row from Ψ by rank (lane t: ranks t + T·q), then the stamps again
+      double pmn = INFINITY, pmx = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const double x = psi[tid + T * q];
+        pmn = sd_min(pmn, x);  // +Inf is neutral
+        pmx = sd_max(pmx, __hiloint2double(x < INFINITY ? __double2hiint(x) : (int)0xFFF00000, __double2loint(x)));
+      }
+      sd_wave_stats(pmn, pmx);
+      if (lane == 0) {
+        sh.rmn[w] = pmn;
+        sh.rmx[w] = pmx;
+      }
+      sd_bar();
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        pmn = sd_min(pmn, sh.rmn[q]);
+        pmx = sd_max(pmx, sh.rmx[q]);
+      }
+      if (tid == 0 && prow) {  // read again at this row's next step, after many barriers
+        const double mg = (pmx - pmn) + 8.0 * beta;
+        prow[0] = pmn - mg;
+        prow[1] = pmx + mg;
+      }
+      scale(pmn, pmx);
+      if (__builtin_amdgcn_readfirstlane((int)(scale_ok && tol < base * 0x1p-20))) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int j = tid + T * q;
+          const double x = psi[j];
+          dtv[sd_swz(j)] = x < INFINITY ? stamp(x, j) : INFINITY;
+        }
+        sd_bar();
+        if constexpr (SLAB) {
+          wave_passes();
+          sd_bar();
+        }
+      }
+      if (tid == 0) sh.cnt[2] += 1;  // rows stamped twice (diagnostics)
+    }
+  } else {
+    double pmn = INFINITY, pmx = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const double x = v[2 * q + hh];
+        psi[(hh ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
+        const bool fin = x < INFINITY;
+        nv += __popcll(__ballot(fin)) << 16;
+        pmn = sd_min(pmn, x);  // +Inf is neutral
+        pmx = sd_max(pmx, __hiloint2double(fin ? __double2hiint(x) : (int)0xFFF00000, __double2loint(x)));  // +Inf -> -Inf
+      }
+    sd_wave_stats(pmn, pmx);
+    if (lane == 0) {
+      sh.rmn[w] = pmn;
+      sh.rmx[w] = pmx;
+      sh.rnv[w] = nv;
+    }
+    sd_bar();  // every wave has consumed its loads of S_{i+1} (their values are in LDS)
+    h.early();
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      pmn = sd_min(pmn, sh.rmn[q]);
+      pmx = sd_max(pmx, sh.rmx[q]);
+    }
+    nv = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) nv += sh.rnv[q];
+    nf = nv >> 16;
+    nv &= 0xFFFF;
+    SD_STAMP(1);
+    // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
+    empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || !(pmn < INFINITY))) != 0;  // uniform
+    scale(pmn, pmx);
   }
-  sd_bar();  // every wave has consumed its loads of S_{i+1} (their values are in LDS)
-  h.early();
-#pragma unroll
-  for (int q = 0; q < NW; ++q) {
-    pmn = sd_min(pmn, sh.rmn[q]);
-    pmx = sd_max(pmx, sh.rmx[q]);
-  }
-  nv = 0;
-#pragma unroll
-  for (int q = 0; q < NW; ++q) nv += sh.rnv[q];
-  const int nf = nv >> 16;
-  nv &= 0xFFFF;
-  SD_STAMP(1);
-  // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
-  const bool empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || !(pmn < INFINITY))) != 0;  // uniform
-
-  // ---- the binade: values base + (Ψ - Ψmin)/β + d lie in [base, 2·base), grid g = 2^18 ulp ----------
-  const double inv = Lv.inv_beta;                      // fl(1/β), host-computed
-  const double rs = (pmx - pmn) * inv + (double)Smax;  // scaled range of every transform value
-  const bool scale_ok = rs < 0x1p31;                   // else unit steps are not on the grid: exact scans
-  const int E = ilogb(fmin(rs, 0x1p31) * (1.0 + 0x1p-20) + 1.0) + 2;  // 2^E >= 2·rs (E <= SD_GRID: g <= 1)
-  const double base = ldexp(1.0, E), g = ldexp(1.0, E - SD_GRID);
-  double qmax = beta * (double)Smax + fmax(fabs(pmn), fabs(pmx));  // >= |T1 + β·d + Ψ| for every candidate
-#pragma unroll
-  for (int m = 0; m < M; ++m) qmax += fabs(a[m]) * (double)max(abs(lb[m]), abs(lb[m] + 7));
-  // 2 × stamping error (< g) + 2 × the reference's rounding (<= 4u·qmax per candidate), in units of β
-  const double tol = 3.0 * g + 0x1p-49 * qmax * inv;
   // few finite sources (rows near c' = 0): every target's minimum over them, directly
   const bool sparse = !empty && nf <= SD_SPARSE;
   const bool direct = !empty && !sparse && (nv <= SD_FEW || !scale_ok || !(tol < base * 0x1p-20));
 
-  double o[8];
   int spj[SD_SPARSE];
   double spv[SD_SPARSE];
   if (sparse) {
     if (tid == 0) sh.nsp = 0;
     sd_bar();
+    if constexpr (PRED) {  // `v` is dead: the finite sources from Ψ by rank
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        if (v[2 * q + h] < INFINITY) {
+      for (int q = 0; q < 8; ++q) {
+        const double x = psi[tid + T * q];
+        if (x < INFINITY) {
           const int e = atomicAdd(&sh.nsp, 1);
-          sh.spj[e] = (int)((h ? ein[q].y : ein[q].x) & 0xFFFFu);
-          sh.spv[e] = v[2 * q + h];
+          sh.spj[e] = tid + T * q;
+          sh.spv[e] = x;
         }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+          if (v[2 * q + hh] < INFINITY) {
+            const int e = atomicAdd(&sh.nsp, 1);
+            sh.spj[e] = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
+            sh.spv[e] = v[2 * q + hh];
+          }
+    }
     sd_bar();
 #pragma unroll
     for (int e = 0; e < SD_SPARSE; ++e) {  // uniform: broadcast reads into registers
@@ -569,73 +784,34 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     }
   }
   const bool transform = !direct && !empty && !sparse;  // uniform
-  if (transform) {
-    // ---- stamp: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) | j --------------------------------------------
+  if constexpr (!PRED) {
+    if (transform) {
+      // ---- stamp: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) | j --------------------------------------------
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int j = (int)((h ? ein[q].y : ein[q].x) & 0xFFFFu);
-        const double x = v[2 * q + h];
-        double V = INFINITY;
-        if (x < INFINITY) {
-          const double y = (x - pmn) * inv + base;
-          V = __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | (j << SD_CB));
+        for (int hh = 0; hh < 2; ++hh) {
+          const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
+          const double x = v[2 * q + hh];
+          dtv[sd_swz(j)] = x < INFINITY ? stamp(x, j) : INFINITY;
         }
-        dtv[sd_swz(j)] = V;
-      }
-    h.drain();
-    sd_bar();
-    SD_STAMP(2);
-  } else {
-    h.drain();
-    sd_bar();
+      h.drain();
+      sd_bar();
+      SD_STAMP(2);
+    } else {
+      h.drain();
+      sd_bar();
+    }
+    // `v` and `pin` are dead from here on: the driver may reuse the latter
+    h.go();
   }
-  // `v` and `pin` are dead from here on: the driver may reuse the latter
-  h.go();
   if (transform) {
-    // ---- M passes: forward and backward sweep along the 8 levels of one dimension, unit step 1.0 -----
+    // ---- the M passes (SDT_SLAB: passes 0 .. M-2 already ran per wave, only the last pass is left) ----------------
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      int pos[8];
-#pragma unroll
-      for (int x = 0; x < 8; ++x) {
-        pos[x] = sd_swz(sd_rank((int)threadIdx.x, m, x));  // tid-only: hoisted out of the row loop
-        o[x] = dtv[pos[x]];
-      }
-#if SDT_PASS_SPLIT
-      // two independent chains (prefix f over sources <= x, strict suffix b over sources > x: disjoint candidate
-      // sets), then one merge per point: half the dependency depth of the in-place sweeps, 20 merges instead of 14
-      {
-        double f[8], b[8];
-        f[0] = o[0];
-        b[7] = o[7];
-#pragma unroll
-        for (int x = 1; x < 8; ++x) {
-          f[x] = sd_merge(o[x], f[x - 1] + 1.0, tol);
-          if (x < 7) b[7 - x] = sd_merge(o[7 - x], b[8 - x] + 1.0, tol);
-        }
-#pragma unroll
-        for (int x = 0; x < 7; ++x) o[x] = sd_merge(f[x], b[x + 1] + 1.0, tol);
-        o[7] = f[7];
-      }
-#else
-      // in place: after the forward sweep o[x] covers the sources at <= x; a backward merge of o[x] with
-      // o[x+1] + 1 compares a source at <= x with itself shifted by >= 2, never within tol, so every
-      // flagged tie is between two distinct sources (as in a merge of disjoint sets)
-#pragma unroll
-      for (int x = 1; x < 8; ++x) o[x] = sd_merge(o[x], o[x - 1] + 1.0, tol);
-#pragma unroll
-      for (int x = 6; x >= 0; --x) o[x] = sd_merge(o[x], o[x + 1] + 1.0, tol);
-#endif
-      if (m + 1 < M) {
-#pragma unroll
-        for (int x = 0; x < 8; ++x) dtv[pos[x]] = o[x];
-      }
+    for (int m = SLAB ? M - 1 : 0; m < M; ++m) {
+      pass(m);
 #if SDT_WAVE_LOCAL
-      // the lines of passes 0 .. M-2 keep the top grid coordinate (rank bits 3(M-1)..) = the wave index (the swizzle
-      // leaves those bits alone): a wave reads only what it wrote itself, so only the last pass, which runs along
-      // that coordinate, needs every wave's values
+      // only the last pass, which runs along the top coordinate, needs every wave's values
       if (m + 2 < M)
         sd_wave_sync();
       else if (m + 1 < M)
@@ -665,8 +841,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
         const bool flg = (__double2loint(o[x]) & SD_CNT) != 0;
         // d(l, j*) exactly: an unflagged finite o[x] is V_j* + d with V_j* = the stamp of Ψ_j* (the same expression
         // as the stamping above, payload j*), every term exact in the binade (garbage, unused, otherwise)
-        const double y = (pv[x] - pmn) * inv + base;
-        const double dd = o[x] - __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | (j << SD_CB));
+        const double dd = o[x] - stamp(pv[x], j);
         const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
         const double val = (t1 + beta * dd) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
         listed |= (unsigned)(fin && flg) << x;
@@ -739,8 +914,8 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   // ---- Φ_i row c' in the sphere order of u_old(i), and the U row, both 16 bytes per lane ------------
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint2 e = *reinterpret_cast<const uint2 *>(pout + 2 * (tid + T * q));
-    sd_store16<PERSIST>(Sout, L * 8, 2 * (tid + T * q), __double_as_longlong(outv[e.x & 0xFFFFu]),
+    const uint2 e = *reinterpret_cast<const uint2 *>(pout + sd_p2<M>(tid, q));
+    sd_store16<PERSIST>(Sout, L * 8, sd_p2<M>(tid, q), __double_as_longlong(outv[e.x & 0xFFFFu]),
                         __double_as_longlong(outv[e.y & 0xFFFFu]));
   }
   {
@@ -763,8 +938,8 @@ __device__ __forceinline__ void sd_issue_loads(double (&v)[8], const uint32_t *p
   const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int p2 = 2 * (tid + T * q);
-    const uint2 e = *reinterpret_cast<const uint2 *>(pin + 2 * (tid + T * q));
+    const int p2 = sd_p2<M>(tid, q);
+    const uint2 e = *reinterpret_cast<const uint2 *>(pin + p2);
     const int ra = cp - (int)(e.x >> 16), rb = cp - (int)(e.y >> 16);
     double va = INFINITY, vb = INFINITY;
     if (ra == rb && (ra >= 1 || (ra == 0 && !r0))) {  // one 16-byte load (the common case)
@@ -837,7 +1012,7 @@ __device__ __forceinline__ void sdt_row0(const ProblemDev &P, const LevelsDev &L
   const double *Sin = Sin_all + (size_t)k * s_stride;
   double *S0 = Sout_all + (size_t)k * s_stride;
   uint16_t *U0 = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(B + 1) * L);
-  const double psi0 = sd_load8<PERSIST>(Sin, (B + 1) * L * (int)sizeof(double), 0);  // Φ_{i+1}[j0, 0]
+  const double psi0 = sd_load8<PERSIST>(Sin, (B + 1) * L * (int)sizeof(double), pm.pin_h);  // Φ_{i+1}[j0, 0]
   const SdEdge<M> E(P, lb_g, k, i);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave's read of S_{i+1} has returned
@@ -854,7 +1029,7 @@ __device__ __forceinline__ void sdt_row0(const ProblemDev &P, const LevelsDev &L
       const double val = (E.t1(r) + beta * (double)SdEdge<M>::dist(r, j0)) + psi0;
       o[h] = src0 && (int)(e >> 16) <= B && val < INFINITY ? val : INFINITY;
     }
-    sd_store16<PERSIST>(S0, L * 8, 2 * (tid + T * q), __double_as_longlong(o[0]), __double_as_longlong(o[1]));
+    sd_store16<PERSIST>(S0, L * 8, sd_p2<M>(tid, q), __double_as_longlong(o[0]), __double_as_longlong(o[1]));
   }
   // U row in natural order: ranks 8·tid .. 8·tid + 7, one 16-byte store
   unsigned short u0[8];
@@ -884,7 +1059,7 @@ __device__ __forceinline__ void sdt_rowB(const ProblemDev &P, const LevelsDev &L
   double v[8];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int p2 = 2 * (tid + T * q);
+    const int p2 = sd_p2<M>(tid, q);
     const int ra = max(B - (int)(pm.in[q].x >> 16), 0), rb = max(B - (int)(pm.in[q].y >> 16), 0);
     sd_load_pair<PERSIST>(Sin, sbytes, ra * L + p2, rb * L + p2 + 1, v[2 * q], v[2 * q + 1]);
   }
@@ -939,8 +1114,8 @@ __device__ __forceinline__ void sdt_rowB(const ProblemDev &P, const LevelsDev &L
   if (has0 && tid == 0) atomicAdd(&counters[1], 1);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const bool p0 = wb && tid == 0 && q == 0;  // only sphere position 0 (= l0) can be finite
-    sd_store16<PERSIST>(SB, L * 8, 2 * (tid + T * q), p0 ? __double_as_longlong(bv) : 0x7FF0000000000000ull,
+    const bool p0 = wb && sd_p2<M>(tid, q) == pm.pout_h;  // only the head position (= l0) can be finite
+    sd_store16<PERSIST>(SB, L * 8, sd_p2<M>(tid, q), p0 ? __double_as_longlong(bv) : 0x7FF0000000000000ull,
                         0x7FF0000000000000ull);
   }
   unsigned short ub[8];
@@ -951,6 +1126,8 @@ __device__ __forceinline__ void sdt_rowB(const ProblemDev &P, const LevelsDev &L
 
 // per-step driver: no pipeline hooks
 struct SdHooksNone {
+  __device__ __forceinline__ void poll() {}
+  __device__ __forceinline__ void arrive() {}
   __device__ __forceinline__ void early() {}
   __device__ __forceinline__ void drain() {}
   __device__ __forceinline__ void go() {}
@@ -976,14 +1153,18 @@ __device__ __forceinline__ void sd_perm_dma(const uint32_t *src, uint32_t *slot)
 // The same copy for the persistent driver, as inline asm: the compiler then does not know these instructions
 // write LDS, and does not make every later LDS atomic wait (vmcnt(0)) for them -- and for the row loads queued
 // behind.  The driver orders them itself: they are issued before the next row's loads and complete under the
-// counted wait at that row's start, and every reader of the slot reads it after a later vmcnt(0) and a barrier.
-template <int M>
+// counted wait at that row's start, and every reader of the slot reads it after a later vmcnt(0) and a barrier
+// (SDT_SLAB: a later counted wait of its own wave).
+// OWN_SLAB (SDT_SLAB): wave w copies only the chunks of its own slab (positions [w·L/NW, (w+1)·L/NW)): the only
+// positions of the slot it reads itself, so no other wave needs to be past its reads of the old contents.
+template <int M, bool OWN_SLAB = false>
 __device__ __forceinline__ void sd_perm_dma_asm(const uint32_t *src, uint32_t *slot) {
-  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, NC = L * 4 / 1024, CPW = NC / NW;
+  static_assert(!OWN_SLAB || CPW * NW == NC, "slab chunks");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)slot);
 #pragma unroll
-  for (int c = wave; c < L * 4 / 1024; c += NW) {
+  for (int c = OWN_SLAB ? wave * CPW : wave; OWN_SLAB ? c < (wave + 1) * CPW : c < NC; c += OWN_SLAB ? 1 : NW) {
     const char *g = (const char *)src + c * 1024 + lane * 16;
     const unsigned m0 = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)c * 1024u);
     unsigned keep;  // M0 is reserved to the compiler: saved and restored around the copy
@@ -1054,11 +1235,11 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
   const int k = (int)blockIdx.y, tid = threadIdx.x;
-  if (tid == 0) sh.cnt[0] = sh.cnt[1] = 0;
+  if (tid == 0) sh.cnt[0] = sh.cnt[1] = sh.cnt[2] = 0;
   // B >= 1: block 0 takes rows 0 and B together, block x the row x (B workgroups, one per CU at B = 256)
   if (blockIdx.x == 0 && P.B >= 1) {
     SdPerm pm;
-    sd_perm_load<M>(pm, perm_all, P.nt, k, i);
+    sd_perm_load<M>(pm, perm_all, P, G, k, i);
     sdt_row0<M, false>(P, Lv, k, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k, G.base, nullptr, 0);
     sdt_rowB<M, false>(P, Lv, k, i, pm, Sin_all, Sout_all, UU_all, s_stride, uu_stride_k, G.base, counters, sh,
                        nullptr, 0);
@@ -1075,10 +1256,10 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
     SdHooksNone hooks;
     uint2 ein[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ein[q] = *reinterpret_cast<const uint2 *>(slot + 2 * (tid + (L / 8) * q));
+    for (int q = 0; q < 4; ++q) ein[q] = *reinterpret_cast<const uint2 *>(slot + sd_p2<M>(tid, q));
     sdt_body<M, false>(P, Lv, G, k, cp, i, v, ein, slot, slot + L, Sout_all + (size_t)k * s_stride + (size_t)cp * L,
                        UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(P.B + 1) * L) + (size_t)cp * L, sh,
-                       sds, hooks, P.df, P.uold);
+                       sds, hooks, P.df, P.uold, nullptr);
     if (tid == 0) {
       if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
       if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
@@ -1103,10 +1284,12 @@ __global__ __launch_bounds__(256) void k_sdt_chain(ProblemDev P, PyrGeom G, doub
   const int k = (int)blockIdx.x, tid = threadIdx.x, nt = P.nt;
   const uint32_t *pk = perm_all + (size_t)k * nt * L;
   double *Vk = V + (size_t)k * nt;
-  auto j0 = [&](int i) { return (int)(pk[(size_t)i * L] & 0xFFFFu); };
+  // the head of step i's sphere order (the level at distance 0 from u_old(i), if u_old(i) is on the grid)
+  auto head = [&](int i) { return pk[(size_t)i * L + sd_headpos<M>(G, P.uold[((size_t)k * nt + i) * M + M - 1])]; };
+  auto j0 = [&](int i) { return (int)(head(i) & 0xFFFFu); };
   // Φ_i[j0(i), 0] exists only where u_old(i) is a level (the head at distance 0); an off-grid u_old(i) leaves
   // budget row 0 empty at step i, and then at every earlier step (+Inf propagates through the additions)
-  auto on_grid = [&](int i) { return (pk[(size_t)i * L] >> 16) == 0u; };
+  auto on_grid = [&](int i) { return (head(i) >> 16) == 0u; };
   auto t1 = [&](int r, int i) {  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
     const double *dfi = P.df + ((size_t)k * nt + i) * M;
     double t = 0.0;
@@ -1157,7 +1340,10 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_row0(ProblemDev P, Lev
   const int i = (int)blockIdx.x, k = (int)blockIdx.y, tid = threadIdx.x, nt = P.nt, B = P.B;
   const uint32_t *pi = perm_all + ((size_t)k * nt + i) * L;
   const bool term = i == nt - 1;
-  const int jn = term ? 0 : (int)(perm_all[((size_t)k * nt + i + 1) * L] & 0xFFFFu);  // j0(i+1)
+  const int jn = term ? 0
+                      : (int)(perm_all[((size_t)k * nt + i + 1) * L +
+                                       sd_headpos<M>(G, P.uold[((size_t)k * nt + i + 1) * M + M - 1])] &
+                              0xFFFFu);  // j0(i+1)
   const double vn = term ? 0.0 : V[(size_t)k * nt + i + 1];
   const SdEdge<M> E(P, G.base, k, i);
   double *reg = S_all + (size_t)k * kstride;
@@ -1168,11 +1354,11 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_row0(ProblemDev P, Lev
   };
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint2 e = *reinterpret_cast<const uint2 *>(pi + 2 * (tid + T * q));
+    const uint2 e = *reinterpret_cast<const uint2 *>(pi + sd_p2<M>(tid, q));
     const double o0 = (int)(e.x >> 16) > B ? INFINITY : val((int)(e.x & 0xFFFFu));
     const double o1 = (int)(e.y >> 16) > B ? INFINITY : val((int)(e.y & 0xFFFFu));
-    *reinterpret_cast<double2 *>(r0 + 2 * (tid + T * q)) = make_double2(o0, o1);
-    if (i == 0) *reinterpret_cast<double2 *>(reg + 2 * (tid + T * q)) = make_double2(o0, o1);  // S_0 row 0 (buffer 0)
+    *reinterpret_cast<double2 *>(r0 + sd_p2<M>(tid, q)) = make_double2(o0, o1);
+    if (i == 0) *reinterpret_cast<double2 *>(reg + sd_p2<M>(tid, q)) = make_double2(o0, o1);  // S_0 row 0 (buffer 0)
   }
   if (!term) {  // U row 0 of step i, natural order: ranks 8·tid .. 8·tid + 7 (written where Φ_i is finite)
     unsigned short u0[8];
@@ -1205,7 +1391,7 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
   const int tid = threadIdx.x;
   uint2 e[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) e[q] = *reinterpret_cast<const uint2 *>(pin + 2 * (tid + T * q));  // reads first
+  for (int q = 0; q < 4; ++q) e[q] = *reinterpret_cast<const uint2 *>(pin + sd_p2<M>(tid, q));  // reads first
 #pragma unroll
   for (int q = 0; q < 4; ++q) w.e[q] = e[q];
   // an offset beyond the resource's range drops the access (the load returns 0 without touching memory): rows
@@ -1214,7 +1400,7 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
   unsigned oa[4], ob[4], mask = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int p2 = 2 * (tid + T * q);
+    const int p2 = sd_p2<M>(tid, q);
     const int ra = cp - (int)(e[q].x >> 16), rb = cp - (int)(e[q].y >> 16);
     oa[q] = ra >= 1 ? boff + (unsigned)ra * rowb + (unsigned)p2 * 8u : ra == 0 ? r0 + (unsigned)p2 * 8u : OOB;
     ob[q] = rb == ra ? OOB
@@ -1293,13 +1479,25 @@ struct SdPipe {
   int need, val;
   SdRaw raw;
 
-  // this row's loads have been consumed by every wave: publish `loaded`; every wave polls its own dependency flags
-  // (lanes 0-31 RAW for the next row, 32-63 WAR for this row's stores; a lane without one polls a flag that always
-  // passes -- every lane loads, no branch), checked in go()
+  // every wave polls its own dependency flags (lanes 0-31 RAW for the next row, 32-63 WAR for this row's stores; a
+  // lane without one polls a flag that always passes -- every lane loads, no branch), checked in go(): SDT_PRED at
+  // the row's start (`loaded` is published in go()), else once every wave has consumed this row's loads (early(),
+  // which publishes `loaded` first)
+  __device__ __forceinline__ void poll() {
+    if constexpr (SDT_PRED) {
+      SD_TL_AT(g0, i, nt, 1);
+      issue_polls();
+    }
+  }
   __device__ __forceinline__ void early() {
-    SD_TL_AT(g0, i, nt, 1);
+    if constexpr (!SDT_PRED) {
+      SD_TL_AT(g0, i, nt, 1);
+      if (threadIdx.x == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      issue_polls();
+    }
+  }
+  __device__ __forceinline__ void issue_polls() {
     const int tid = threadIdx.x, lane = tid & 63, s = lane < 32 ? lane + 1 : lane - 31;
-    if (tid == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     fp = lk + cp;
     need = INT32_MIN;
     if (lane < 32) {
@@ -1320,7 +1518,27 @@ struct SdPipe {
   // every wave, right before a barrier: its stores of the previous row (and its polls) have landed
   __device__ __forceinline__ void drain() {
     SD_TL_AT(g0, i, nt, 2);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // SDT_PRED: the wave's poll (one load, issued after the previous row's stores) may still be in flight
+    if constexpr (SDT_PRED)
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  // SDT_SLAB (instead of drain + barrier + the flag stores of go()): this wave's stores of the previous row have
+  // landed (its one poll may be in flight) and it has consumed this row's loads; it counts itself in, and the last wave
+  // to arrive publishes `loaded` for this row and `done` for the previous one -- the measured-valid hand-off with an
+  // LDS arrival count in the place of the workgroup barrier (every storing wave drained before it is counted, one
+  // lane of the last wave stores the flags)
+  __device__ __forceinline__ void arrive() {
+    drain();
+    if ((threadIdx.x & 63) == 0) {
+      constexpr int NW = (1 << (3 * M - 3)) / 64;
+      if (atomicAdd(&sh->arrive, 1) == NW - 1) {
+        sh->arrive = 0;  // every wave is counted: the next row's arrivals come after this row's barrier
+        __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (pcp >= 0) __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
   // after that barrier: publish the previous row; this wave waits until its polls match (re-polling), then issues
   // the first quarter of the next row's loads -- the measured-valid consumer form: the polling wave loads only
@@ -1330,7 +1548,12 @@ struct SdPipe {
     const int tid = threadIdx.x;
     // evaluated before the flag store below: the compiler's wait for `val` would otherwise cover that store
     bool ready = __all(val >= need);
-    if (tid == 0 && pcp >= 0) __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (the SDT_SLAB row flow publishes both in arrive() instead)
+    constexpr bool flags_here = !(SDT_PRED && SDT_SLAB);
+    if (flags_here && SDT_PRED && tid == 0)
+      __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (flags_here && tid == 0 && pcp >= 0)
+      __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     while (!ready) {
       if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
@@ -1360,7 +1583,7 @@ struct SdPipe {
       // u_old alone (k_pyr_order), so the slot already holds it (by induction, every slot holds the order of the last
       // step assigned to it)
       if (ni != i && !(SDT_PERM_SKIP && sd_same_uold<M>(uoa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + i + 1) * M)))
-        sd_perm_dma_asm<M>(pk + (size_t)ni * L, slot + (ni & 1) * L);
+        sd_perm_dma_asm<M, (SDT_PRED && SDT_SLAB)>(pk + (size_t)ni * L, slot + (ni & 1) * L);
       sd_dfuo_dma<M>(dfa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + ni) * M, sds);
     }
     SD_TL_AT(g0, i, nt, 5);
@@ -1402,7 +1625,12 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   h.pcp = -1, h.pi = 0;
   if (tid == 0) {
     sh.stop = 0;
-    sh.cnt[0] = sh.cnt[1] = 0;
+    sh.arrive = 0;
+    sh.cnt[0] = sh.cnt[1] = sh.cnt[2] = 0;
+  }
+  if (tid < SD_PRED_ROWS) {  // no predicted scale yet (the prologue's barrier orders these before every use)
+    sh.pred[tid][0] = INFINITY;
+    sh.pred[tid][1] = -INFINITY;
   }
   // prologue: both sphere orders of the first step, df / u_old, and the first row's loads (the terminal row was
   // written by an earlier launch)
@@ -1440,15 +1668,17 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       // one row per workgroup: a sphere-0 source at distance 0 (u_old(i+1) on the level grid: position 0 with b̃ = 0)
       // is this workgroup's own output of the previous row, still in LDS (the loaded copy predates it); an off-grid
       // u_old(i+1) has b̃ >= 1 everywhere and no such source
-      if (hi - lo == 1 && h.pcp >= 0 && tid == 0 && (pslot(i + 1)[0] >> 16) == 0)
-        v[0] = status == 1 ? INFINITY : dtv[pslot(i + 1)[0] & 0xFFFFu];
+      // (the head of the sphere order is the first position of some wave's lane 0: position 0, or (SDT_SLAB) the first
+      // position of u_old(i+1)'s slab)
+      if (hi - lo == 1 && h.pcp >= 0 && (tid & 63) == 0 && (h.raw.e[0].x >> 16) == 0)
+        v[0] = status == 1 ? INFINITY : dtv[h.raw.e[0].x & 0xFFFFu];
       uint2 ein[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) ein[q] = h.raw.e[q];
       status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, ein, pslot(i + 1), pslot(i),
                                  reg + (size_t)(i % NB) * R * L + (size_t)cp * L,
                                  UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L, sh,
-                                 sds, h, df_all, uo_all);
+                                 sds, h, df_all, uo_all, cp - lo < SD_PRED_ROWS ? sh.pred[cp - lo] : nullptr);
       SD_TL(6);
       stop = sh.stop != 0;  // written before a barrier the row has passed since (every path has one)
     }
@@ -1456,10 +1686,13 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   if (tid == 0) {
     if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
     if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
+    if (sh.cnt[2]) atomicAdd(&counters[4], sh.cnt[2]);
   }
   SD_FLUSH();
   SD_TL_FLUSH(h.g0);
 }
+
+int sdt_slab_shift(const PyrGeom &G) { return SDT_SLAB ? 3 * (G.M - 1) : 0; }
 
 bool sdt_supported(const PyrGeom &G) {
   if (G.M != 3 && G.M != 4) return false;

@@ -2,14 +2,20 @@
 stamps_tl`): for every row and the 64 steps from nt/2 down, s_memrealtime (100 MHz) at 8 points of the row body:
 0 start, 1 loads consumed, 2 mid point, 3 previous row drained, 4 next row's inputs ready, 5 next row's loads issued,
 6 stores issued.  Prints the phase durations, the step period and the pipeline skew between neighbouring rows.
-Usage: python scripts/probe_sdt_timeline.py [nt] [NB]"""
+Usage: python scripts/probe_sdt_timeline.py [nt] [NB]  [save.npy] [--lib another timeline build]
+(SDT_PRED builds: point 1 is the row's poll issue, right after its loads are taken.)"""
 import ctypes
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")
-os.environ["MIOC_LIB"] = os.path.join(PKG, "lib", "libmioc_stamps_tl.so")
+_lib = os.path.join(PKG, "lib", "libmioc_stamps_tl.so")
+if "--lib" in sys.argv:  # another timeline build (e.g. make variant VFLAGS="-DMIOC_STAMPS -DMIOC_STAMPS_TL ...")
+    q = sys.argv.index("--lib")
+    _lib = sys.argv[q + 1]
+    del sys.argv[q:q + 2]
+os.environ["MIOC_LIB"] = _lib
 sys.path.insert(0, PKG)
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
