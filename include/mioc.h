@@ -284,7 +284,7 @@ int32_t mioc_last_algo(mioc_ctx *ctx);
  * by the exact scan, or for the U-table walks (generic, pyramid) the run-ahead rounds taken (each round
  * settles up to 64 steps), [3] internal consistency failures (must be 0); [4..7] pyramid internals: rows whose
  * value hash overflowed, targets whose value was not found, values flagged as colliding (after a separable-transform
- * DP, [6] instead counts this context's persistent DPs redone with per-step launches: cooperative launch refused, or
+ * DP, [4] instead counts the persistent driver's rows whose predicted stamp scale missed (stamped twice), and [6] counts this context's persistent DPs redone with per-step launches: the grid does not fit, or
  * a dependency wait timed out -- 0 on a healthy run; after a fused separable DP, the segmented launches redone with
  * one workgroup per subproblem); [7] fused DP: resident workgroups per CU (occupancy query); [8] fused separable DP:
  * row segments per subproblem (0: the one-lane-per-row kernel); [9] p=Inf segmented walk: subproblems whose path

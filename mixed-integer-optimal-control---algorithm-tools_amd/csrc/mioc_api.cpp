@@ -103,7 +103,7 @@ void free_all(mioc_ctx *ctx) {
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
                   ctx->pinf.kabs, ctx->pinf.ftab, ctx->pinf.fseg, ctx->pinf.fneed,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
-                  ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm,
+                  ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm, ctx->d_same2,
                   ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own, ctx->d_ode_state};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -317,11 +317,12 @@ int run_bellman(mioc_ctx *ctx) {
     rc = grow(ctx, &ctx->d_U, &ctx->U_cap, K * uu_stride_k * sizeof(uint16_t), "argmin table U");
     if (rc) return rc;
     rc = grow(ctx, &ctx->d_perm, &ctx->perm_cap, K * nt * L * sizeof(uint32_t), "sphere orders");
+    if (!rc) rc = grow(ctx, &ctx->d_same2, &ctx->same2_cap, K * nt * sizeof(int32_t), "sphere-order reuse flags");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
     double *term = persist ? ctx->d_stage + ((nt - 1) % nbuf) * s_stride : st[(nt - 1) & 1];
     HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm,
-                                  algo == MIOC_ALGO_SEPARABLE ? sdt_slab_shift(ctx->pyr) : 0));
+                                  algo == MIOC_ALGO_SEPARABLE ? sdt_slab_shift(ctx->pyr) : 0, ctx->d_same2));
     HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, term, ks));
     if (algo == MIOC_ALGO_SEPARABLE && persist) {
       // the whole DP as one persistent launch: rows handed between resident workgroups by flags
@@ -329,10 +330,11 @@ int run_bellman(mioc_ctx *ctx) {
                                    (size_t)nbuf * s_stride, (uint16_t *)ctx->d_U, uu_stride_k));
       HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, runflag_bytes, ctx->stream));
       ev_begin(ctx, 0, "k_sdt_run");
-      const hipError_t le = launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_stage, ks, nbuf,
+      const hipError_t le = launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_same2, ctx->d_stage, ks,
+                                           nbuf,
                                            (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags, nwg,
                                            ctx->spin_limit, run_lds);
-      if (le == hipErrorCooperativeLaunchTooLarge) {  // not every workgroup can be resident: one launch per step
+      if (le == hipErrorCooperativeLaunchTooLarge) {  // (kept for a grid the runtime refuses): one launch per step
         (void)hipGetLastError();
         ev_end(ctx, 0, 0);
         ctx->n_persist_fallbacks += 1;
@@ -399,11 +401,15 @@ int run_bellman(mioc_ctx *ctx) {
         *ctx->h_run_err = 0;
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_segflags, 0, (2 * K * (size_t)S + 1) * sizeof(int32_t), ctx->stream));
         ev_begin(ctx, 0, "k_fsep2");
-        const hipError_t le = launch_fsep2(ctx->stream, P, Lv, ctx->pyr, plan, ctx->d_front, front_stride,
-                                           (uint8_t *)ctx->d_U, u_stride_k, ctx->d_counters, ctx->d_ring, NB,
-                                           ctx->d_segflags, ctx->spin_limit);
+        int ncu = 0;
+        HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        // every segment must be resident at once (they wait for each other): else the unsegmented kernel below
+        const hipError_t le =
+            (size_t)K * (size_t)S > (size_t)ncu * (size_t)std::max<int64_t>(ctx->occupancy, 0)
+                ? hipErrorCooperativeLaunchTooLarge
+                : launch_fsep2(ctx->stream, P, Lv, ctx->pyr, plan, ctx->d_front, front_stride, (uint8_t *)ctx->d_U,
+                               u_stride_k, ctx->d_counters, ctx->d_ring, NB, ctx->d_segflags, ctx->spin_limit);
         if (le == hipErrorCooperativeLaunchTooLarge) {  // not every segment resident: one workgroup per subproblem
-          (void)hipGetLastError();
           ev_end(ctx, 0, 0);
           ctx->n_persist_fallbacks += 1;
           ctx->force_steps = true;

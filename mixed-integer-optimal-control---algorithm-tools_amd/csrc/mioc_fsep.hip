@@ -19,8 +19,9 @@
 //     segment q never waits for q+1 except to reuse a ring slot (NB steps back).  Flags are relaxed agent-scope
 //     atomics in the measured-valid form of MI355X_MICROARCH.md (sc1 stores drained by every storing wave,
 //     then one lane's flag store behind a barrier; the consumer loads the bytes only after its own poll
-//     matched).  S > 1 is a cooperative launch (every workgroup resident); a wait past the spin limit sets
-//     *err and every workgroup leaves, and the host redoes the DP with S = 1 (check_run).
+//     matched).  S > 1 needs every workgroup resident: the host launches it only when K·S fits the CUs x resident
+//     workgroups per CU (an ordinary launch, not a cooperative one); a wait past the spin limit sets *err and every
+//     workgroup leaves, and the host redoes the DP with S = 1 (check_run).
 //
 // Certified argmin, as in mioc_fused.hip's k_fsep_run: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) with the source
 // coordinates x0 | x1 << 3 in the 6 low mantissa bits and bit 6 as the near-tie flag; an unflagged winner is the
@@ -725,10 +726,10 @@ hipError_t launch_fsep2(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv,
   ProblemDev Pc = P;
   LevelsDev Lc = Lv;
   const dim3 grid((unsigned)(P.K * p.S)), block((unsigned)p.threads);
-  if (p.S > 1) {  // the segments of a subproblem wait for each other: every workgroup must be resident
-    void *args[] = {&Pc, &Lc, &A};
-    return hipLaunchCooperativeKernel(fsep2_fn(G, p), grid, block, args, (unsigned)p.lds, s);
-  }
+  // S > 1: the segments of a subproblem wait for each other, so every workgroup must be resident -- the caller checks
+  // the grid against the CUs x resident workgroups per CU (launch_fsep2 is not a cooperative launch: a cooperative
+  // launch makes the HIP runtime tear down its cooperative-queue state at process exit, which crashed every
+  // rocprofv3 run of round 3), and a dependency wait that times out makes the host redo the DP unsegmented
   void *args[] = {&Pc, &Lc, &A};
   return hipLaunchKernel(fsep2_fn(G, p), grid, block, args, p.lds, s);
 }

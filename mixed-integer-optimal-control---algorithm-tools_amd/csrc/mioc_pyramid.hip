@@ -823,7 +823,8 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
 // slab_shift > 0 (separable transform): slab-major -- the ranks are grouped first by their top grid coordinate
 // j >> slab_shift (the slab a row workgroup's wave owns), then by sphere, then ascending; every slab is one contiguous
 // block of L/8 positions, so the wave that owns a slab loads exactly its slab's sources (mioc_sdt.hip).
-__global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all, int slab_shift) {
+__global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all, int slab_shift,
+                                                   int32_t *same2) {
   constexpr int NK = 8 * 64;        // bucket keys: slab << 6 | min(distance, 63)
   __shared__ int start[NK];         // the next free position of each bucket
   __shared__ int wcnt[4][NK + 1];   // ranks of the current chunk per wave and bucket (NK: the inactive lanes)
@@ -834,6 +835,11 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
   int u[kMaxM];
 #pragma unroll
   for (int m = 0; m < kMaxM; ++m) u[m] = m < M ? (int)uo[m] : 0;
+  if (same2 && tid == 0) {  // u_old(i) == u_old(i+2) bit for bit: equal sphere orders (the persistent driver's reuse)
+    bool eq = i + 2 < P.nt;
+    for (int m = 0; eq && m < M; ++m) eq = __double_as_longlong(uo[m]) == __double_as_longlong(uo[2 * M + m]);
+    same2[(size_t)k * P.nt + i] = eq ? 1 : 0;
+  }
   for (int e = tid; e < NK; e += blockDim.x) start[e] = 0;
   for (int e = tid; e < 4 * (NK + 1); e += blockDim.x) (&wcnt[0][0])[e] = 0;
   __syncthreads();
@@ -888,8 +894,9 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
   }
 }
 
-hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int slab_shift) {
-  hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm, slab_shift);
+hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int slab_shift,
+                            int32_t *same2) {
+  hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm, slab_shift, same2);
   return hipGetLastError();
 }
 

@@ -406,7 +406,6 @@ struct SdtShared {
   int cnt[3];  // targets sent to the exact scan (near ties, direct rows), rows stamped twice (predicted scale
               // missed); flushed to the global counters [0], [1], [4] once
   int rfail[NW];  // per wave: a finite Ψ outside the row's predicted range (SDT_PRED)
-  int arrive;     // SDT_SLAB: waves of the current row past their drain (the last one publishes the row flags)
   double pred[SD_PRED_ROWS][2];  // per chunk row: the predicted range [lo, hi] of its Ψ (lo = +Inf: none yet)
 };
 
@@ -414,18 +413,23 @@ template <int M>
 __host__ __device__ constexpr size_t sd_slot_offset() {  // the two sphere-order slots follow the row body's arrays
   return ((size_t)1 << (3 * M)) * (2 * sizeof(double) + sizeof(uint16_t)) + SD_LCAP * sizeof(uint16_t);
 }
+// per wave: df(:, i) and u_old(:, i) (2M doubles), then one int32 flag (sphere-order reuse, SdPipe::go), padded to 16 B
 template <int M>
-__host__ __device__ constexpr size_t sd_dfuo_offset() {  // then df(:, i), u_old(:, i) per wave (persistent driver)
+__host__ __device__ constexpr size_t sd_dfuo_stride() {
+  return (2 * M + 2) * sizeof(double);
+}
+template <int M>
+__host__ __device__ constexpr size_t sd_dfuo_offset() {  // then df(:, i), u_old(:, i), a flag word per wave (persistent)
   return sd_slot_offset<M>() + 2 * ((size_t)1 << (3 * M)) * sizeof(uint32_t);
 }
 template <int M>
 __host__ __device__ constexpr size_t sd_out_offset() {  // then the row's outputs (natural order), SDT_WAVE_LOCAL
-  return sd_dfuo_offset<M>() + ((2 * M * sizeof(double) * (((size_t)1 << (3 * M - 3)) / 64) + 255) & ~(size_t)255);
+  return sd_dfuo_offset<M>() + ((sd_dfuo_stride<M>() * (((size_t)1 << (3 * M - 3)) / 64) + 255) & ~(size_t)255);
 }
 template <int M>
 __host__ __device__ constexpr size_t sd_lds_total() {
   return SDT_WAVE_LOCAL ? sd_out_offset<M>() + ((size_t)1 << (3 * M)) * sizeof(double)
-                        : sd_dfuo_offset<M>() + 2 * M * sizeof(double) * (((size_t)1 << (3 * M - 3)) / 64);
+                        : sd_dfuo_offset<M>() + sd_dfuo_stride<M>() * (((size_t)1 << (3 * M - 3)) / 64);
 }
 
 // Wave-local LDS ordering: this wave's LDS stores are complete before its next LDS reads (LDS instructions of one
@@ -498,7 +502,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   const double beta = Lv.beta;
   // df / u_old of this step: the persistent driver has copied them into this wave's LDS words (LDS-DMA issued one
   // row ahead: a global load here would cost a memory round trip per row); the per-step driver reads them directly
-  const double *dfi = PERSIST ? reinterpret_cast<const double *>(sds + sd_dfuo_offset<M>()) + 2 * M * (threadIdx.x >> 6)
+  const double *dfi = PERSIST ? reinterpret_cast<const double *>(sds + sd_dfuo_offset<M>()) + (2 * M + 2) * (threadIdx.x >> 6)
                               : df_all + ((size_t)k * P.nt + i) * M;
   const double *uoi = PERSIST ? dfi + M : uo_all + ((size_t)k * P.nt + i) * M;
   SD_RSTAMP(13);
@@ -508,7 +512,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   uint2 ein[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) ein[q] = ein_in[q];
-  h.poll();  // (SDT_PRED) this wave's dependency polls, checked after the row's first barrier
+  if constexpr (PERSIST && SDT_PRED && !SDT_SLAB) h.poll();  // this wave's dependency polls, checked in go()
   // ---- this thread's targets: ranks tid | x << 3(M-1) (the lines of the last pass) -----------------
   double a[M];
   int lb[M], uo[M];
@@ -646,13 +650,13 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     if constexpr (SLAB) {
       // SDT_SLAB: every Ψ this wave loaded lies in its own slab, so its stamps and passes 0 .. M-2 need no other
       // wave: they run at once, on the predicted stamps (redone below on a miss; discarded if the row takes no
-      // transform); then this wave's share of the pipeline, and the row's first barrier only before the last pass
+      // transform); the row's first barrier comes only before the last pass, with the drain before it (late in the
+      // row: the previous row's stores have long landed) and the pipeline hooks after it
+      h.poll();  // this wave's dependency polls (about as long before go() as their round trip takes)
       wave_passes();
-      h.arrive();  // this wave's previous stores drained; the last wave to arrive publishes `loaded` and `done`
-      h.go();      // this wave's polls matched -> its share of the next row's loads and of the sphere-order copy
-      sd_bar();    // every wave's passes 0 .. M-2 and counts are in LDS
+      sd_bar();  // every wave's passes 0 .. M-2 and counts are in LDS; every wave has consumed its loads
+      h.go();    // publish `loaded`, check the polls, issue the next row's loads and copies
     } else {
-      h.drain();
       sd_bar();  // Ψ by rank and the stamps of every wave are in LDS; every wave has consumed its loads
       // `v` and `pin` are dead from here on: the driver may reuse the latter
       h.go();
@@ -795,11 +799,9 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
           const double x = v[2 * q + hh];
           dtv[sd_swz(j)] = x < INFINITY ? stamp(x, j) : INFINITY;
         }
-      h.drain();
       sd_bar();
       SD_STAMP(2);
     } else {
-      h.drain();
       sd_bar();
     }
     // `v` and `pin` are dead from here on: the driver may reuse the latter
@@ -890,7 +892,9 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
           ++e;
         }
     }
+    h.late_drain();  // this wave's stores of the previous row have landed (late: they have had the whole row)
     sd_bar();
+    h.publish();     // ... so have every wave's: the previous row is done
     SD_STAMP(7);
     const int nl = sh.nlist;
     if (nl) {
@@ -908,7 +912,9 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
 #pragma unroll
     for (int x = 0; x < 8; ++x) outv[tid | (x << (3 * (M - 1)))] = INFINITY;
     reinterpret_cast<ulonglong2 *>(uu)[tid] = make_ulonglong2(~0ull, ~0ull);
+    h.late_drain();
     sd_bar();
+    h.publish();
   }
   SD_STAMP(8);
   // ---- Φ_i row c' in the sphere order of u_old(i), and the U row, both 16 bytes per lane ------------
@@ -1127,10 +1133,10 @@ __device__ __forceinline__ void sdt_rowB(const ProblemDev &P, const LevelsDev &L
 // per-step driver: no pipeline hooks
 struct SdHooksNone {
   __device__ __forceinline__ void poll() {}
-  __device__ __forceinline__ void arrive() {}
   __device__ __forceinline__ void early() {}
-  __device__ __forceinline__ void drain() {}
   __device__ __forceinline__ void go() {}
+  __device__ __forceinline__ void late_drain() {}
+  __device__ __forceinline__ void publish() {}
 };
 
 // LDS bytes of the row body: Ψ by rank, the transform / output values, the U row, the scan list, and two
@@ -1175,45 +1181,18 @@ __device__ __forceinline__ void sd_perm_dma_asm(const uint32_t *src, uint32_t *s
   }
 }
 
-// u_old(:, a) and u_old(:, b) bit for bit, by scalar loads in one asm statement with its own lgkmcnt wait (a plain C++
-// load here becomes a vector load whose vmcnt(0) wait would also wait for the row loads just issued)
-typedef unsigned int sd_s32x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int sd_s32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int sd_s32x2 __attribute__((ext_vector_type(2)));
+// df(:, s) and u_old(:, s) (M doubles each) into this wave's LDS words, and the flag same2[s - 1] (u_old(s-1) ==
+// u_old(s+1): the sphere order of step s-1 equals the one its slot holds, k_pyr_order) after them: lanes 0..4M move
+// one dword each (global_load_lds_dword, LDS-DMA, inline asm for the same reason as sd_perm_dma_asm)
 template <int M>
-__device__ __forceinline__ bool sd_same_uold(const double *a, const double *b) {
-  static_assert(M == 3 || M == 4, "sd_same_uold: M = 3 or 4");
-  if constexpr (M == 4) {
-    sd_s32x8 x, y;
-    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx8 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&s"(x), "=&s"(y)
-                 : "s"(a), "s"(b)
-                 : "memory");
-    bool same = true;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) same &= x[e] == y[e];
-    return same;
-  } else {
-    sd_s32x4 x0, y0;
-    sd_s32x2 x1, y1;
-    asm volatile("s_load_dwordx4 %0, %4, 0x0\n\ts_load_dwordx2 %1, %4, 0x10\n\ts_load_dwordx4 %2, %5, 0x0\n\t"
-                 "s_load_dwordx2 %3, %5, 0x10\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&s"(x0), "=&s"(x1), "=&s"(y0), "=&s"(y1)
-                 : "s"(a), "s"(b)
-                 : "memory");
-    return x0[0] == y0[0] && x0[1] == y0[1] && x0[2] == y0[2] && x0[3] == y0[3] && x1[0] == y1[0] && x1[1] == y1[1];
-  }
-}
-
-// df(:, i) and u_old(:, i) (M doubles each) into this wave's LDS words: lanes 0..4M-1 move one dword each
-// (global_load_lds_dword, LDS-DMA, inline asm for the same reason as sd_perm_dma_asm)
-template <int M>
-__device__ __forceinline__ void sd_dfuo_dma(const double *df, const double *uo, unsigned char *sds) {
+__device__ __forceinline__ void sd_dfuo_dma(const double *df, const double *uo, const int32_t *flag, unsigned char *sds) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane < 4 * M) {
-    const char *g = lane < 2 * M ? (const char *)df + 4 * lane : (const char *)uo + 4 * (lane - 2 * M);
-    const unsigned lds0 =
-        (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)(sds + sd_dfuo_offset<M>())) + wave * 16u * M;
+  if (lane < 4 * M + (flag ? 1 : 0)) {
+    const char *g = lane < 2 * M   ? (const char *)df + 4 * lane
+                    : lane < 4 * M ? (const char *)uo + 4 * (lane - 2 * M)
+                                   : (const char *)flag;
+    const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)(sds + sd_dfuo_offset<M>())) +
+                          wave * (unsigned)sd_dfuo_stride<M>();
     const unsigned m0 = __builtin_amdgcn_readfirstlane(lds0);
     unsigned keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -1470,6 +1449,7 @@ struct SdPipe {
   uint32_t *slot;
   __amdgpu_buffer_rsrc_t rs;
   const double *dfa, *uoa;
+  const int32_t *sm;  // same2 (k_pyr_order): u_old(s) == u_old(s + 2) per step s
   unsigned char *sds;
   SdtShared<(1 << (3 * M - 3)) / 64> *sh;
   // carried from row to row: the previous row (its `done` is published at this row's go()), this wave's polls, the
@@ -1492,7 +1472,6 @@ struct SdPipe {
   __device__ __forceinline__ void early() {
     if constexpr (!SDT_PRED) {
       SD_TL_AT(g0, i, nt, 1);
-      if (threadIdx.x == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       issue_polls();
     }
   }
@@ -1515,45 +1494,15 @@ struct SdPipe {
     }
     val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // every wave, right before a barrier: its stores of the previous row (and its polls) have landed
-  __device__ __forceinline__ void drain() {
-    SD_TL_AT(g0, i, nt, 2);
-    // SDT_PRED: the wave's poll (one load, issued after the previous row's stores) may still be in flight
-    if constexpr (SDT_PRED)
-      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  // SDT_SLAB (instead of drain + barrier + the flag stores of go()): this wave's stores of the previous row have
-  // landed (its one poll may be in flight) and it has consumed this row's loads; it counts itself in, and the last wave
-  // to arrive publishes `loaded` for this row and `done` for the previous one -- the measured-valid hand-off with an
-  // LDS arrival count in the place of the workgroup barrier (every storing wave drained before it is counted, one
-  // lane of the last wave stores the flags)
-  __device__ __forceinline__ void arrive() {
-    drain();
-    if ((threadIdx.x & 63) == 0) {
-      constexpr int NW = (1 << (3 * M - 3)) / 64;
-      if (atomicAdd(&sh->arrive, 1) == NW - 1) {
-        sh->arrive = 0;  // every wave is counted: the next row's arrivals come after this row's barrier
-        __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (pcp >= 0) __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  // after that barrier: publish the previous row; this wave waits until its polls match (re-polling), then issues
-  // the first quarter of the next row's loads -- the measured-valid consumer form: the polling wave loads only
-  // after its own poll matched
+  // after the row's first barrier (every wave has consumed this row's loads): publish `loaded`; this wave waits until
+  // its polls match (re-polling), then issues the next row's loads -- the measured-valid consumer form: the polling
+  // wave loads only after its own poll matched
   __device__ __forceinline__ void go() {
-    SD_TL_AT(g0, i, nt, 3);
+    SD_TL_AT(g0, i, nt, 2);
     const int tid = threadIdx.x;
     // evaluated before the flag store below: the compiler's wait for `val` would otherwise cover that store
     bool ready = __all(val >= need);
-    // (the SDT_SLAB row flow publishes both in arrive() instead)
-    constexpr bool flags_here = !(SDT_PRED && SDT_SLAB);
-    if (flags_here && SDT_PRED && tid == 0)
-      __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (flags_here && tid == 0 && pcp >= 0)
-      __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     while (!ready) {
       if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
@@ -1567,26 +1516,37 @@ struct SdPipe {
       val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       ready = __all(val >= need);
     }
-    SD_TL_AT(g0, i, nt, 4);
-    pcp = cp;
-    pi = i;
+    SD_TL_AT(g0, i, nt, 3);
     // the next row's loads; then (LDS-DMA, after them so that they do not wait for it) the next step's sphere order
-    // into the slot of step i+1 (every wave is past its last read of it: the drain barrier) and the next row's df /
-    // u_old; all of it is older than this row's five stores, so the counted wait at the next row's start covers it
+    // into the slot of step i+1 (every wave is past its last read of it: the barrier before go(); SDT_SLAB: each wave
+    // copies its own slab only) and the next row's df / u_old; all of it is older than this row's five stores, so the
+    // counted wait at the next row's start covers it
     if (has_next) {
+      // the reuse flag of the slot: same2[i-1] = (u_old(i-1) == u_old(i+1)), copied with this step's df / u_old (the
+      // slot of step i+1 already holds the order of step ni = i-1 then: the order is a function of u_old alone,
+      // k_pyr_order, and by induction every slot holds the order of the last step assigned to it)
+      const int same = *reinterpret_cast<const volatile int32_t *>(sds + sd_dfuo_offset<M>() +
+                                                                   (threadIdx.x >> 6) * sd_dfuo_stride<M>() + 16 * M);
       sd_issue_pipe<M>(raw, rs, slot + ((ni + 1) & 1) * L, ncp, (unsigned)((ni + 1) % NB) * bufb,
                        r0b + (unsigned)(ni + 1) * rowb, rowb);
-#ifdef SDT_TL_ISSUE  // timeline diagnostic: point 7 = the next row's loads issued (else: this row's loads consumed)
-      SD_TL_AT(g0, i, nt, 7);
-#endif
-      // the sphere order of step ni into the slot of step i+1 -- unless u_old(ni) = u_old(i+1): the order is a function of
-      // u_old alone (k_pyr_order), so the slot already holds it (by induction, every slot holds the order of the last
-      // step assigned to it)
-      if (ni != i && !(SDT_PERM_SKIP && sd_same_uold<M>(uoa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + i + 1) * M)))
+      if (ni != i && !(SDT_PERM_SKIP && same))
         sd_perm_dma_asm<M, (SDT_PRED && SDT_SLAB)>(pk + (size_t)ni * L, slot + (ni & 1) * L);
-      sd_dfuo_dma<M>(dfa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + ni) * M, sds);
+      sd_dfuo_dma<M>(dfa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + ni) * M,
+                     ni >= 1 ? sm + (size_t)k * nt + ni - 1 : nullptr, sds);
     }
+    SD_TL_AT(g0, i, nt, 4);
+  }
+  // late in the row, before the barrier after the winners: this wave's stores of the previous row have landed (they
+  // have had the whole row: no wait), so after that barrier the previous row can be published
+  __device__ __forceinline__ void late_drain() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     SD_TL_AT(g0, i, nt, 5);
+  }
+  __device__ __forceinline__ void publish() {
+    if (threadIdx.x == 0 && pcp >= 0)
+      __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pcp = cp;
+    pi = i;
   }
 };
 
@@ -1597,7 +1557,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
                                                               size_t uu_stride_k, int32_t *__restrict__ counters,
                                                               int32_t *flags, int nwg, unsigned spin_limit,
                                                               const double *__restrict__ df_all,
-                                                              const double *__restrict__ uo_all) {
+                                                              const double *__restrict__ uo_all,
+                                                              const int32_t *__restrict__ same2) {
   constexpr int L = 1 << (3 * M);
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
@@ -1621,11 +1582,10 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   h.dk = done + k * R, h.lk = loaded + k * R, h.err = err;
   h.pk = perm_all + (size_t)k * nt * L, h.slot = slot;
   h.rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(h.r0b + (unsigned)nt * h.rowb), 0x00020000);
-  h.dfa = df_all, h.uoa = uo_all, h.sds = sds, h.sh = &sh;
+  h.dfa = df_all, h.uoa = uo_all, h.sm = same2, h.sds = sds, h.sh = &sh;
   h.pcp = -1, h.pi = 0;
   if (tid == 0) {
     sh.stop = 0;
-    sh.arrive = 0;
     sh.cnt[0] = sh.cnt[1] = sh.cnt[2] = 0;
   }
   if (tid < SD_PRED_ROWS) {  // no predicted scale yet (the prologue's barrier orders these before every use)
@@ -1636,7 +1596,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   // written by an earlier launch)
   sd_perm_dma_asm<M>(h.pk + (size_t)(nt - 1) * L, pslot(nt - 1));
   sd_perm_dma_asm<M>(h.pk + (size_t)(nt - 2) * L, pslot(nt - 2));
-  sd_dfuo_dma<M>(df_all + ((size_t)k * nt + nt - 2) * M, uo_all + ((size_t)k * nt + nt - 2) * M, sds);
+  sd_dfuo_dma<M>(df_all + ((size_t)k * nt + nt - 2) * M, uo_all + ((size_t)k * nt + nt - 2) * M,
+                 nt >= 3 ? same2 + (size_t)k * nt + nt - 3 : nullptr, sds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   sd_bar();
   sd_issue_pipe<M>(h.raw, h.rs, pslot(nt - 1), lo, (unsigned)((nt - 1) % NB) * h.bufb, h.r0b + (unsigned)(nt - 1) * h.rowb,
@@ -1718,18 +1679,21 @@ hipError_t launch_sdt_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &
 }
 
 hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
-                          const uint32_t *perm, double *S, size_t kstride, int NB, uint16_t *UU, size_t uu_stride_k,
-                          int32_t *counters, int32_t *flags, int nwg, unsigned spin_limit, size_t lds) {
+                          const uint32_t *perm, const int32_t *same2, double *S, size_t kstride, int NB, uint16_t *UU,
+                          size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, unsigned spin_limit,
+                          size_t lds) {
   if (!sdt_supported(G)) return hipErrorInvalidValue;
-  // cooperative launch: the runtime checks at launch time that every workgroup can be resident at once (the
-  // row hand-off spins on other workgroups), and refuses the launch otherwise (hipErrorCooperativeLaunchTooLarge)
+  // every workgroup must be resident at once (the row hand-off spins on other workgroups): the caller sizes the grid
+  // to the CUs x resident workgroups per CU (sdt_run_blocks_per_cu); a dependency wait that times out anyway (another
+  // process's kernels holding CUs) sets the error word and the host redoes the DP per step.  An ordinary launch, not a
+  // cooperative one: a cooperative launch leaves the HIP runtime cooperative-queue state that it tears down at process
+  // exit, which crashed every rocprofv3 run of round 3 (profiles/round4_exit_probe.txt)
   void *args[] = {(void *)&P,     (void *)&Lv,       (void *)&G,         (void *)&perm,
                   (void *)&S,     (void *)&kstride,  (void *)&NB,        (void *)&UU,
                   (void *)&uu_stride_k, (void *)&counters, (void *)&flags, (void *)&nwg, (void *)&spin_limit,
-                  (void *)&P.df,  (void *)&P.uold};
-  if (G.M == 4)
-    return hipLaunchCooperativeKernel((const void *)k_sdt_run<4>, dim3(nwg), dim3(512), args, (unsigned)lds, s);
-  return hipLaunchCooperativeKernel((const void *)k_sdt_run<3>, dim3(nwg), dim3(64), args, (unsigned)lds, s);
+                  (void *)&P.df,  (void *)&P.uold, (void *)&same2};
+  if (G.M == 4) return hipLaunchKernel((const void *)k_sdt_run<4>, dim3(nwg), dim3(512), args, lds, s);
+  return hipLaunchKernel((const void *)k_sdt_run<3>, dim3(nwg), dim3(64), args, lds, s);
 }
 
 int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds) {

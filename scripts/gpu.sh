@@ -10,6 +10,7 @@
 #   pmc:c1+c2[:args]   ONE rocprofv3 --pmc pass (counters joined by +) over bench.py args -> pmc_<c1>/
 #   py:script[,args]   python scripts/<script> args (probes, A/B harnesses)
 #   exe:path[,args]    a binary built in this container (e.g. scripts/ubench/pass_occ)
+#   with:VAR=value     export VAR for the steps that follow (e.g. with:MIOC_LIB=<a variant build>)
 #   pyprof:script[,args]  rocprofv3 --kernel-trace --stats over python scripts/<script> args -> pyprof/
 set -o pipefail
 export TMPDIR=/tmp
@@ -56,6 +57,8 @@ for step in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/pyprof$n" -o prof --output-format csv \
         -- python3 scripts/$args > "$log" 2>&1
       rc=$?; tail -5 "$log"; find "$O/pyprof$n" -name "*kernel_stats.csv" ;;
+    with)
+      export "$rest"; echo "exported $rest"; rc=0 ;;
     exe)
       timeout -k 10 300 $args > "$log" 2>&1
       rc=$?; tail -40 "$log" ;;

@@ -1,7 +1,8 @@
 """Timeline of the pipelined persistent separable-transform kernel (diagnostic build libmioc_stamps_tl.so, `make
 stamps_tl`): for every row and the 64 steps from nt/2 down, s_memrealtime (100 MHz) at 8 points of the row body:
-0 start, 1 loads consumed, 2 mid point, 3 previous row drained, 4 next row's inputs ready, 5 next row's loads issued,
-6 stores issued.  Prints the phase durations, the step period and the pipeline skew between neighbouring rows.
+0 start, 7 loads taken, 1 dependency polls issued (after the first barrier; SDT_PRED builds: after the stamps), 2 go()
+(the first barrier passed), 3 polls matched, 4 next row's loads and copies issued, 5 previous row's stores drained (late,
+before the winners' barrier), 6 stores issued.  Prints the phase durations, the step period and the pipeline skew between neighbouring rows.
 Usage: python scripts/probe_sdt_timeline.py [nt] [NB]  [save.npy] [--lib another timeline build]
 (SDT_PRED builds: point 1 is the row's poll issue, right after its loads are taken.)"""
 import ctypes
@@ -56,8 +57,8 @@ rows = np.arange(1, R)  # row 0 has no workgroup
 steps = np.arange(2, 62)
 T = tl[rows][:, steps, :]
 ok = np.all(T[:, :, :8] > 0, axis=2)
-names = ["loads consumed + reductions (0->1)", "stamp + passes (1->2)", "drain previous row (2->3)",
-         "poll next inputs (3->4)", "issue next loads (4->5)", "winners + scans + stores (5->6)"]
+names = ["row start -> polls issued (0->1)", "polls issued -> go (1->2)", "poll wait at go (2->3)",
+         "issue next loads + copies (3->4)", "-> late drain done (4->5)", "list barrier, scans, stores (5->6)"]
 for q, nm in enumerate(names):
     d = (T[:, :, q + 1] - T[:, :, q])[ok]
     print(f"{nm:36s} median {np.median(d):6.3f}  p10 {np.percentile(d, 10):6.3f}  p90 {np.percentile(d, 90):6.3f} us")
@@ -72,7 +73,7 @@ print(f"stores issued -> next row start: median {np.median(rest):.3f} us")
 skew = T[1:, :, 0] - T[:-1, :, 0]  # row c starts step i this long after row c-1
 print(f"skew row c vs row c-1 (same step start): median {np.median(skew):.3f}  p10 {np.percentile(skew, 10):.3f}  "
       f"p90 {np.percentile(skew, 90):.3f} us; total over rows 1..{R - 1}: {np.median(T[-1, :, 0] - T[0, :, 0]):.1f} us")
-by_row = np.median(T[:, :, 4] - T[:, :, 3], axis=1)
+by_row = np.median(T[:, :, 3] - T[:, :, 2], axis=1)
 print("poll wait by row (median, every 16th row):", [round(float(x), 3) for x in by_row[::16]])
-ld = np.median(T[:, :, 1] - T[:, :, 0], axis=1)
+ld = np.median(T[:, :, 7] - T[:, :, 0], axis=1)
 print("load wait by row (median, every 16th row):", [round(float(x), 3) for x in ld[::16]])
