@@ -103,7 +103,7 @@ void free_all(mioc_ctx *ctx) {
                   ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
                   ctx->pinf.kabs, ctx->pinf.ftab, ctx->pinf.fseg, ctx->pinf.fneed,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
-                  ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm, ctx->d_same2,
+                  ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm, ctx->d_same2, ctx->d_strad,
                   ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own, ctx->d_ode_state};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -318,11 +318,13 @@ int run_bellman(mioc_ctx *ctx) {
     if (rc) return rc;
     rc = grow(ctx, &ctx->d_perm, &ctx->perm_cap, K * nt * L * sizeof(uint32_t), "sphere orders");
     if (!rc) rc = grow(ctx, &ctx->d_same2, &ctx->same2_cap, K * nt * sizeof(int32_t), "sphere-order reuse flags");
+    const bool slab = algo == MIOC_ALGO_SEPARABLE && sdt_slab_shift(ctx->pyr) > 0;
+    if (!rc && slab) rc = grow(ctx, &ctx->d_strad, &ctx->strad_cap, K * nt * 8 * 32 * sizeof(uint16_t), "seam lists");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
     double *term = persist ? ctx->d_stage + ((nt - 1) % nbuf) * s_stride : st[(nt - 1) & 1];
     HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm,
-                                  algo == MIOC_ALGO_SEPARABLE ? sdt_slab_shift(ctx->pyr) : 0, ctx->d_same2));
+                                  slab ? sdt_slab_shift(ctx->pyr) : 0, ctx->d_same2, slab ? ctx->d_strad : nullptr));
     HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, term, ks));
     if (algo == MIOC_ALGO_SEPARABLE && persist) {
       // the whole DP as one persistent launch: rows handed between resident workgroups by flags
@@ -330,8 +332,8 @@ int run_bellman(mioc_ctx *ctx) {
                                    (size_t)nbuf * s_stride, (uint16_t *)ctx->d_U, uu_stride_k));
       HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, runflag_bytes, ctx->stream));
       ev_begin(ctx, 0, "k_sdt_run");
-      const hipError_t le = launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_same2, ctx->d_stage, ks,
-                                           nbuf,
+      const hipError_t le = launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_same2, ctx->d_strad,
+                                           ctx->d_stage, ks, nbuf,
                                            (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags, nwg,
                                            ctx->spin_limit, run_lds);
       if (le == hipErrorCooperativeLaunchTooLarge) {  // (kept for a grid the runtime refuses): one launch per step

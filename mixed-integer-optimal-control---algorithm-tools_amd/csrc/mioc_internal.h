@@ -106,9 +106,10 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
 
 // ---- L1-ball pyramid (mioc_pyramid.hip) + staging-layout backtrack (mioc_generic.hip) -------------
 // slab_shift: 0 = sphere order (pyramid); sdt_slab_shift(G) for the separable transform (slab-major, see k_pyr_order)
-// same2 (nullable): [K][nt] int32, u_old(s) == u_old(s + 2) bit for bit (0 for s >= nt - 2)
+// same2 (nullable): [K][nt] int32, u_old(s) == u_old(s + 2) bit for bit (0 for s >= nt - 2); strad (nullable, slab
+// mode): [K][nt][8 slabs][32] uint16, the in-slab offsets of the second elements of seam-straddling position pairs
 hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int slab_shift,
-                            int32_t *same2 = nullptr);
+                            int32_t *same2 = nullptr, uint16_t *strad = nullptr);
 hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm, double *S,
                                size_t s_stride);
 hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
@@ -130,7 +131,8 @@ hipError_t launch_sdt_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &
                            size_t uu_stride_k);
 // same2[k][s] = (u_old(s) == u_old(s + 2)), written by launch_pyr_order: the persistent driver's sphere-order reuse
 hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
-                          const uint32_t *perm, const int32_t *same2, double *S, size_t kstride, int NB, uint16_t *UU,
+                          const uint32_t *perm, const int32_t *same2, const uint16_t *strad, double *S, size_t kstride,
+                          int NB, uint16_t *UU,
                           size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, unsigned spin_limit,
                           size_t lds);
 int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds);
@@ -295,6 +297,8 @@ struct mioc_ctx {
   uint32_t *d_perm = nullptr;      // [K][nt][L] sphere order of u_old(i): rank | (L1 distance << 16)
   int32_t *d_same2 = nullptr;      // [K][nt] u_old(i) == u_old(i+2) (the persistent separable driver's order reuse)
   size_t same2_cap = 0;
+  uint16_t *d_strad = nullptr;     // [K][nt][8][32] seam-straddling pairs per slab (slab-major sphere orders)
+  size_t strad_cap = 0;
   size_t perm_cap = 0;
   bool opt_persist = true;         // separable transform: one persistent launch (MIOC_OPT_PERSIST)
   bool force_steps = false;        // redo of a persistent DP whose waits timed out: per-step launches

@@ -824,7 +824,7 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
 // j >> slab_shift (the slab a row workgroup's wave owns), then by sphere, then ascending; every slab is one contiguous
 // block of L/8 positions, so the wave that owns a slab loads exactly its slab's sources (mioc_sdt.hip).
 __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all, int slab_shift,
-                                                   int32_t *same2) {
+                                                   int32_t *same2, uint16_t *strad) {
   constexpr int NK = 8 * 64;        // bucket keys: slab << 6 | min(distance, 63)
   __shared__ int start[NK];         // the next free position of each bucket
   __shared__ int wcnt[4][NK + 1];   // ranks of the current chunk per wave and bucket (NK: the inactive lanes)
@@ -892,11 +892,26 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
     if (tid == 0) wcnt[0][NK] = wcnt[1][NK] = wcnt[2][NK] = wcnt[3][NK] = 0;
     __syncthreads();
   }
+  // slab mode, strad (the persistent separable driver at 8^4): per slab of L/8 positions, the in-slab offsets p of the
+  // odd positions whose distance differs from position p-1's -- the second elements of the 16-byte position pairs that
+  // straddle a sphere seam (at most 21 per slab of the 8^4 grid: 22 distances), 0xFFFF-padded to 32
+  if (slab_shift && strad) {
+    uint16_t *st = strad + ((size_t)k * P.nt + i) * 8 * 32;
+    const int SL = L / 8;
+    for (int e = tid; e < 8 * 32; e += blockDim.x) st[e] = 0xFFFFu;
+    if (tid < 8) start[tid] = 0;  // per-slab counts
+    __syncthreads();
+    for (int p = 2 * tid + 1; p < L; p += 2 * blockDim.x)
+      if ((perm[p] >> 16) != (perm[p - 1] >> 16)) {
+        const int sl = p / SL, e = atomicAdd(&start[sl], 1);
+        if (e < 32) st[sl * 32 + e] = (uint16_t)(p - sl * SL);
+      }
+  }
 }
 
 hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int slab_shift,
-                            int32_t *same2) {
-  hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm, slab_shift, same2);
+                            int32_t *same2, uint16_t *strad) {
+  hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm, slab_shift, same2, strad);
   return hipGetLastError();
 }
 

@@ -66,10 +66,20 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_PRED
 #define SDT_PRED 0                       // persistent driver: stamp with a per-row predicted scale (see sdt_body)
 #endif
+#ifndef SDT_STRAD
+#define SDT_STRAD 1                      // SDT_SLAB: per-slab seam lists instead of one straddle load per pair (SdRaw)
+#endif
 #ifndef SDT_SLAB
 #define SDT_SLAB 0                       // slab-major sphere order: a wave loads and stamps only its own slab (sdt_body)
 #endif
 constexpr int SD_PRED_ROWS = 64;         // rows of a workgroup's chunk that keep a predicted scale (the others: none)
+constexpr int SD_STRAD_N = 32;           // straddle list entries per slab (a slab of the 8^4 grid has <= 21 spheres' seams)
+// SDT_SLAB at M = 4: the position pairs that straddle a sphere seam get their second element from one straddle load per
+// lane (a per-slab list, k_pyr_order) instead of one masked 8-byte load per pair and lane (SdRaw)
+template <int M>
+__host__ __device__ constexpr bool sd_strad() {
+  return SDT_PRED && SDT_SLAB && SDT_STRAD && M == 4;
+}
 
 // Diagnostic build only (make stamps -> libmioc_stamps.so): per-workgroup phase clocks of the last launch.
 #if defined(MIOC_STAMPS) && !defined(MIOC_STAMPS_TL)
@@ -419,8 +429,12 @@ __host__ __device__ constexpr size_t sd_dfuo_stride() {
   return (2 * M + 2) * sizeof(double);
 }
 template <int M>
-__host__ __device__ constexpr size_t sd_dfuo_offset() {  // then df(:, i), u_old(:, i), a flag word per wave (persistent)
+__host__ __device__ constexpr size_t sd_strad_offset() {  // then the two slots' straddle lists (8 slabs x SD_STRAD_N)
   return sd_slot_offset<M>() + 2 * ((size_t)1 << (3 * M)) * sizeof(uint32_t);
+}
+template <int M>
+__host__ __device__ constexpr size_t sd_dfuo_offset() {  // then df(:, i), u_old(:, i), a flag word per wave (persistent)
+  return sd_strad_offset<M>() + 2 * 8 * SD_STRAD_N * sizeof(uint16_t);
 }
 template <int M>
 __host__ __device__ constexpr size_t sd_out_offset() {  // then the row's outputs (natural order), SDT_WAVE_LOCAL
@@ -477,6 +491,8 @@ __device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restr
 //            sphere order and df / u_old).  A timed-out wait sets sh.stop, which the driver reads after the row.
 //   prow   : (persistent driver, SDT_PRED) this row's predicted Ψ range [lo, hi] in LDS, refreshed here on a miss;
 //            null: none
+//   smask, srank, xs: (sd_strad) the pairs q whose second element straddles a sphere seam (bit 3q+2 of smask: not
+//            this lane's to store), and this lane's straddle element (rank srank, value xs; srank < 0: none)
 // Returns 1 if the row is all +Inf (no target in the trust region or no finite source), else 0.
 // Writes row c' of S_i (sphere order of u_old(i)) and of UU_i: exactly five 16-byte vector-memory stores per
 // thread on every path, the last vector-memory instructions of the row (the persistent driver's counted wait
@@ -488,7 +504,8 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
                                          const uint32_t *pout,
                                          double *Sout, uint16_t *UU, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
                                          unsigned char *sds, Hooks &h, const double *__restrict__ df_all,
-                                         const double *__restrict__ uo_all, double *prow) {
+                                         const double *__restrict__ uo_all, double *prow, unsigned smask = 0,
+                                         int srank = -1, double xs = 0.0) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
   double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
   double *dtv = psi + L;                                // [L] transform values (swizzled)
@@ -636,12 +653,27 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       for (int hh = 0; hh < 2; ++hh) {
         const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
         const double x = v[2 * q + hh];
-        psi[j] = x;
         const bool fin = x < INFINITY;
         nv += __popcll(__ballot(fin)) << 16;
         bad |= fin && !(x >= plo && x <= phi);
-        dtv[sd_swz(j)] = fin ? stamp(x, j) : INFINITY;
+        const double V = fin ? stamp(x, j) : INFINITY;
+        if (!(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) {  // (a straddling second element: its loader's)
+          psi[j] = x;
+          dtv[sd_swz(j)] = V;
+        }
       }
+    if constexpr (sd_strad<M>()) {  // this lane's straddle element
+      const int js = srank & 0xFFFF;
+      const double x = (srank & 0x10000) ? INFINITY : xs;
+      const bool fin = srank >= 0 && x < INFINITY;
+      nv += __popcll(__ballot(fin)) << 16;
+      bad |= fin && !(x >= plo && x <= phi);
+      const double V = fin ? stamp(x, js) : INFINITY;
+      if (srank >= 0) {
+        psi[js] = x;
+        dtv[sd_swz(js)] = V;
+      }
+    }
     const bool wbad = __ballot(bad) != 0;
     if (lane == 0) {
       sh.rnv[w] = nv;
@@ -1202,6 +1234,22 @@ __device__ __forceinline__ void sd_dfuo_dma(const double *df, const double *uo, 
   }
 }
 
+// (sd_strad) this wave's slab of a step's seam list (SD_STRAD_N uint16 = 64 bytes) into the slot's list in LDS:
+// lanes 0..15 move one dword each (LDS-DMA, inline asm as sd_perm_dma_asm); only this wave reads its slab's list
+__device__ __forceinline__ void sd_strad_dma(const uint16_t *src, uint16_t *slot) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane < SD_STRAD_N / 2) {
+    const char *g = (const char *)(src + wave * SD_STRAD_N) + 4 * lane;
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)(slot + wave * SD_STRAD_N)));
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(m0)
+                 : "memory");
+  }
+}
+
 // One launch per step: one workgroup per (source row c', subproblem k).
 template <int M>
 __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, LevelsDev Lv, PyrGeom G, int i,
@@ -1359,18 +1407,30 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_row0(ProblemDev P, Lev
 // next row's start).
 struct SdRaw {
   sd_u32x4 a[4];
-  sd_u32x2 b[4];
+  sd_u32x2 b[4];  // (not sd_strad) the second elements of straddling pairs
+  sd_u32x2 sv;    // (sd_strad) this lane's straddle element, at position sp of its slab: rank srank
+  int srank;      // -1: no straddle element for this lane; bit 16: its source row is below 0 (+Inf)
   uint2 e[4];     // the sphere-order entries the offsets came from (the row body's `ein`)
   unsigned mask;  // per pair q: bit 3q the first element has no source row, 3q+1 the second, 3q+2 it straddles
 };
+// sl: (sd_strad) the seam list of the slot `pin` (SD_STRAD_N in-slab offsets per slab, 0xFFFF: none)
 template <int M>
-__device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t rs, const uint32_t *pin, int cp,
-                                              unsigned boff, unsigned r0, const unsigned rowb) {
-  constexpr int L = 1 << (3 * M), T = L / 8;
+__device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t rs, const uint32_t *pin,
+                                              const uint16_t *sl, int cp, unsigned boff, unsigned r0,
+                                              const unsigned rowb) {
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
   const int tid = threadIdx.x;
   uint2 e[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) e[q] = *reinterpret_cast<const uint2 *>(pin + sd_p2<M>(tid, q));  // reads first
+  // sd_strad: lane l < SD_STRAD_N of wave w takes the l-th seam of slab w (its rank and distance from the slot)
+  unsigned sp = 0xFFFFu;
+  uint32_t se = 0;
+  if constexpr (sd_strad<M>()) {
+    const int lane = tid & 63, wv = tid >> 6;
+    sp = lane < SD_STRAD_N ? sl[wv * SD_STRAD_N + lane] : 0xFFFFu;
+    se = pin[wv * (L / NW) + (sp & (L / NW - 1))];
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) w.e[q] = e[q];
   // an offset beyond the resource's range drops the access (the load returns 0 without touching memory): rows
@@ -1391,23 +1451,41 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa[q], 0, 16);
+    if constexpr (!sd_strad<M>()) {
 #ifndef SDT_EXP_NOB64  // timing experiment only (wrong results): without the straddle loads
-    w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob[q], 0, 16);
+      w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob[q], 0, 16);
 #else
-    w.b[q] = sd_u32x2{0u, 0u};
+      w.b[q] = sd_u32x2{0u, 0u};
 #endif
+    }
+  }
+  if constexpr (sd_strad<M>()) {
+    const int P = (tid >> 6) * (L / NW) + (int)(sp & (L / NW - 1));
+    const int rsr = cp - (int)(se >> 16);
+    const bool has = sp != 0xFFFFu;
+    w.sv = __builtin_amdgcn_raw_buffer_load_b64(
+        rs, !has || rsr < 0 ? OOB : rsr >= 1 ? boff + (unsigned)rsr * rowb + (unsigned)P * 8u : r0 + (unsigned)P * 8u, 0,
+        16);
+    w.srank = has ? (int)(se & 0xFFFFu) | (rsr < 0 ? 0x10000 : 0) : -1;
   }
   w.mask = mask;
 }
+// this lane's eight values; (sd_strad) the second element of a straddling pair is +Inf here -- its value comes with
+// the lane that loaded it as a straddle element, and the row body does not store it (the `skip` bits of the mask)
+template <int M>
 __device__ __forceinline__ void sd_take(double (&v)[8], const SdRaw &w) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const unsigned m = w.mask >> (3 * q);
     const double a0 = __hiloint2double((int)w.a[q].y, (int)w.a[q].x);
     const double a1 = __hiloint2double((int)w.a[q].w, (int)w.a[q].z);
-    const double b1 = __hiloint2double((int)w.b[q].y, (int)w.b[q].x);
     v[2 * q] = (m & 1) ? INFINITY : a0;
-    v[2 * q + 1] = (m & 2) ? INFINITY : (m & 4) ? b1 : a1;
+    if constexpr (sd_strad<M>()) {
+      v[2 * q + 1] = (m & 6) ? INFINITY : a1;
+    } else {
+      const double b1 = __hiloint2double((int)w.b[q].y, (int)w.b[q].x);
+      v[2 * q + 1] = (m & 2) ? INFINITY : (m & 4) ? b1 : a1;
+    }
   }
 }
 
@@ -1450,6 +1528,8 @@ struct SdPipe {
   __amdgpu_buffer_rsrc_t rs;
   const double *dfa, *uoa;
   const int32_t *sm;  // same2 (k_pyr_order): u_old(s) == u_old(s + 2) per step s
+  const uint16_t *sk;  // (sd_strad) this subproblem's seam lists, [nt][8][SD_STRAD_N]
+  uint16_t *sslot;     // (sd_strad) the two slots' seam lists in LDS
   unsigned char *sds;
   SdtShared<(1 << (3 * M - 3)) / 64> *sh;
   // carried from row to row: the previous row (its `done` is published at this row's go()), this wave's polls, the
@@ -1527,10 +1607,12 @@ struct SdPipe {
       // k_pyr_order, and by induction every slot holds the order of the last step assigned to it)
       const int same = *reinterpret_cast<const volatile int32_t *>(sds + sd_dfuo_offset<M>() +
                                                                    (threadIdx.x >> 6) * sd_dfuo_stride<M>() + 16 * M);
-      sd_issue_pipe<M>(raw, rs, slot + ((ni + 1) & 1) * L, ncp, (unsigned)((ni + 1) % NB) * bufb,
-                       r0b + (unsigned)(ni + 1) * rowb, rowb);
-      if (ni != i && !(SDT_PERM_SKIP && same))
+      sd_issue_pipe<M>(raw, rs, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N, ncp,
+                       (unsigned)((ni + 1) % NB) * bufb, r0b + (unsigned)(ni + 1) * rowb, rowb);
+      if (ni != i && !(SDT_PERM_SKIP && same)) {
         sd_perm_dma_asm<M, (SDT_PRED && SDT_SLAB)>(pk + (size_t)ni * L, slot + (ni & 1) * L);
+        if constexpr (sd_strad<M>()) sd_strad_dma(sk + (size_t)ni * 8 * SD_STRAD_N, sslot + (ni & 1) * 8 * SD_STRAD_N);
+      }
       sd_dfuo_dma<M>(dfa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + ni) * M,
                      ni >= 1 ? sm + (size_t)k * nt + ni - 1 : nullptr, sds);
     }
@@ -1558,7 +1640,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
                                                               int32_t *flags, int nwg, unsigned spin_limit,
                                                               const double *__restrict__ df_all,
                                                               const double *__restrict__ uo_all,
-                                                              const int32_t *__restrict__ same2) {
+                                                              const int32_t *__restrict__ same2,
+                                                              const uint16_t *__restrict__ strad) {
   constexpr int L = 1 << (3 * M);
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
@@ -1583,6 +1666,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   h.pk = perm_all + (size_t)k * nt * L, h.slot = slot;
   h.rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(h.r0b + (unsigned)nt * h.rowb), 0x00020000);
   h.dfa = df_all, h.uoa = uo_all, h.sm = same2, h.sds = sds, h.sh = &sh;
+  h.sk = strad ? strad + (size_t)k * nt * 8 * SD_STRAD_N : nullptr;
+  h.sslot = reinterpret_cast<uint16_t *>(sds + sd_strad_offset<M>());
   h.pcp = -1, h.pi = 0;
   if (tid == 0) {
     sh.stop = 0;
@@ -1596,11 +1681,16 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   // written by an earlier launch)
   sd_perm_dma_asm<M>(h.pk + (size_t)(nt - 1) * L, pslot(nt - 1));
   sd_perm_dma_asm<M>(h.pk + (size_t)(nt - 2) * L, pslot(nt - 2));
+  if constexpr (sd_strad<M>()) {
+    sd_strad_dma(h.sk + (size_t)(nt - 1) * 8 * SD_STRAD_N, h.sslot + ((nt - 1) & 1) * 8 * SD_STRAD_N);
+    sd_strad_dma(h.sk + (size_t)(nt - 2) * 8 * SD_STRAD_N, h.sslot + ((nt - 2) & 1) * 8 * SD_STRAD_N);
+  }
   sd_dfuo_dma<M>(df_all + ((size_t)k * nt + nt - 2) * M, uo_all + ((size_t)k * nt + nt - 2) * M,
                  nt >= 3 ? same2 + (size_t)k * nt + nt - 3 : nullptr, sds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   sd_bar();
-  sd_issue_pipe<M>(h.raw, h.rs, pslot(nt - 1), lo, (unsigned)((nt - 1) % NB) * h.bufb, h.r0b + (unsigned)(nt - 1) * h.rowb,
+  sd_issue_pipe<M>(h.raw, h.rs, pslot(nt - 1), h.sslot + ((nt - 1) & 1) * 8 * SD_STRAD_N, lo,
+                   (unsigned)((nt - 1) % NB) * h.bufb, h.r0b + (unsigned)(nt - 1) * h.rowb,
                    h.rowb);
   // a wait the compiler sees (vmcnt(0), other counters untouched): entering the loop with these loads pending would
   // make it assume, at the loop head, that nothing younger can be outstanding, and wait for every store there
@@ -1622,7 +1712,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       // the memory clobber keeps the LDS reads of what the DMA wrote below this point
       asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       double v[8];
-      sd_take(v, h.raw);
+      sd_take<M>(v, h.raw);
 #ifndef SDT_TL_ISSUE
       SD_TL(7);
 #endif
@@ -1636,10 +1726,12 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       uint2 ein[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) ein[q] = h.raw.e[q];
+      const double xs = __hiloint2double((int)h.raw.sv.y, (int)h.raw.sv.x);
       status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, ein, pslot(i + 1), pslot(i),
                                  reg + (size_t)(i % NB) * R * L + (size_t)cp * L,
                                  UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L, sh,
-                                 sds, h, df_all, uo_all, cp - lo < SD_PRED_ROWS ? sh.pred[cp - lo] : nullptr);
+                                 sds, h, df_all, uo_all, cp - lo < SD_PRED_ROWS ? sh.pred[cp - lo] : nullptr,
+                                 h.raw.mask, h.raw.srank, xs);
       SD_TL(6);
       stop = sh.stop != 0;  // written before a barrier the row has passed since (every path has one)
     }
@@ -1679,7 +1771,8 @@ hipError_t launch_sdt_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &
 }
 
 hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
-                          const uint32_t *perm, const int32_t *same2, double *S, size_t kstride, int NB, uint16_t *UU,
+                          const uint32_t *perm, const int32_t *same2, const uint16_t *strad, double *S, size_t kstride,
+                          int NB, uint16_t *UU,
                           size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, unsigned spin_limit,
                           size_t lds) {
   if (!sdt_supported(G)) return hipErrorInvalidValue;
@@ -1691,7 +1784,7 @@ hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &L
   void *args[] = {(void *)&P,     (void *)&Lv,       (void *)&G,         (void *)&perm,
                   (void *)&S,     (void *)&kstride,  (void *)&NB,        (void *)&UU,
                   (void *)&uu_stride_k, (void *)&counters, (void *)&flags, (void *)&nwg, (void *)&spin_limit,
-                  (void *)&P.df,  (void *)&P.uold, (void *)&same2};
+                  (void *)&P.df,  (void *)&P.uold, (void *)&same2, (void *)&strad};
   if (G.M == 4) return hipLaunchKernel((const void *)k_sdt_run<4>, dim3(nwg), dim3(512), args, lds, s);
   return hipLaunchKernel((const void *)k_sdt_run<3>, dim3(nwg), dim3(64), args, lds, s);
 }
