@@ -297,11 +297,14 @@ int run_bellman(mioc_ctx *ctx) {
     }
     // persistent layout: per subproblem NB staging buffers of (B+1)·L, then row 0 of every step (nt·L), one region
     // addressed by one buffer resource (< 4 GiB); per-step layout: two buffers of K blocks of (B+1)·L
-    const int nbuf = persist ? ctx->opt_nb : 2;
+    int nbuf = persist ? ctx->opt_nb : 2;
+    // one buffer resource addresses a subproblem's whole region (32-bit offsets): fewer buffers where it would not fit
+    while (persist && nbuf > 4 && ((size_t)nbuf * s_stride + nt * L) * sizeof(double) >= (1ull << 32)) nbuf /= 2;
     const size_t kstride = persist ? (size_t)nbuf * s_stride + nt * L : s_stride;
     if (persist && kstride * sizeof(double) >= (1ull << 32)) persist = false;  // (then also kstride = s_stride)
     const size_t ks = persist ? kstride : s_stride;
-    const size_t runflag_bytes = ((2 * K * (size_t)(ctx->B + 1) + 1) * sizeof(int32_t) + 15) / 16 * 16;
+    const size_t fw = (size_t)sdt_flag_words(ctx->pyr);
+    const size_t runflag_bytes = ((2 * K * (size_t)(ctx->B + 1) * fw + 1) * sizeof(int32_t) + 15) / 16 * 16;
     if (persist) {
       int rcf = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, runflag_bytes, "persistent row flags");
       if (!rcf) rcf = grow(ctx, &ctx->d_chain, &ctx->chain_cap, K * nt * sizeof(double), "row 0 chain");
@@ -347,7 +350,7 @@ int run_bellman(mioc_ctx *ctx) {
       }
       HIP_TRY(ctx, le);
       ev_end(ctx, 0, 1);
-      HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + 2 * K * (size_t)(ctx->B + 1), sizeof(int32_t),
+      HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + 2 * K * (size_t)(ctx->B + 1) * fw, sizeof(int32_t),
                                   hipMemcpyDeviceToHost, ctx->stream));
       ctx->run_pending = true;
     } else if (algo == MIOC_ALGO_SEPARABLE) {
@@ -671,7 +674,7 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
     return MIOC_OK;
   }
   if (option == MIOC_OPT_SDT_BUFFERS) {
-    if (value < 4 || value > kSdtMaxBuffers) return fail(ctx, MIOC_EINVAL, "staging buffers must be in [4, 64]");
+    if (value < 4 || value > kSdtMaxBuffers) return fail(ctx, MIOC_EINVAL, "staging buffers must be in [4, 192]");
     ctx->opt_nb = (int)value;
     return MIOC_OK;
   }

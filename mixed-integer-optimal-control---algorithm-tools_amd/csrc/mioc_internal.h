@@ -119,8 +119,10 @@ size_t pyr_lds_bytes(const PyrGeom &G);
 // separable L1 transform (mioc_sdt.hip): same staging layout, 8^M grids (M = 3, 4), beta > 0
 bool sdt_supported(const PyrGeom &G);
 int sdt_slab_shift(const PyrGeom &G);  // the sphere-order mode the separable transform's kernels were built for
+int sdt_flag_words(const PyrGeom &G);  // persistent driver: hand-off flags per row (one per wave under SDT_SLAB)
 size_t sdt_lds_bytes(const PyrGeom &G);
-constexpr int kSdtMaxBuffers = 64;  // persistent separable transform: staging buffers S_i, step i in buffer i % NB
+constexpr int kSdtMaxBuffers = 192;  // persistent separable transform: staging buffers S_i, step i in buffer i % NB
+constexpr int kSdtDefaultBuffers = 128;  // (C4: 128 x 8.4 MB + the 2.1 GB row-0 array, under the 4 GiB buffer range)
 hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
                            const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
                            size_t uu_stride_k, int32_t *counters);
@@ -308,7 +310,7 @@ struct mioc_ctx {
   size_t chain_cap = 0;
   unsigned spin_limit = 1u << 24;  // persistent DP: polls before a dependency wait gives up (MIOC_OPT_SPIN_LIMIT)
   size_t stage_kstride = 0;        // doubles between two subproblems' staging blocks in the last pyramid / sdt DP
-  int opt_nb = mioc::kSdtMaxBuffers;    // staging buffers of a persistent separable DP (MIOC_OPT_SDT_BUFFERS)
+  int opt_nb = mioc::kSdtDefaultBuffers;  // staging buffers of a persistent separable DP (MIOC_OPT_SDT_BUFFERS)
   const int32_t *gate = nullptr;   // device TRM control (mioc_trm_attach): the state block's gate word
   int32_t *h_trm_poll = nullptr;   // pinned: the gate and any-active words (mioc_trm_poll)
   int opt_fsep_seg = 0;            // fused separable DP: row segments (MIOC_OPT_FSEP_SEGMENTS)

@@ -76,6 +76,12 @@ constexpr int SD_PRED_ROWS = 64;         // rows of a workgroup's chunk that kee
 constexpr int SD_STRAD_N = 32;           // straddle list entries per slab (a slab of the 8^4 grid has <= 21 spheres' seams)
 // SDT_SLAB at M = 4: the position pairs that straddle a sphere seam get their second element from one straddle load per
 // lane (a per-slab list, k_pyr_order) instead of one masked 8-byte load per pair and lane (SdRaw)
+// hand-off flags per row: SDT_SLAB's row flow hands off per slab (wave w of a row reads and writes only slab w's
+// positions), so every wave has its own `done` / `loaded` flag; else one per row
+template <int M>
+__host__ __device__ constexpr int sd_flag_words() {
+  return SDT_PRED && SDT_SLAB ? (1 << (3 * M - 3)) / 64 : 1;
+}
 template <int M>
 __host__ __device__ constexpr bool sd_strad() {
   return SDT_PRED && SDT_SLAB && SDT_STRAD && M == 4;
@@ -686,8 +692,9 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       // row: the previous row's stores have long landed) and the pipeline hooks after it
       h.poll();  // this wave's dependency polls (about as long before go() as their round trip takes)
       wave_passes();
-      sd_bar();  // every wave's passes 0 .. M-2 and counts are in LDS; every wave has consumed its loads
-      h.go();    // publish `loaded`, check the polls, issue the next row's loads and copies
+      h.wave_done();  // this wave's stores of the previous row have landed: its slab of that row is done
+      h.go();         // its polls matched -> its slab of the next row's loads and of the sphere-order copy
+      sd_bar();       // every wave's passes 0 .. M-2 and counts are in LDS
     } else {
       sd_bar();  // Ψ by rank and the stamps of every wave are in LDS; every wave has consumed its loads
       // `v` and `pin` are dead from here on: the driver may reuse the latter
@@ -1165,6 +1172,7 @@ __device__ __forceinline__ void sdt_rowB(const ProblemDev &P, const LevelsDev &L
 // per-step driver: no pipeline hooks
 struct SdHooksNone {
   __device__ __forceinline__ void poll() {}
+  __device__ __forceinline__ void wave_done() {}
   __device__ __forceinline__ void early() {}
   __device__ __forceinline__ void go() {}
   __device__ __forceinline__ void late_drain() {}
@@ -1515,7 +1523,11 @@ __device__ __forceinline__ void sd_take(double (&v)[8], const SdRaw &w) {
 // The pipeline hooks of the persistent driver (the row body calls them, see sdt_body).
 template <int M>
 struct SdPipe {
-  static constexpr int L = 1 << (3 * M);
+  static constexpr int L = 1 << (3 * M), FW = sd_flag_words<M>();
+  static constexpr bool SLAB = SDT_PRED && SDT_SLAB;
+  // this wave's hand-off flag of row r (per slab under SDT_SLAB, else per row)
+  __device__ __forceinline__ int32_t *dflag(int r) const { return dk + r * FW + (FW > 1 ? (int)(threadIdx.x >> 6) : 0); }
+  __device__ __forceinline__ int32_t *lflag(int r) const { return lk + r * FW + (FW > 1 ? (int)(threadIdx.x >> 6) : 0); }
   // the current row (cp, step i) and the next one (ncp, step ni)
   int cp, i, ncp, ni;
   bool has_next;
@@ -1557,18 +1569,18 @@ struct SdPipe {
   }
   __device__ __forceinline__ void issue_polls() {
     const int tid = threadIdx.x, lane = tid & 63, s = lane < 32 ? lane + 1 : lane - 31;
-    fp = lk + cp;
+    fp = lflag(cp);
     need = INT32_MIN;
     if (lane < 32) {
       const int r = ncp - s;
       if (has_next && s <= 7 * M && r >= 1 && r < lo && nt - 2 - ni > 0) {
-        fp = dk + r;
+        fp = dflag(r);
         need = nt - 2 - ni;  // token(ni + 1)
       }
     } else {
       const int r = cp + s;
       if (s <= 7 * M && r <= B && r >= hi && nt - i - NB > 0) {
-        fp = lk + r;
+        fp = lflag(r);
         need = nt - i - NB;  // token(i + NB - 1)
       }
     }
@@ -1577,12 +1589,28 @@ struct SdPipe {
   // after the row's first barrier (every wave has consumed this row's loads): publish `loaded`; this wave waits until
   // its polls match (re-polling), then issues the next row's loads -- the measured-valid consumer form: the polling
   // wave loads only after its own poll matched
-  __device__ __forceinline__ void go() {
+  // SDT_SLAB, at the row's start: this wave has consumed its loads of this row -- its slab's `loaded` flag
+  __device__ __forceinline__ void consumed() {
+    if constexpr (SLAB)
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store(lflag(cp), nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // SDT_SLAB, mid-row: this wave's stores of the previous row have landed (its `loaded` store and its poll, younger,
+  // may be in flight) -- its slab's `done` flag for the previous row (the measured-valid form, per wave: the storing
+  // wave drains, then one lane of it stores the flag)
+  __device__ __forceinline__ void wave_done() {
     SD_TL_AT(g0, i, nt, 2);
+    if constexpr (SLAB) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if ((threadIdx.x & 63) == 0 && pcp >= 0)
+        __hip_atomic_store(dflag(pcp), nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __device__ __forceinline__ void go() {
+    if constexpr (!SLAB) SD_TL_AT(g0, i, nt, 2);
     const int tid = threadIdx.x;
     // evaluated before the flag store below: the compiler's wait for `val` would otherwise cover that store
     bool ready = __all(val >= need);
-    if (tid == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!SLAB && tid == 0) __hip_atomic_store(lflag(cp), nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     while (!ready) {
       if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
@@ -1621,12 +1649,12 @@ struct SdPipe {
   // late in the row, before the barrier after the winners: this wave's stores of the previous row have landed (they
   // have had the whole row: no wait), so after that barrier the previous row can be published
   __device__ __forceinline__ void late_drain() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (!SLAB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     SD_TL_AT(g0, i, nt, 5);
   }
   __device__ __forceinline__ void publish() {
-    if (threadIdx.x == 0 && pcp >= 0)
-      __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!SLAB && threadIdx.x == 0 && pcp >= 0)
+      __hip_atomic_store(dflag(pcp), nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     pcp = cp;
     pi = i;
   }
@@ -1646,7 +1674,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
   const int B = P.B, R = B + 1, nt = P.nt, tid = threadIdx.x;
-  int32_t *done = flags, *loaded = flags + P.K * R, *err = flags + 2 * P.K * R;
+  constexpr int FW = sd_flag_words<M>();
+  int32_t *done = flags, *loaded = flags + P.K * R * FW, *err = flags + 2 * P.K * R * FW;
   const int W = nwg / P.K;  // workgroups per subproblem (the host guarantees 1 <= W <= B)
   const int k = (int)blockIdx.x / W, wl = (int)blockIdx.x - k * W;
   if (k >= P.K) return;
@@ -1662,7 +1691,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   SdPipe<M> h;
   h.lo = lo, h.hi = hi, h.B = B, h.NB = NB, h.nt = nt, h.k = k, h.g0 = k * R + lo;
   h.spin_limit = spin_limit, h.rowb = (unsigned)L * 8u, h.bufb = (unsigned)R * h.rowb, h.r0b = (unsigned)NB * h.bufb;
-  h.dk = done + k * R, h.lk = loaded + k * R, h.err = err;
+  h.dk = done + (size_t)k * R * FW, h.lk = loaded + (size_t)k * R * FW, h.err = err;
   h.pk = perm_all + (size_t)k * nt * L, h.slot = slot;
   h.rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(h.r0b + (unsigned)nt * h.rowb), 0x00020000);
   h.dfa = df_all, h.uoa = uo_all, h.sm = same2, h.sds = sds, h.sh = &sh;
@@ -1713,6 +1742,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       double v[8];
       sd_take<M>(v, h.raw);
+      h.consumed();  // (SDT_SLAB) this wave's slab of the row's loads is in: its `loaded` flag
 #ifndef SDT_TL_ISSUE
       SD_TL(7);
 #endif
@@ -1746,6 +1776,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
 }
 
 int sdt_slab_shift(const PyrGeom &G) { return SDT_SLAB ? 3 * (G.M - 1) : 0; }
+int sdt_flag_words(const PyrGeom &G) { return G.M == 4 ? sd_flag_words<4>() : sd_flag_words<3>(); }
 
 bool sdt_supported(const PyrGeom &G) {
   if (G.M != 3 && G.M != 4) return false;

@@ -1,11 +1,14 @@
 """A/B timing of k_sdt_run (C4 inputs at full L and B, truncated nt) across library builds, each in its own process.
 Prints per library: µs per DP step (HIP events, best of REPS calls) and a digest of u / Φ* at three budgets and of
 the argmin tables of a few steps, which must agree across builds.
-Usage: python scripts/probe_sdt_ab.py NT LIB [LIB ...]"""
+Usage: python scripts/probe_sdt_ab.py NT LIB [LIB ...]   (SDT_NB=n: staging buffers)"""
 import hashlib, json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")
 REPS = 3
+
+
+NB = int(os.environ.get("SDT_NB", "0"))  # staging buffers (MIOC_OPT_SDT_BUFFERS), 0: the library default
 
 
 def one(nt, lib):
@@ -20,6 +23,8 @@ def one(nt, lib):
     with native.Context(0) as ctx:
         ctx.set_levels(lt); ctx.set_cost(1, cfg.beta)
         ctx.set_option(native.MIOC_OPT_TIMING, 1); ctx.set_option(native.MIOC_OPT_PERSIST, 1)
+        if NB:
+            ctx.set_option(native.MIOC_OPT_SDT_BUFFERS, NB)
         best = None
         for _ in range(REPS):
             ctx.reset_stats()
