@@ -322,12 +322,13 @@ int run_bellman(mioc_ctx *ctx) {
     rc = grow(ctx, &ctx->d_perm, &ctx->perm_cap, K * nt * L * sizeof(uint32_t), "sphere orders");
     if (!rc) rc = grow(ctx, &ctx->d_same2, &ctx->same2_cap, K * nt * sizeof(int32_t), "sphere-order reuse flags");
     const bool slab = algo == MIOC_ALGO_SEPARABLE && sdt_slab_shift(ctx->pyr) > 0;
-    if (!rc && slab) rc = grow(ctx, &ctx->d_strad, &ctx->strad_cap, K * nt * 8 * 32 * sizeof(uint16_t), "seam lists");
+    const bool seams = persist && sdt_seam_lists(ctx->pyr);
+    if (!rc && seams) rc = grow(ctx, &ctx->d_strad, &ctx->strad_cap, K * nt * 8 * 32 * sizeof(uint16_t), "seam lists");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
     double *term = persist ? ctx->d_stage + ((nt - 1) % nbuf) * s_stride : st[(nt - 1) & 1];
     HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm,
-                                  slab ? sdt_slab_shift(ctx->pyr) : 0, ctx->d_same2, slab ? ctx->d_strad : nullptr));
+                                  slab ? sdt_slab_shift(ctx->pyr) : 0, ctx->d_same2, seams ? ctx->d_strad : nullptr));
     HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, term, ks));
     if (algo == MIOC_ALGO_SEPARABLE && persist) {
       // the whole DP as one persistent launch: rows handed between resident workgroups by flags

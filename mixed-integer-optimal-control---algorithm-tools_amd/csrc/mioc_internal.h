@@ -118,6 +118,7 @@ hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &
 size_t pyr_lds_bytes(const PyrGeom &G);
 // separable L1 transform (mioc_sdt.hip): same staging layout, 8^M grids (M = 3, 4), beta > 0
 bool sdt_supported(const PyrGeom &G);
+bool sdt_seam_lists(const PyrGeom &G);  // the persistent driver loads straddling pair elements by seam lists (k_pyr_order)
 int sdt_slab_shift(const PyrGeom &G);  // the sphere-order mode the separable transform's kernels were built for
 int sdt_flag_words(const PyrGeom &G);  // persistent driver: hand-off flags per row (one per wave under SDT_SLAB)
 size_t sdt_lds_bytes(const PyrGeom &G);

@@ -892,19 +892,24 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
     if (tid == 0) wcnt[0][NK] = wcnt[1][NK] = wcnt[2][NK] = wcnt[3][NK] = 0;
     __syncthreads();
   }
-  // slab mode, strad (the persistent separable driver at 8^4): per slab of L/8 positions, the in-slab offsets p of the
-  // odd positions whose distance differs from position p-1's -- the second elements of the 16-byte position pairs that
-  // straddle a sphere seam (at most 21 per slab of the 8^4 grid: 22 distances), 0xFFFF-padded to 32
-  if (slab_shift && strad) {
+  // strad (the persistent separable driver at 8^4, 8 waves of 512 positions): per wave, the in-wave offsets of the odd
+  // positions whose distance differs from position p-1's -- the second elements of the 16-byte position pairs that
+  // straddle a sphere seam -- 0xFFFF-padded to 32.  A wave's positions (sd_seam_pos, mioc_sdt.hip): slab mode, the
+  // slab p / (L/8) (at most 21 seams in a slab: 22 distances); else positions 2(64w + l + (L/8)·q) + {0, 1} at offset
+  // 128q + 2l + {0, 1} (at most 28 seams in the whole order: 29 distances)
+  if (strad) {
     uint16_t *st = strad + ((size_t)k * P.nt + i) * 8 * 32;
-    const int SL = L / 8;
+    const int SL = L / 8, T = L / 8;
     for (int e = tid; e < 8 * 32; e += blockDim.x) st[e] = 0xFFFFu;
-    if (tid < 8) start[tid] = 0;  // per-slab counts
+    if (tid < 8) start[tid] = 0;  // per-wave counts
     __syncthreads();
     for (int p = 2 * tid + 1; p < L; p += 2 * blockDim.x)
       if ((perm[p] >> 16) != (perm[p - 1] >> 16)) {
-        const int sl = p / SL, e = atomicAdd(&start[sl], 1);
-        if (e < 32) st[sl * 32 + e] = (uint16_t)(p - sl * SL);
+        const int u = (p - 1) >> 1, t = u % T;
+        const int wv = slab_shift ? p / SL : t >> 6;
+        const int o = slab_shift ? p - wv * SL : 128 * (u / T) + 2 * (t & 63) + 1;
+        const int e = atomicAdd(&start[wv], 1);
+        if (e < 32) st[wv * 32 + e] = (uint16_t)o;
       }
   }
 }

@@ -67,15 +67,16 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #define SDT_PRED 0                       // persistent driver: stamp with a per-row predicted scale (see sdt_body)
 #endif
 #ifndef SDT_STRAD
-#define SDT_STRAD 1                      // SDT_SLAB: per-slab seam lists instead of one straddle load per pair (SdRaw)
+#define SDT_STRAD 1                      // persistent driver: per-wave seam lists instead of one straddle load per pair
 #endif
 #ifndef SDT_SLAB
 #define SDT_SLAB 0                       // slab-major sphere order: a wave loads and stamps only its own slab (sdt_body)
 #endif
 constexpr int SD_PRED_ROWS = 64;         // rows of a workgroup's chunk that keep a predicted scale (the others: none)
-constexpr int SD_STRAD_N = 32;           // straddle list entries per slab (a slab of the 8^4 grid has <= 21 spheres' seams)
-// SDT_SLAB at M = 4: the position pairs that straddle a sphere seam get their second element from one straddle load per
-// lane (a per-slab list, k_pyr_order) instead of one masked 8-byte load per pair and lane (SdRaw)
+constexpr int SD_STRAD_N = 32;           // seam list entries per wave (<= 21 seams in a slab, <= 28 in a sphere order)
+// the persistent driver at M = 4: the position pairs that straddle a sphere seam get their second element from one
+// straddle load per lane (a per-wave list of the wave's seams, k_pyr_order) instead of one masked 8-byte load per pair
+// and lane (SdRaw)
 // hand-off flags per row: SDT_SLAB's row flow hands off per slab (wave w of a row reads and writes only slab w's
 // positions), so every wave has its own `done` / `loaded` flag; else one per row
 template <int M>
@@ -84,7 +85,7 @@ __host__ __device__ constexpr int sd_flag_words() {
 }
 template <int M>
 __host__ __device__ constexpr bool sd_strad() {
-  return SDT_PRED && SDT_SLAB && SDT_STRAD && M == 4;
+  return SDT_STRAD && M == 4;
 }
 
 // Diagnostic build only (make stamps -> libmioc_stamps.so): per-workgroup phase clocks of the last launch.
@@ -242,6 +243,17 @@ __device__ __forceinline__ int sd_p2(int tid, int q) {
 }
 // The position of the level at distance 0 from u_old (when u_old is on the grid): the head of the first sphere --
 // position 0 of the sphere order, or (SDT_SLAB) the first position of u_old's slab.  Callers check b̃ == 0 there.
+// (sd_strad) the position of in-wave offset o (0 .. 511) of wave w: its slab under SDT_SLAB, else the wave's four runs
+// of 128 positions 2(64w + l + T·q) + {0, 1} (o = 128q + 2l + {0, 1}); k_pyr_order builds the seam lists with the same map
+template <int M>
+__device__ __forceinline__ int sd_seam_pos(int w, int o) {
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
+  if constexpr (SDT_SLAB)
+    return w * (L / NW) + o;
+  else
+    return 2 * T * (o >> 7) + 128 * w + (o & 127);
+}
+
 template <int M>
 __device__ __forceinline__ int sd_headpos(const PyrGeom &G, double uo_top) {
   constexpr int L = 1 << (3 * M);
@@ -759,13 +771,21 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
-        const double x = v[2 * q + hh];
-        psi[(hh ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
+        const double x = v[2 * q + hh];  // (sd_strad: +Inf for a straddling second element, written by its loader)
+        if (!(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) psi[(hh ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
         const bool fin = x < INFINITY;
         nv += __popcll(__ballot(fin)) << 16;
         pmn = sd_min(pmn, x);  // +Inf is neutral
         pmx = sd_max(pmx, __hiloint2double(fin ? __double2hiint(x) : (int)0xFFF00000, __double2loint(x)));  // +Inf -> -Inf
       }
+    if constexpr (sd_strad<M>()) {  // this lane's straddle element
+      const double x = (srank & 0x10000) ? INFINITY : xs;
+      const bool fin = srank >= 0 && x < INFINITY;
+      nv += __popcll(__ballot(fin)) << 16;
+      if (srank >= 0) psi[srank & 0xFFFF] = x;
+      pmn = sd_min(pmn, fin ? x : INFINITY);
+      pmx = sd_max(pmx, fin ? x : -INFINITY);
+    }
     sd_wave_stats(pmn, pmx);
     if (lane == 0) {
       sh.rmn[w] = pmn;
@@ -818,6 +838,11 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
             sh.spj[e] = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
             sh.spv[e] = v[2 * q + hh];
           }
+      if (sd_strad<M>() && srank >= 0 && !(srank & 0x10000) && xs < INFINITY) {
+        const int e = atomicAdd(&sh.nsp, 1);
+        sh.spj[e] = srank & 0xFFFF;
+        sh.spv[e] = xs;
+      }
     }
     sd_bar();
 #pragma unroll
@@ -836,8 +861,13 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
         for (int hh = 0; hh < 2; ++hh) {
           const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
           const double x = v[2 * q + hh];
-          dtv[sd_swz(j)] = x < INFINITY ? stamp(x, j) : INFINITY;
+          if (!(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) dtv[sd_swz(j)] = x < INFINITY ? stamp(x, j) : INFINITY;
         }
+      if (sd_strad<M>() && srank >= 0) {
+        const int js = srank & 0xFFFF;
+        const double x = (srank & 0x10000) ? INFINITY : xs;
+        dtv[sd_swz(js)] = x < INFINITY ? stamp(x, js) : INFINITY;
+      }
       sd_bar();
       SD_STAMP(2);
     } else {
@@ -1437,7 +1467,7 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
   if constexpr (sd_strad<M>()) {
     const int lane = tid & 63, wv = tid >> 6;
     sp = lane < SD_STRAD_N ? sl[wv * SD_STRAD_N + lane] : 0xFFFFu;
-    se = pin[wv * (L / NW) + (sp & (L / NW - 1))];
+    se = pin[sd_seam_pos<M>(wv, (int)(sp & (L / NW - 1)))];
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) w.e[q] = e[q];
@@ -1468,7 +1498,7 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
     }
   }
   if constexpr (sd_strad<M>()) {
-    const int P = (tid >> 6) * (L / NW) + (int)(sp & (L / NW - 1));
+    const int P = sd_seam_pos<M>(tid >> 6, (int)(sp & (L / NW - 1)));
     const int rsr = cp - (int)(se >> 16);
     const bool has = sp != 0xFFFFu;
     w.sv = __builtin_amdgcn_raw_buffer_load_b64(
@@ -1776,6 +1806,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
 }
 
 int sdt_slab_shift(const PyrGeom &G) { return SDT_SLAB ? 3 * (G.M - 1) : 0; }
+bool sdt_seam_lists(const PyrGeom &G) { return G.M == 4 && sd_strad<4>(); }
 int sdt_flag_words(const PyrGeom &G) { return G.M == 4 ? sd_flag_words<4>() : sd_flag_words<3>(); }
 
 bool sdt_supported(const PyrGeom &G) {

@@ -266,21 +266,27 @@ def test_trm_batch_production_path_equals_logged_and_sequential(chunk):
     of a chunk (mid-chunk for chunk 2, at a chunk end for 1 and 3)."""
     import torch
     from mioc.trm_batch import TRM_batch
-    K, nt, name = 12, 240, "doubletank"
+    K, nt = 12, 240
     par = mioc.TRM_parameters(beta=1e-3, Delta0=1.0, p=math.inf, maxiter=6, kmax=3)
     ctx = native.Context(0)
     ctx.set_levels(LevelTable([[0, 1]] * 3, mioc.bounded_sum_iterator([[0, 1]] * 3, 1, 1)))
     x0 = torch.empty(K, nt, 3, dtype=torch.float64, device="cuda")
-    ctx.rand_start_tensor(x0, seed=1234)
-    ctx.synchronize()
-    log = []
-    vl, ul, il = TRM_batch(name, par, x0=x0, log=log)
+    # the first of a few fixed (problem, seed) whose starts make some restart halve its radius (an inner loop of
+    # length > 1)
+    for name, seed in [(nm, sd) for nm in ("doubletank", "fishing") for sd in (1234, 99, 7, 2024)]:
+        ctx.rand_start_tensor(x0, seed=seed)
+        ctx.synchronize()
+        log = []
+        vl, ul, il = TRM_batch(name, par, x0=x0, log=log)
+        halvings = sum(int(np.sum(d == 1)) for *_, d, _inner in log)
+        if halvings >= 1:
+            break
+    assert halvings >= 1, "no restart halved its radius: the chunked inner loop was not exercised"
+    print(f"{name} seed {seed}: halvings {halvings}")
     stats = {}
     vals, u, iters = TRM_batch(name, par, x0=x0, inner_chunk=chunk, stats=stats)
     assert np.array_equal(vals, vl) and np.array_equal(iters, il)
     assert torch.equal(u, ul)
-    halvings = sum(int(np.sum(d == 1)) for *_, d, _inner in log)
-    assert halvings >= 1, "no restart halved its radius: the chunked inner loop was not exercised"
     assert stats["polls"] <= stats["outer"] * -(-par.kmax // chunk)
     ub = u.cpu().numpy()
     for k in range(K):
