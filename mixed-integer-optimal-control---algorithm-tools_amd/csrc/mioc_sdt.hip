@@ -69,6 +69,12 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_STRAD
 #define SDT_STRAD 1                      // persistent driver: per-wave seam lists instead of one straddle load per pair
 #endif
+#ifndef SDT_HOIST
+#define SDT_HOIST 0                      // persistent driver: read the next row's sphere-order entries early (SdPipe)
+#endif
+#ifndef SDT_BF
+#define SDT_BF 1                         // row body: straddle pairs and +Inf stamps without branches (in-wave LDS order)
+#endif
 #ifndef SDT_SLAB
 #define SDT_SLAB 0                       // slab-major sphere order: a wave loads and stamps only its own slab (sdt_body)
 #endif
@@ -601,6 +607,13 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     const double y = (x - ref) * inv + base;
     return __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | (j << SD_CB));
   };
+  // the stamp, +Inf kept +Inf, without a branch (SDT_BF)
+  auto stamp_inf = [&](double x, int j) {
+    const double y = stamp(x, j);
+    const unsigned m = x < INFINITY ? ~0u : 0u;
+    return __hiloint2double((int)(((unsigned)__double2hiint(y) & m) | (0x7FF00000u & ~m)),
+                            (int)((unsigned)__double2loint(y) & m));
+  };
   // ---- one pass of the transform: forward and backward sweep along the 8 levels of dimension m, unit step 1.0;
   // this thread's line is read from and (but for the last pass) written back to the swizzled LDS values ---------
   double o[8];
@@ -772,7 +785,8 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const double x = v[2 * q + hh];  // (sd_strad: +Inf for a straddling second element, written by its loader)
-        if (!(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) psi[(hh ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
+        // (SDT_BF: written anyway -- the straddle lane is in this wave and writes after it, in-wave LDS order)
+        if (SDT_BF || !(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) psi[(hh ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
         const bool fin = x < INFINITY;
         nv += __popcll(__ballot(fin)) << 16;
         pmn = sd_min(pmn, x);  // +Inf is neutral
@@ -861,12 +875,15 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
         for (int hh = 0; hh < 2; ++hh) {
           const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
           const double x = v[2 * q + hh];
-          if (!(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) dtv[sd_swz(j)] = x < INFINITY ? stamp(x, j) : INFINITY;
+          if constexpr (SDT_BF)
+            dtv[sd_swz(j)] = stamp_inf(x, j);
+          else if (!(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1)))
+            dtv[sd_swz(j)] = x < INFINITY ? stamp(x, j) : INFINITY;
         }
       if (sd_strad<M>() && srank >= 0) {
         const int js = srank & 0xFFFF;
         const double x = (srank & 0x10000) ? INFINITY : xs;
-        dtv[sd_swz(js)] = x < INFINITY ? stamp(x, js) : INFINITY;
+        dtv[sd_swz(js)] = SDT_BF ? stamp_inf(x, js) : x < INFINITY ? stamp(x, js) : INFINITY;
       }
       sd_bar();
       SD_STAMP(2);
@@ -1452,23 +1469,39 @@ struct SdRaw {
   unsigned mask;  // per pair q: bit 3q the first element has no source row, 3q+1 the second, 3q+2 it straddles
 };
 // sl: (sd_strad) the seam list of the slot `pin` (SD_STRAD_N in-slab offsets per slab, 0xFFFF: none)
+// the LDS side of a row's loads: this thread's sphere-order entries of the slot `pin` and (sd_strad) its seam -- read
+// early (SDT_HOIST: right after the row's first barrier) so that the issue does not wait for LDS
+struct SdNext {
+  uint2 e[4];
+  unsigned sp;  // (sd_strad) in-wave offset of this lane's seam (0xFFFF: none)
+  uint32_t se;  // its sphere-order entry
+};
 template <int M>
-__device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t rs, const uint32_t *pin,
-                                              const uint16_t *sl, int cp, unsigned boff, unsigned r0,
-                                              const unsigned rowb) {
+__device__ __forceinline__ void sd_read_next(SdNext &n, const uint32_t *pin, const uint16_t *sl) {
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) n.e[q] = *reinterpret_cast<const uint2 *>(pin + sd_p2<M>(tid, q));
+  // sd_strad: lane l < SD_STRAD_N of wave w takes the l-th seam of the wave's positions (its rank and distance)
+  n.sp = 0xFFFFu;
+  n.se = 0;
+  if constexpr (sd_strad<M>()) {
+    const int lane = tid & 63, wv = tid >> 6;
+    n.sp = lane < SD_STRAD_N ? sl[wv * SD_STRAD_N + lane] : 0xFFFFu;
+    n.se = pin[sd_seam_pos<M>(wv, (int)(n.sp & (L / NW - 1)))];
+  }
+}
+template <int M>
+__device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t rs, const SdNext &n, int cp,
+                                              unsigned boff, unsigned r0, const unsigned rowb) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
   const int tid = threadIdx.x;
   uint2 e[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) e[q] = *reinterpret_cast<const uint2 *>(pin + sd_p2<M>(tid, q));  // reads first
-  // sd_strad: lane l < SD_STRAD_N of wave w takes the l-th seam of slab w (its rank and distance from the slot)
-  unsigned sp = 0xFFFFu;
-  uint32_t se = 0;
-  if constexpr (sd_strad<M>()) {
-    const int lane = tid & 63, wv = tid >> 6;
-    sp = lane < SD_STRAD_N ? sl[wv * SD_STRAD_N + lane] : 0xFFFFu;
-    se = pin[sd_seam_pos<M>(wv, (int)(sp & (L / NW - 1)))];
-  }
+  for (int q = 0; q < 4; ++q) e[q] = n.e[q];
+  const unsigned sp = n.sp;
+  const uint32_t se = n.se;
+  (void)se;
 #pragma unroll
   for (int q = 0; q < 4; ++q) w.e[q] = e[q];
   // an offset beyond the resource's range drops the access (the load returns 0 without touching memory): rows
@@ -1580,6 +1613,7 @@ struct SdPipe {
   int32_t *fp;
   int need, val;
   SdRaw raw;
+  SdNext nx;  // the next row's sphere-order entries and seam (sd_read_next)
 
   // every wave polls its own dependency flags (lanes 0-31 RAW for the next row, 32-63 WAR for this row's stores; a
   // lane without one polls a flag that always passes -- every lane loads, no branch), checked in go(): SDT_PRED at
@@ -1595,6 +1629,10 @@ struct SdPipe {
     if constexpr (!SDT_PRED) {
       SD_TL_AT(g0, i, nt, 1);
       issue_polls();
+      // SDT_HOIST: the next row's sphere-order entries and seam, while the row computes (both slots are complete
+      // after this row's first barrier, and neither is rewritten before go() has issued the loads)
+      if constexpr (SDT_HOIST)
+        if (has_next) sd_read_next<M>(nx, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N);
     }
   }
   __device__ __forceinline__ void issue_polls() {
@@ -1665,8 +1703,8 @@ struct SdPipe {
       // k_pyr_order, and by induction every slot holds the order of the last step assigned to it)
       const int same = *reinterpret_cast<const volatile int32_t *>(sds + sd_dfuo_offset<M>() +
                                                                    (threadIdx.x >> 6) * sd_dfuo_stride<M>() + 16 * M);
-      sd_issue_pipe<M>(raw, rs, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N, ncp,
-                       (unsigned)((ni + 1) % NB) * bufb, r0b + (unsigned)(ni + 1) * rowb, rowb);
+      if constexpr (!SDT_HOIST || SDT_PRED) sd_read_next<M>(nx, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N);
+      sd_issue_pipe<M>(raw, rs, nx, ncp, (unsigned)((ni + 1) % NB) * bufb, r0b + (unsigned)(ni + 1) * rowb, rowb);
       if (ni != i && !(SDT_PERM_SKIP && same)) {
         sd_perm_dma_asm<M, (SDT_PRED && SDT_SLAB)>(pk + (size_t)ni * L, slot + (ni & 1) * L);
         if constexpr (sd_strad<M>()) sd_strad_dma(sk + (size_t)ni * 8 * SD_STRAD_N, sslot + (ni & 1) * 8 * SD_STRAD_N);
@@ -1748,8 +1786,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
                  nt >= 3 ? same2 + (size_t)k * nt + nt - 3 : nullptr, sds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   sd_bar();
-  sd_issue_pipe<M>(h.raw, h.rs, pslot(nt - 1), h.sslot + ((nt - 1) & 1) * 8 * SD_STRAD_N, lo,
-                   (unsigned)((nt - 1) % NB) * h.bufb, h.r0b + (unsigned)(nt - 1) * h.rowb,
+  sd_read_next<M>(h.nx, pslot(nt - 1), h.sslot + ((nt - 1) & 1) * 8 * SD_STRAD_N);
+  sd_issue_pipe<M>(h.raw, h.rs, h.nx, lo, (unsigned)((nt - 1) % NB) * h.bufb, h.r0b + (unsigned)(nt - 1) * h.rowb,
                    h.rowb);
   // a wait the compiler sees (vmcnt(0), other counters untouched): entering the loop with these loads pending would
   // make it assume, at the loop head, that nothing younger can be outstanding, and wait for every store there
