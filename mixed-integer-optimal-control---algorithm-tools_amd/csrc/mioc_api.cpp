@@ -477,7 +477,8 @@ int run_bellman(mioc_ctx *ctx) {
     HIP_TRY(ctx, launch_pinf_prep(ctx->stream, P, Lv, D));
     ev_end(ctx, 2, 1);
     ev_begin(ctx, 0, "k_pinf_recur");
-    HIP_TRY(ctx, launch_pinf_recur(ctx->stream, P, D));
+    if (!ctx->ncu) HIP_TRY(ctx, hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HIP_TRY(ctx, launch_pinf_recur(ctx->stream, P, D, ctx->ncu));
     ev_end(ctx, 0, 1);
   }
   ctx->have_dp = true;

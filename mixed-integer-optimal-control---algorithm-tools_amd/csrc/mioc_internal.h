@@ -188,7 +188,7 @@ struct PinfDev {
 // the walk's chunk and band for a p = Inf problem (mioc_pinf.hip)
 void pinf_plan(int RP, int nt, PinfDev &D);
 hipError_t launch_pinf_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D);
-hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D);
+hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ncu);  // ncu: the device's CUs
 hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D, int Bu,
                              Start *start);
 hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
@@ -243,6 +243,7 @@ void heat_free(HeatState *h);
 // ---- the context ----------------------------------------------------------------------------------
 struct mioc_ctx {
   int device = 0;
+  int ncu = 0;  // the device's compute units (cached on first use)
   hipStream_t stream = nullptr;
   std::string err;
   int64_t opt_algo = MIOC_ALGO_AUTO;

@@ -330,26 +330,155 @@ __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P
   }
 }
 
+// Budget rows 0 .. 32·NW (one more than NW full waves of lane quads, C4: B = 256, NW = 8): k_pinf_recur<BWP, 4> would
+// take a ninth wave (three waves on one SIMD, which bounds the step) for the one extra row E = 32·NW.  Here NW waves
+// of row pairs (two per SIMD) and the extra row split by classes: wave w's lane 0 takes classes [w·CW, (w+1)·CW) of
+// row E (CW = BWP / NW) and leaves its partial minimum in the LDS; after the step's barrier, wave 0 folds the NW
+// partials into R_i[E] (min is exact: the same value as one lane's fold over all classes) while the next step runs.
+template <int BWP, int NW>
+__global__ __launch_bounds__(NW * 64) void k_pinf_recur_xr(ProblemDev P, PinfDev D, int CH) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  constexpr int G = 4, CB = BWP / G, NP = CB / 2 + 1, CW = BWP / NW, E = 32 * NW;
+  static_assert(CB % 2 == 0 && CW * NW == BWP, "k_pinf_recur_xr shape");
+  const int RP = P.RP, B = P.B, nt = P.nt, k = blockIdx.x;
+  const int tid = (int)threadIdx.x / G, h = (int)threadIdx.x % G, w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+  const int AW = RP + BWP;
+  double *A = sm, *Kbuf = sm + 2 * AW, *part = Kbuf + 2 * CH * BWP;  // part: [2 parities][NW]
+  const double *kmin = D.kmin + (size_t)k * nt * BWP;
+  double *R = D.R + (size_t)k * nt * RP;
+  const int c0 = 2 * tid;
+  {
+    const int pt = (nt - 1) & 1;
+    for (int q = (int)threadIdx.x; q < 2 * AW; q += (int)blockDim.x) {
+      const int par = q / AW, kk = q % AW, c = kk + 1 - BWP;
+      double v = INFINITY;
+      if (par == pt && c >= 0 && c < BWP) v = kmin[(size_t)(nt - 1) * BWP + c];
+      A[q] = v;
+      if (par == pt && c >= 0 && c < RP) R[(size_t)(nt - 1) * RP + c] = c <= B ? v : INFINITY;
+    }
+  }
+  if (nt < 2) return;
+  // R_{i+1}[E] for wave 0's classes (b = 0 reads row E itself): the terminal value first
+  double rE = E < BWP ? kmin[(size_t)(nt - 1) * BWP + E] : INFINITY;
+  int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
+  glds_copy(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, (int)threadIdx.x, (int)blockDim.x);
+  vm_drain();
+  lds_barrier();
+  for (int q = 0; hi >= 0; ++q) {
+    const double *Kc = Kbuf + (size_t)(q & 1) * CH * BWP;
+    const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
+    if (nhi >= 0)
+      glds_copy(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
+                (int)threadIdx.x, (int)blockDim.x);
+    for (int i = hi; i >= lo; --i) {
+      const double *Ain = A + (size_t)((i + 1) & 1) * AW;
+      // wave 0: R_{i+1}[E] from the partials of step i+1 (written before the last barrier)
+      if (w == 0 && i + 1 <= nt - 2) {
+        const double *pp = part + ((i + 1) & 1) * NW;
+        double m = pp[0];
+#pragma unroll
+        for (int u = 1; u < NW; ++u) m = pvmin(m, pp[u]);
+        rE = m;
+        if (lane == 0) R[(size_t)(i + 1) * RP + E] = E <= B ? m : INFINITY;
+      }
+      const double2 *win = reinterpret_cast<const double2 *>(Ain + c0 + BWP - (h + 1) * CB);
+      const double2 *kr = reinterpret_cast<const double2 *>(Kc + (size_t)(i - lo) * BWP + h * CB);
+      double wv[2 * NP], kv[CB];
+#pragma unroll
+      for (int p2 = 0; p2 < NP; ++p2) {
+        const double2 x = win[p2];
+        wv[2 * p2] = x.x;
+        wv[2 * p2 + 1] = x.y;
+      }
+#pragma unroll
+      for (int p2 = 0; p2 < CB / 2; ++p2) {
+        const double2 y = kr[p2];
+        kv[2 * p2] = y.x;
+        kv[2 * p2 + 1] = y.y;
+      }
+      // row E, classes [w·CW, (w+1)·CW): R_{i+1}[E - b] (row E itself from rE)
+      double pe = INFINITY;
+      {
+        const double *ke = Kc + (size_t)(i - lo) * BWP + w * CW;
+#pragma unroll
+        for (int bb = 0; bb < CW; ++bb) {
+          const int b = w * CW + bb;
+          const double rv = b == 0 ? rE : Ain[E - b + BWP - 1];
+          pe = pvmin(pe, ke[bb] + rv);
+        }
+      }
+      double m0[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, m1[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+#pragma unroll
+      for (int b2 = 0; b2 < CB; ++b2) {
+        m0[b2 & 3] = pvmin(m0[b2 & 3], kv[b2] + wv[CB - 1 - b2]);
+        m1[b2 & 3] = pvmin(m1[b2 & 3], kv[b2] + wv[CB - b2]);
+      }
+      double r0 = pvmin(pvmin(m0[0], m0[1]), pvmin(m0[2], m0[3]));
+      double r1 = pvmin(pvmin(m1[0], m1[1]), pvmin(m1[2], m1[3]));
+      r0 = pvmin(r0, pv_dpp<0xB1>(r0));
+      r1 = pvmin(r1, pv_dpp<0xB1>(r1));
+      r0 = pvmin(r0, pv_dpp<0x4E>(r0));
+      r1 = pvmin(r1, pv_dpp<0x4E>(r1));
+      double *Aout = A + (size_t)(i & 1) * AW;
+      if (h == 0) {
+        Aout[c0 + BWP - 1] = r0;
+        R[(size_t)i * RP + c0] = c0 <= B ? r0 : INFINITY;
+      }
+      if (h == 1) {
+        Aout[c0 + BWP] = r1;
+        R[(size_t)i * RP + c0 + 1] = c0 + 1 <= B ? r1 : INFINITY;
+      }
+      if (lane == 0) part[(i & 1) * NW + w] = pe;
+      lds_barrier();
+    }
+    vm_drain();
+    lds_barrier();
+    hi = nhi;
+    lo = nlo;
+  }
+  // R_0[E]
+  if (threadIdx.x == 0) {
+    double m = part[0];
+    for (int u = 1; u < NW; ++u) m = pvmin(m, part[u]);
+    R[E] = E <= B ? m : INFINITY;
+  }
+}
+
+// rows c_from .. RP-1 of R (beyond k_pinf_recur_xr's rows, all above B): +Inf for every step
+__global__ void k_pinf_rfill(ProblemDev P, PinfDev D, int c_from) {
+  const int k = blockIdx.y, RP = P.RP, nt = P.nt, n = RP - c_from;
+  double *R = D.R + (size_t)k * nt * RP;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)nt * n; e += (size_t)gridDim.x * blockDim.x)
+    R[(e / n) * RP + c_from + e % n] = INFINITY;
+}
+
 int pinf_chunk_recur(int BWP) { return BWP <= 16 ? 64 : 32; }
 #ifndef PINF_RECUR_SPLIT
 #define PINF_RECUR_SPLIT 1  // few subproblems: G lanes per row pair (A/B builds: 0)
+#endif
+#ifndef PINF_RECUR_XR
+#define PINF_RECUR_XR 1     // C4's B = 256: eight waves and the extra row split by classes (k_pinf_recur_xr)
 #endif
 #ifndef PINF_RECUR_G
 #define PINF_RECUR_G 4      // lanes per row pair when split (2 or 4)
 #endif
 
-hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D) {
+hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ncu) {
   int pairs = ((P.RP / 2 + 63) / 64) * 64;  // one thread (G = 1) or lane quad (G = 4) per two budget rows
   if (pairs > 512) pairs = 512;
   // few subproblems (fewer workgroups than a quarter of the CUs): four lanes per row pair; a batch keeps one lane
   // (its workgroups already fill the CUs, and the recursion is then bound by the R stores)
-  int ncu = 0, dev = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int G = PINF_RECUR_SPLIT && P.K * 4 <= ncu && D.BWP >= 8 ? PINF_RECUR_G : 1;
+  const int CH = pinf_chunk_recur(D.BWP);
+  // ... and with B + 1 = 32·8 + 1 (C4), eight waves of row pairs and the extra row split by classes (k_pinf_recur_xr)
+  if (PINF_RECUR_XR && G == 4 && D.BWP == 32 && P.B + 1 == 32 * 8 + 1 && 32 * 8 + 1 <= P.RP) {
+    const size_t lds = (size_t)(2 * (D.BWP + P.RP) + 2 * CH * D.BWP + 2 * 8) * sizeof(double);
+    if (32 * 8 + 1 < P.RP) hipLaunchKernelGGL(k_pinf_rfill, dim3(64, P.K), dim3(256), 0, s, P, D, 32 * 8 + 1);
+    hipLaunchKernelGGL((k_pinf_recur_xr<32, 8>), dim3(P.K), dim3(512), lds, s, P, D, CH);
+    return hipGetLastError();
+  }
   if (G * pairs > 1024) pairs = 1024 / G;
   const int threads = pairs * G;
-  const int CH = pinf_chunk_recur(D.BWP);
   size_t lds = (size_t)(2 * (D.BWP + P.RP) + 2 * CH * D.BWP) * sizeof(double);
 #define PINF_RECUR(BW)                                                                                    \
   if (G == 4)                                                                                             \

@@ -72,6 +72,9 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_HOIST
 #define SDT_HOIST 0                      // persistent driver: read the next row's sphere-order entries early (SdPipe)
 #endif
+#ifndef SDT_SPREAD
+#define SDT_SPREAD 0                     // persistent driver: the next row's loads issued between the passes (SdPipe; measured slower)
+#endif
 #ifndef SDT_BF
 #define SDT_BF 1                         // row body: straddle pairs and +Inf stamps without branches (in-wave LDS order)
 #endif
@@ -892,12 +895,14 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     }
     // `v` and `pin` are dead from here on: the driver may reuse the latter
     h.go();
+    if (!transform) h.load_part(-1);  // (SDT_SPREAD) no passes to spread the loads over
   }
   if (transform) {
     // ---- the M passes (SDT_SLAB: passes 0 .. M-2 already ran per wave, only the last pass is left) ----------------
 #pragma unroll
     for (int m = SLAB ? M - 1 : 0; m < M; ++m) {
       pass(m);
+      h.load_part(m);  // (SDT_SPREAD) the next row's loads, a part after each pass
 #if SDT_WAVE_LOCAL
       // only the last pass, which runs along the top coordinate, needs every wave's values
       if (m + 2 < M)
@@ -1222,6 +1227,7 @@ struct SdHooksNone {
   __device__ __forceinline__ void wave_done() {}
   __device__ __forceinline__ void early() {}
   __device__ __forceinline__ void go() {}
+  __device__ __forceinline__ void load_part(int) {}
   __device__ __forceinline__ void late_drain() {}
   __device__ __forceinline__ void publish() {}
 };
@@ -1461,6 +1467,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_row0(ProblemDev P, Lev
 // hardware) where a row is below 0 or no second load is needed.  `sd_take` selects once the data is in (at the
 // next row's start).
 struct SdRaw {
+  unsigned oa[4], osv;  // (SDT_SPREAD) the offsets of the loads not yet issued
   sd_u32x4 a[4];
   sd_u32x2 b[4];  // (not sd_strad) the second elements of straddling pairs
   sd_u32x2 sv;    // (sd_strad) this lane's straddle element, at position sp of its slab: rank srank
@@ -1491,9 +1498,11 @@ __device__ __forceinline__ void sd_read_next(SdNext &n, const uint32_t *pin, con
     n.se = pin[sd_seam_pos<M>(wv, (int)(n.sp & (L / NW - 1)))];
   }
 }
-template <int M>
+// SPREAD (sd_strad only): compute the offsets, issue nothing (sd_pipe_part issues the loads in three parts)
+template <int M, bool SPREAD = false>
 __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t rs, const SdNext &n, int cp,
                                               unsigned boff, unsigned r0, const unsigned rowb) {
+  static_assert(!SPREAD || sd_strad<M>(), "spread issue needs the seam lists");
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
   const int tid = threadIdx.x;
   uint2 e[4];
@@ -1519,9 +1528,13 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
                       : OOB;
     mask |= ((unsigned)(ra < 0) | (unsigned)(rb < 0) << 1 | (unsigned)(ra != rb) << 2) << (3 * q);
   }
+  if constexpr (SPREAD) {  // sd_strad: issued later, in parts (sd_pipe_part)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w.oa[q] = oa[q];
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa[q], 0, 16);
+    if constexpr (!SPREAD) w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa[q], 0, 16);
     if constexpr (!sd_strad<M>()) {
 #ifndef SDT_EXP_NOB64  // timing experiment only (wrong results): without the straddle loads
       w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob[q], 0, 16);
@@ -1534,12 +1547,28 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
     const int P = sd_seam_pos<M>(tid >> 6, (int)(sp & (L / NW - 1)));
     const int rsr = cp - (int)(se >> 16);
     const bool has = sp != 0xFFFFu;
-    w.sv = __builtin_amdgcn_raw_buffer_load_b64(
-        rs, !has || rsr < 0 ? OOB : rsr >= 1 ? boff + (unsigned)rsr * rowb + (unsigned)P * 8u : r0 + (unsigned)P * 8u, 0,
-        16);
+    const unsigned osv =
+        !has || rsr < 0 ? OOB : rsr >= 1 ? boff + (unsigned)rsr * rowb + (unsigned)P * 8u : r0 + (unsigned)P * 8u;
+    if constexpr (SPREAD)
+      w.osv = osv;
+    else
+      w.sv = __builtin_amdgcn_raw_buffer_load_b64(rs, osv, 0, 16);
     w.srank = has ? (int)(se & 0xFFFFu) | (rsr < 0 ? 0x10000 : 0) : -1;
   }
   w.mask = mask;
+}
+// (SDT_SPREAD) part `part` of the loads prepared by sd_issue_pipe<M, true>: 0 and 1 two pairs each, 2 the straddle
+// element; part < 0: all of them
+__device__ __forceinline__ void sd_pipe_part(SdRaw &w, __amdgpu_buffer_rsrc_t rs, int part) {
+  if (part <= 0) {
+    w.a[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, w.oa[0], 0, 16);
+    w.a[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, w.oa[1], 0, 16);
+  }
+  if (part < 0 || part == 1) {
+    w.a[2] = __builtin_amdgcn_raw_buffer_load_b128(rs, w.oa[2], 0, 16);
+    w.a[3] = __builtin_amdgcn_raw_buffer_load_b128(rs, w.oa[3], 0, 16);
+  }
+  if (part < 0 || part == 2) w.sv = __builtin_amdgcn_raw_buffer_load_b64(rs, w.osv, 0, 16);
 }
 // this lane's eight values; (sd_strad) the second element of a straddling pair is +Inf here -- its value comes with
 // the lane that loaded it as a straddle element, and the row body does not store it (the `skip` bits of the mask)
@@ -1588,6 +1617,9 @@ template <int M>
 struct SdPipe {
   static constexpr int L = 1 << (3 * M), FW = sd_flag_words<M>();
   static constexpr bool SLAB = SDT_PRED && SDT_SLAB;
+  // SDT_SPREAD: the next row's loads are issued in parts between the passes (load_part), not all at go(), so that
+  // the CU's memory pipeline works on them while the row computes
+  static constexpr bool SPREAD = SDT_SPREAD && !SDT_PRED && sd_strad<M>();
   // this wave's hand-off flag of row r (per slab under SDT_SLAB, else per row)
   __device__ __forceinline__ int32_t *dflag(int r) const { return dk + r * FW + (FW > 1 ? (int)(threadIdx.x >> 6) : 0); }
   __device__ __forceinline__ int32_t *lflag(int r) const { return lk + r * FW + (FW > 1 ? (int)(threadIdx.x >> 6) : 0); }
@@ -1704,7 +1736,7 @@ struct SdPipe {
       const int same = *reinterpret_cast<const volatile int32_t *>(sds + sd_dfuo_offset<M>() +
                                                                    (threadIdx.x >> 6) * sd_dfuo_stride<M>() + 16 * M);
       if constexpr (!SDT_HOIST || SDT_PRED) sd_read_next<M>(nx, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N);
-      sd_issue_pipe<M>(raw, rs, nx, ncp, (unsigned)((ni + 1) % NB) * bufb, r0b + (unsigned)(ni + 1) * rowb, rowb);
+      sd_issue_pipe<M, SPREAD>(raw, rs, nx, ncp, (unsigned)((ni + 1) % NB) * bufb, r0b + (unsigned)(ni + 1) * rowb, rowb);
       if (ni != i && !(SDT_PERM_SKIP && same)) {
         sd_perm_dma_asm<M, (SDT_PRED && SDT_SLAB)>(pk + (size_t)ni * L, slot + (ni & 1) * L);
         if constexpr (sd_strad<M>()) sd_strad_dma(sk + (size_t)ni * 8 * SD_STRAD_N, sslot + (ni & 1) * 8 * SD_STRAD_N);
@@ -1713,6 +1745,11 @@ struct SdPipe {
                      ni >= 1 ? sm + (size_t)k * nt + ni - 1 : nullptr, sds);
     }
     SD_TL_AT(g0, i, nt, 4);
+  }
+  // (SPREAD) after pass m of the row body (m < 0: the row takes no transform -- all at once)
+  __device__ __forceinline__ void load_part(int m) {
+    if constexpr (SPREAD)
+      if (has_next && m <= 2) sd_pipe_part(raw, rs, m);
   }
   // late in the row, before the barrier after the winners: this wave's stores of the previous row have landed (they
   // have had the whole row: no wait), so after that barrier the previous row can be published
