@@ -284,7 +284,7 @@ def candidates_per_step(levels, uo, B):
     return levels.L * tot / max(1, nt - 1)
 
 
-def pmc_traffic(kernel, cfg=None):
+def pmc_traffic(kernel, cfg=None, K=None):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/roundN_pmc_traffic.json,
     made by scripts/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None."""
     import glob
@@ -299,7 +299,12 @@ def pmc_traffic(kernel, cfg=None):
             continue
         # entries recorded from a single-config pass are qualified "kernel@CFG"; plain names come from the default
         # bench passes, where each kernel belongs to one line (C4 headline / its p=Inf variant / the C5 batch)
-        e = ks.get(f"{kernel}@{cfg}") or (ks.get(kernel) if cfg in (None, "C4", "C5") else None)
+        # a batch size qualifier first ("k_fsep2@C5x128": the grid-size split of scripts/pmc_traffic.py --qualify),
+        # then the config, then (C4) a launch variant of the kernel ("k_pinf_recur_xr" for the event "k_pinf_recur")
+        e = (ks.get(f"{kernel}@{cfg}x{K}") if K else None) or ks.get(f"{kernel}@{cfg}") or \
+            (ks.get(kernel) if cfg in (None, "C4", "C5") else None)
+        if not e and cfg in (None, "C4"):
+            e = next((v for n, v in sorted(ks.items()) if n.startswith(kernel + "_") and "@" not in n), None)
         if e and "hbm_bytes_per_launch" in e:
             found.append((int(re.search(r"round(\d+)_", os.path.basename(f)).group(1)), e["hbm_bytes_per_launch"], f))
     if not found:
@@ -375,7 +380,7 @@ def roofline_of(res):
         ops = 2.0 * K * (nt - 1) * (B + 1) * bw
         steps = nt - 1  # one launch runs the whole recursion
     ach = bytes_per_launch / avg_s / 1e9
-    traffic, tsrc = pmc_traffic(name, res["config"])
+    traffic, tsrc = pmc_traffic(name, res["config"], K)
     roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None if traffic is None else round(traffic),
             "traffic_source": tsrc, "kernel": name,
@@ -400,8 +405,11 @@ def pmc_valu_of(kernel, avg_s, steps):
     """Counter-backed VALU figures of `kernel` from the --pmc-valu CSV (a separate rocprofv3 --pmc pass of THIS build
     over the same bench command; no committed file of an older build is ever used): the dispatches of `kernel` whose
     duration is within 20 % of this line's HIP-event launch time, averaged.  VALU instructions per wave and DP step
-    (SQ_INSTS_VALU / SQ_WAVES / steps) and the SIMDs' VALU-busy fraction (rocprof's gfx950 VALUBusy:
-    ΣSQ_ACTIVE_INST_VALU / (CUs x GRBM_GUI_ACTIVE))."""
+    (SQ_INSTS_VALU / SQ_WAVES / steps) and the SIMDs' VALU-busy fraction: SQ_ACTIVE_INST_VALU counts quad-cycles
+    summed over every wave, GRBM_GUI_ACTIVE cycles summed over the 8 XCDs (MI355X_MICROARCH.md, rocprofv3 PMC), so
+    busy = ΣSQ_ACTIVE_INST_VALU·4 / (4 SIMDs · CUs · GRBM_GUI_ACTIVE/8) over the whole chip, and the same over the CUs
+    the launch occupies (min(256, workgroups)); the wave-time split ACTIVE_INST_ANY / WAIT_ANY / WAIT_INST_ANY
+    (disjoint, summing to SQ_WAVE_CYCLES) where the pass has them."""
     import csv
     path, how = PMC_VALU_FILE, "--pmc-valu (this build)"
     if not path:
@@ -424,6 +432,7 @@ def pmc_valu_of(kernel, avg_s, steps):
                 continue
             d = per.setdefault(r["Dispatch_Id"], {})
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            d["_wgs"] = int(r["Grid_Size"]) // max(1, int(r["Workgroup_Size"]))
     if not per:
         return None
     avg = {}
@@ -434,7 +443,16 @@ def pmc_valu_of(kernel, avg_s, steps):
     if avg.get("SQ_INSTS_VALU") and avg.get("SQ_WAVES"):
         out["pmc_valu_instructions_per_wave_step"] = round(avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"] / steps, 1)
     if avg.get("SQ_ACTIVE_INST_VALU") and avg.get("GRBM_GUI_ACTIVE"):
-        out["pmc_valu_busy_frac"] = round(avg["SQ_ACTIVE_INST_VALU"] / (256 * avg["GRBM_GUI_ACTIVE"]), 4)
+        simd_cycles = 4 * avg["GRBM_GUI_ACTIVE"] / 8  # per CU: 4 SIMDs x the kernel's cycles
+        out["pmc_valu_busy_frac"] = round(4 * avg["SQ_ACTIVE_INST_VALU"] / (256 * simd_cycles), 4)
+        ncu = min(256, max(1, int(avg.get("_wgs", 256))))
+        out["pmc_valu_busy_frac_active_cus"] = round(4 * avg["SQ_ACTIVE_INST_VALU"] / (ncu * simd_cycles), 4)
+        out["pmc_active_cus"] = ncu
+    wc = avg.get("SQ_WAVE_CYCLES")
+    if wc and avg.get("SQ_ACTIVE_INST_ANY") and avg.get("SQ_WAIT_ANY") and avg.get("SQ_WAIT_INST_ANY"):
+        out["pmc_wave_time_split"] = {"issuing": round(avg["SQ_ACTIVE_INST_ANY"] / wc, 3),
+                                      "waiting (waitcnt, barrier)": round(avg["SQ_WAIT_ANY"] / wc, 3),
+                                      "issue-stalled": round(avg["SQ_WAIT_INST_ANY"] / wc, 3)}
     return out
 
 

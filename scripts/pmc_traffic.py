@@ -3,7 +3,8 @@
 Usage: python scripts/pmc_traffic.py OUT.json [--qualify KERNEL@CFG:MIN_WGS ...] [CFG:]LABEL=DIR/NAME_counter_collection.csv ...
 A CFG: prefix (a pass over one bench config, e.g. `bench.py --config C2 ...`) stores the kernels as "name@CFG".
 --qualify KERNEL@CFG:MIN_WGS stores the dispatches of KERNEL with at least MIN_WGS workgroups as "KERNEL@CFG" (one
-pass over the default bench holds both the single-subproblem C4 line and the 1024-restart batch lines).
+pass over the default bench holds both the single-subproblem C4 line and the 1024-restart batch lines); several per
+kernel split it by grid size (the largest threshold met wins), e.g. k_fsep2@C5x1024:1024 and k_fsep2@C5x128:256.
 FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE
 reports half the bytes of wide reads, so it is doubled; WRITE_SIZE is taken as is.  Both counters
 count Infinity-Cache hits as memory-side traffic.
@@ -26,7 +27,8 @@ def main():
     while args and args[0] == "--qualify":
         kc, mw = args[1].rsplit(":", 1)
         kname, kcfg = kc.split("@")
-        qual[kname] = (kcfg, int(mw))
+        qual.setdefault(kname, []).append((int(mw), kcfg))  # several per kernel: the largest threshold met wins
+        qual[kname].sort(reverse=True)
         args = args[2:]
     res = {}
     for spec in args:
@@ -38,8 +40,10 @@ def main():
                 name = short(row["Kernel_Name"])
                 if name in qual:
                     wgs = int(row["Grid_Size"]) // max(1, int(row["Workgroup_Size"]))
-                    if wgs >= qual[name][1]:
-                        name = f"{name}@{qual[name][0]}"
+                    for mw, qc in qual[name]:
+                        if wgs >= mw:
+                            name = f"{name}@{qc}"
+                            break
                 acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
         for k, d in acc.items():
             e = res.setdefault(f"{k}@{cfg}" if cfg and "@" not in k else k, {})
