@@ -78,6 +78,9 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_BF
 #define SDT_BF 1                         // row body: straddle pairs and +Inf stamps without branches (in-wave LDS order)
 #endif
+#ifndef SDT_PRED_PROBE
+#define SDT_PRED_PROBE 0                 // diagnostic build: count where a same-binade predicted scale would miss
+#endif
 #ifndef SDT_SLAB
 #define SDT_SLAB 0                       // slab-major sphere order: a wave loads and stamps only its own slab (sdt_body)
 #endif
@@ -440,7 +443,7 @@ struct SdtShared {
   int nsp;   // sparse rows: the finite sources (rank, Ψ)
   int spj[SD_SPARSE];
   double spv[SD_SPARSE];
-  int cnt[3];  // targets sent to the exact scan (near ties, direct rows), rows stamped twice (predicted scale
+  int cnt[4];  // targets sent to the exact scan (near ties, direct rows), rows stamped twice (predicted scale
               // missed); flushed to the global counters [0], [1], [4] once
   int rfail[NW];  // per wave: a finite Ψ outside the row's predicted range (SDT_PRED)
   double pred[SD_PRED_ROWS][2];  // per chunk row: the predicted range [lo, hi] of its Ψ (lo = +Inf: none yet)
@@ -671,29 +674,46 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   constexpr bool PRED = PERSIST && SDT_PRED;
   constexpr bool SLAB = PRED && SDT_SLAB;
   if constexpr (PRED) {
-    // Predicted scale (persistent driver): a row's Ψ move little from one step to the next, so the range [lo, hi]
-    // this row saw at an earlier step, widened by its own width, is stamped with at once -- no min/max reduction and
-    // no barrier before the stamps.  Every finite Ψ is checked to lie in [lo, hi]; then every bound of the
-    // certification holds as if (lo, hi) were the row's own min and max (the binade holds [lo, hi] + Smax, tol
-    // covers |Ψ| <= max(|lo|, |hi|)), only the grid is up to ~3x coarser.  A miss (or no prediction yet) redoes the
-    // stamps from the exact min and max below, exactly as the per-step driver does, and refreshes the prediction.
+    // Predicted scale (persistent driver): a row's Ψ move little from one step to the next.  prow holds the exact
+    // range [lo, hi] of this row's Ψ at its previous step; its scale has binade exponent E, and every range up to
+    // R(E) (the widest one whose exact scale still has exponent E) stamps on the same grid.  So the window
+    // [lo - r, hi + r], r = (R(E) - rs)/2 in β units, stamps at once -- no min/max reduction and no barrier before
+    // the stamps -- on the grid the row's own exact range would give whenever its range stays in the window (98 % of
+    // the C4 rows; SDT_PRED_PROBE).  Every finite Ψ is checked to lie in the window; then every bound of the
+    // certification holds as if the window were the row's own min and max (the binade holds it + Smax, tol covers
+    // |Ψ| up to its ends).  A miss (or no prediction yet) redoes the stamps from the exact min and max, which every
+    // wave reduces alongside its stamps anyway (they become the next step's prediction).
     const double plo = prow ? prow[0] : INFINITY, phi = prow ? prow[1] : -INFINITY;
-    scale(plo, phi);
+    double wlo = plo, whi = phi;
+    if (plo <= phi) {
+      const double rs_p = (phi - plo) * inv + (double)Smax;
+      const int E = ilogb(fmin(rs_p, 0x1p31) * (1.0 + 0x1p-20) + 1.0) + 2;
+      // scale() below: exponent E for rs·(1 + 2^-20) + 1 < 2^(E-1); the last factor keeps the window's computed
+      // range below that bound through the roundings of (whi - wlo)·inv
+      const double R = (ldexp(1.0, E - 1) - 1.0) / (1.0 + 0x1p-20) * (1.0 - 0x1p-30);
+      const double room = fmax(R - rs_p, 0.0) * 0.5 * beta;
+      wlo = plo - room;
+      whi = phi + room;
+    }
+    scale(wlo, whi);
     const bool miss = !(plo <= phi) || !scale_ok || !(tol < base * 0x1p-20);
     bool bad = false;
+    double pmn = INFINITY, pmx = -INFINITY;  // the exact range, for the next step (and a miss)
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
-        const double x = v[2 * q + hh];
+        const double x = v[2 * q + hh];  // (sd_strad: +Inf for a straddling second element, written by its loader)
         const bool fin = x < INFINITY;
         nv += __popcll(__ballot(fin)) << 16;
-        bad |= fin && !(x >= plo && x <= phi);
-        const double V = fin ? stamp(x, j) : INFINITY;
-        if (!(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) {  // (a straddling second element: its loader's)
+        bad |= fin && !(x >= wlo && x <= whi);
+        pmn = sd_min(pmn, x);
+        pmx = sd_max(pmx, fin ? x : -INFINITY);
+        // (SDT_BF: written anyway -- the straddle lane is in this wave and writes after it, in-wave LDS order)
+        if (SDT_BF || !(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) {
           psi[j] = x;
-          dtv[sd_swz(j)] = V;
+          dtv[sd_swz(j)] = SDT_BF ? stamp_inf(x, j) : fin ? stamp(x, j) : INFINITY;
         }
       }
     if constexpr (sd_strad<M>()) {  // this lane's straddle element
@@ -701,17 +721,21 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       const double x = (srank & 0x10000) ? INFINITY : xs;
       const bool fin = srank >= 0 && x < INFINITY;
       nv += __popcll(__ballot(fin)) << 16;
-      bad |= fin && !(x >= plo && x <= phi);
-      const double V = fin ? stamp(x, js) : INFINITY;
+      bad |= fin && !(x >= wlo && x <= whi);
+      pmn = sd_min(pmn, fin ? x : INFINITY);
+      pmx = sd_max(pmx, fin ? x : -INFINITY);
       if (srank >= 0) {
         psi[js] = x;
-        dtv[sd_swz(js)] = V;
+        dtv[sd_swz(js)] = fin ? stamp(x, js) : INFINITY;
       }
     }
     const bool wbad = __ballot(bad) != 0;
+    sd_wave_stats(pmn, pmx);
     if (lane == 0) {
       sh.rnv[w] = nv;
       sh.rfail[w] = wbad;
+      sh.rmn[w] = pmn;
+      sh.rmx[w] = pmx;
     }
     if constexpr (SLAB) {
       // SDT_SLAB: every Ψ this wave loaded lies in its own slab, so its stamps and passes 0 .. M-2 need no other
@@ -724,7 +748,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       h.go();         // its polls matched -> its slab of the next row's loads and of the sphere-order copy
       sd_bar();       // every wave's passes 0 .. M-2 and counts are in LDS
     } else {
-      sd_bar();  // Ψ by rank and the stamps of every wave are in LDS; every wave has consumed its loads
+      sd_bar();  // Ψ by rank, the stamps and the range of every wave are in LDS; every wave has consumed its loads
       // `v` and `pin` are dead from here on: the driver may reuse the latter
       h.go();
     }
@@ -738,33 +762,22 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     }
     nf = nv >> 16;
     nv &= 0xFFFF;
-    // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
-    empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || nf == 0)) != 0;  // uniform
-    if (__builtin_amdgcn_readfirstlane((int)(!empty && nf > SD_SPARSE && nv > SD_FEW && fail))) {
-      // the exact range of the row from Ψ by rank (lane t: ranks t + T·q), then the stamps again
-      double pmn = INFINITY, pmx = -INFINITY;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const double x = psi[tid + T * q];
-        pmn = sd_min(pmn, x);  // +Inf is neutral
-        pmx = sd_max(pmx, __hiloint2double(x < INFINITY ? __double2hiint(x) : (int)0xFFF00000, __double2loint(x)));
-      }
-      sd_wave_stats(pmn, pmx);
-      if (lane == 0) {
-        sh.rmn[w] = pmn;
-        sh.rmx[w] = pmx;
-      }
-      sd_bar();
+    // the row's exact range: the next step's prediction (wave 0), and the scale of a miss
+    const bool redo = __builtin_amdgcn_readfirstlane((int)(nv != 0 && nf > SD_SPARSE && nv > SD_FEW && fail)) != 0;
+    if (redo || (w == 0 && prow)) {
 #pragma unroll
       for (int q = 0; q < NW; ++q) {
         pmn = sd_min(pmn, sh.rmn[q]);
         pmx = sd_max(pmx, sh.rmx[q]);
       }
-      if (tid == 0 && prow) {  // read again at this row's next step, after many barriers
-        const double mg = (pmx - pmn) + 8.0 * beta;
-        prow[0] = pmn - mg;
-        prow[1] = pmx + mg;
+      if (tid == 0 && prow) {  // read again by this thread at the row's next step
+        prow[0] = pmn;
+        prow[1] = pmx;
       }
+    }
+    // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
+    empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || nf == 0)) != 0;  // uniform
+    if (redo) {
       scale(pmn, pmx);
       if (__builtin_amdgcn_readfirstlane((int)(scale_ok && tol < base * 0x1p-20))) {
 #pragma unroll
@@ -824,6 +837,30 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     SD_STAMP(1);
     // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
     empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || !(pmn < INFINITY))) != 0;  // uniform
+#if SDT_PRED_PROBE
+    // diagnostic build: would a scale predicted from this row's previous step hold?  The window keeps the previous
+    // step's binade exponent E and centres its range in the widest range E allows; counters [4] misses, [5] hits
+    // only one binade up (grid twice as coarse)
+    if (tid == 0 && prow && pmn < INFINITY) {
+      const double lo_p = prow[0], hi_p = prow[1];
+      if (lo_p <= hi_p) {
+        const double rs_p = (hi_p - lo_p) * inv + (double)Smax;
+        const int E = ilogb(fmin(rs_p, 0x1p31) * (1.0 + 0x1p-20) + 1.0) + 2;
+        auto fits = [&](int e) {
+          const double R = (ldexp(1.0, e - 1) - 1.0) / (1.0 + 0x1p-20) * (1.0 - 0x1p-40), ref = lo_p - 0.5 * (R - rs_p) * beta;
+          return pmn >= ref && (pmx - ref) * inv + (double)Smax < R;
+        };
+        if (!fits(E)) {
+          if (fits(E + 1))
+            sh.cnt[3] += 1;
+          else
+            sh.cnt[2] += 1;
+        }
+      }
+      prow[0] = pmn;
+      prow[1] = pmx;
+    }
+#endif
     scale(pmn, pmx);
   }
   // few finite sources (rows near c' = 0): every target's minimum over them, directly
@@ -1805,7 +1842,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   h.pcp = -1, h.pi = 0;
   if (tid == 0) {
     sh.stop = 0;
-    sh.cnt[0] = sh.cnt[1] = sh.cnt[2] = 0;
+    sh.cnt[0] = sh.cnt[1] = sh.cnt[2] = sh.cnt[3] = 0;
   }
   if (tid < SD_PRED_ROWS) {  // no predicted scale yet (the prologue's barrier orders these before every use)
     sh.pred[tid][0] = INFINITY;
@@ -1875,6 +1912,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
     if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
     if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
     if (sh.cnt[2]) atomicAdd(&counters[4], sh.cnt[2]);
+    if (sh.cnt[3]) atomicAdd(&counters[5], sh.cnt[3]);
   }
   SD_FLUSH();
   SD_TL_FLUSH(h.g0);
