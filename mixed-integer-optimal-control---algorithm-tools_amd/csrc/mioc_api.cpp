@@ -478,8 +478,26 @@ int run_bellman(mioc_ctx *ctx) {
     ev_end(ctx, 2, 1);
     ev_begin(ctx, 0, "k_pinf_recur");
     if (!ctx->ncu) HIP_TRY(ctx, hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    HIP_TRY(ctx, launch_pinf_recur(ctx->stream, P, D, ctx->ncu));
+    // row segments on several CUs need their hand-off flags (and a timed-out wait redoes the DP in one workgroup)
+    int32_t *pflags = nullptr;
+    if (!ctx->force_steps) {
+      const size_t fbytes = ((size_t)K * (RP / 16 + 1) + 1) * sizeof(int32_t);
+      rc = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, fbytes, "p=Inf segment flags");
+      if (rc) return rc;
+      HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, fbytes, ctx->stream));
+      if (!ctx->h_run_err) HIP_TRY(ctx, hipHostMalloc(&ctx->h_run_err, 16, 0));
+      *ctx->h_run_err = 0;
+      pflags = ctx->d_runflags;
+    }
+    bool segmented = false;
+    HIP_TRY(ctx, launch_pinf_recur(ctx->stream, P, D, ctx->ncu, pflags, ctx->spin_limit, &segmented));
     ev_end(ctx, 0, 1);
+    if (segmented) {
+      const int nseg = pinf_recur_segments(P);
+      HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + (size_t)K * nseg, sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, ctx->stream));
+      ctx->run_pending = true;
+    }
   }
   ctx->have_dp = true;
   return MIOC_OK;

@@ -188,7 +188,11 @@ struct PinfDev {
 // the walk's chunk and band for a p = Inf problem (mioc_pinf.hip)
 void pinf_plan(int RP, int nt, PinfDev &D);
 hipError_t launch_pinf_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D);
-hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ncu);  // ncu: the device's CUs
+// ncu: the device's CUs; flags (K·ceil((B+1)/32) + 1 zeroed words, or null): lets few subproblems run in row segments
+// on several CUs, *segmented then says so (the caller checks the error word after it, check_run)
+hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ncu, int32_t *flags,
+                             unsigned spin_limit, bool *segmented);
+int pinf_recur_segments(const ProblemDev &P);  // row segments of k_pinf_recur_mc per subproblem (its error word's offset)
 hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D, int Bu,
                              Start *start);
 hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,

@@ -21,6 +21,24 @@
 #include "mioc_internal.h"
 
 namespace mioc {
+#ifndef PINF_RECUR_SPLIT
+#define PINF_RECUR_SPLIT 1  // few subproblems: G lanes per row pair (A/B builds: 0)
+#endif
+#ifndef PINF_RECUR_MC
+#define PINF_RECUR_MC 1     // few subproblems: row segments on several CUs (k_pinf_recur_mc)
+#endif
+#ifndef PINF_MC_CHUNK
+#define PINF_MC_CHUNK 16       // k_pinf_recur_mc: steps per segment hand-off
+#endif
+#ifndef PINF_RECUR_MC_LANES
+#define PINF_RECUR_MC_LANES 4  // k_pinf_recur_mc: lanes per budget row (4: 16 rows per segment; 2: 32)
+#endif
+#ifndef PINF_RECUR_XR
+#define PINF_RECUR_XR 1     // C4's B = 256: eight waves and the extra row split by classes (k_pinf_recur_xr)
+#endif
+#ifndef PINF_RECUR_G
+#define PINF_RECUR_G 4      // lanes per row pair when split (2 or 4)
+#endif
 
 __device__ __forceinline__ double p_t1(const double *nuv, const double *dfi, int M, double dt) {
   double t = 0.0;
@@ -181,6 +199,33 @@ __device__ __forceinline__ void glds_copy(const void *gsrc, void *ldst, int byte
           (__attribute__((address_space(3))) void *)((char *)ldst + off), 16, 0, 0);
   }
 }
+// a wave-uniform pointer as an SGPR pair (the "s" operand of an LDS-DMA needs it provably)
+__device__ __forceinline__ const void *pi_uniform(const void *p) {
+  const unsigned long long x = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x), hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
+  return (const void *)(((unsigned long long)hi << 32) | lo);
+}
+typedef unsigned int pi_u32x2 __attribute__((ext_vector_type(2)));
+
+// glds_copy as inline asm (M0 saved and restored): the compiler does not see these LDS writes, so it does not make
+// every later LDS read wait for ALL outstanding vector-memory operations (the recursions' streamed R stores among
+// them: a store round trip per step); the callers complete them explicitly (vm_drain, then a barrier or, in one
+// wave, program order) before the first read of the copy
+__device__ __forceinline__ void glds_copy_asm(const void *gsrc_, void *ldst, int bytes, int tid, int nthreads) {
+  const int wave = tid >> 6, lane = tid & 63, nw = (nthreads + 63) >> 6;
+  const void *gsrc = pi_uniform(gsrc_);
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)ldst);
+  for (int off = wave * 1024; off < bytes; off += nw * 1024) {
+    if (off + lane * 16 < bytes) {
+      const unsigned m0 = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)off), voff = (unsigned)(off + lane * 16);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(voff), "s"(gsrc), "s"(m0)
+                   : "memory");
+    }
+  }
+}
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -249,14 +294,14 @@ __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P
   }
   if (nt < 2) return;
   int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
-  glds_copy(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, (int)threadIdx.x, (int)blockDim.x);
+  glds_copy_asm(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, (int)threadIdx.x, (int)blockDim.x);
   vm_drain();
   lds_barrier();
   for (int q = 0; hi >= 0; ++q) {
     const double *Kc = Kbuf + (size_t)(q & 1) * CH * BWP;
     const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
     if (nhi >= 0)
-      glds_copy(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
+      glds_copy_asm(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
                 (int)threadIdx.x, (int)blockDim.x);
     for (int i = hi; i >= lo; --i) {
       PI_T(t0);
@@ -361,14 +406,14 @@ __global__ __launch_bounds__(NW * 64) void k_pinf_recur_xr(ProblemDev P, PinfDev
   // R_{i+1}[E] for wave 0's classes (b = 0 reads row E itself): the terminal value first
   double rE = E < BWP ? kmin[(size_t)(nt - 1) * BWP + E] : INFINITY;
   int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
-  glds_copy(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, (int)threadIdx.x, (int)blockDim.x);
+  glds_copy_asm(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, (int)threadIdx.x, (int)blockDim.x);
   vm_drain();
   lds_barrier();
   for (int q = 0; hi >= 0; ++q) {
     const double *Kc = Kbuf + (size_t)(q & 1) * CH * BWP;
     const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
     if (nhi >= 0)
-      glds_copy(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
+      glds_copy_asm(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((q + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
                 (int)threadIdx.x, (int)blockDim.x);
     for (int i = hi; i >= lo; --i) {
       const double *Ain = A + (size_t)((i + 1) & 1) * AW;
@@ -444,7 +489,142 @@ __global__ __launch_bounds__(NW * 64) void k_pinf_recur_xr(ProblemDev P, PinfDev
   }
 }
 
-// rows c_from .. RP-1 of R (beyond k_pinf_recur_xr's rows, all above B): +Inf for every step
+// Row segments on several CUs (few subproblems, classes <= 32): R_i[c] needs R_{i+1}[c - b] for b < BWP <= 32, i.e.
+// rows c-31 .. c only, so rows split into segments of 32 (one wave, one workgroup each: lane pair per row, each lane
+// half the classes) form a pipeline like k_sdt_run's: segment q runs a step once segment q-1 has published that
+// step's rows below it.  Segments hand over in chunks of CH steps: q-1 stores its rows of R (sc1 buffer stores, the
+// R array the walk reads anyway), drains, and publishes the chunk's last step (relaxed agent flag); q polls that flag
+// one chunk ahead and copies the 32 rows below its own for the next chunk's steps into its LDS ring by LDS-DMA (sc1),
+// then computes the chunk with no further waits (MI355X_MICROARCH.md, the measured-valid hand-off).  A wave needs no
+// barrier: its LDS accesses execute in order.  Every candidate is the same expression and min is exact, so R is
+// bit-identical to k_pinf_recur's.  A wait past the spin limit sets the error word and the host redoes the DP with
+// the one-workgroup kernel (check_run).
+template <int BWP, int LPR>
+__global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, int nseg, int32_t *flags,
+                                                      unsigned spin_limit) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  constexpr int CB = BWP / LPR;      // classes per lane
+  constexpr int RPS = 64 / LPR;      // rows per segment (one wave)
+  constexpr int AS = 32 + RPS;       // step array: the 32 rows below the segment, then its own
+  constexpr int CH = PINF_MC_CHUNK;  // steps per hand-off
+  static_assert(BWP >= 8 && BWP <= 32 && CB >= 2 && CB % 2 == 0 && (LPR == 2 || LPR == 4), "k_pinf_recur_mc shape");
+  const int RP = P.RP, B = P.B, nt = P.nt, K = P.K;
+  const int k = (int)blockIdx.x / nseg, q = (int)blockIdx.x - k * nseg;
+  const int lane = (int)threadIdx.x, r = lane / LPR, h = lane % LPR, c = RPS * q + r, u = r + 32;
+  constexpr int NS = 2 * CH;                     // ring of step arrays
+  double *A = sm, *Kbuf = sm + (size_t)NS * AS;  // Kbuf: [2][CH][BWP]
+  const double *kmin = D.kmin + (size_t)k * nt * BWP;
+  double *R = D.R + (size_t)k * nt * RP;
+  int32_t *done = flags + (size_t)k * nseg, *err = flags + (size_t)K * nseg;
+  const __amdgpu_buffer_rsrc_t Rr = __builtin_amdgcn_make_buffer_rsrc(R, 0, (int)((size_t)nt * RP * 8), 0x00020000);
+  auto slot = [&](int s) { return A + (size_t)(s % NS) * AS; };
+  // terminal row R_{n-1}[c'] = Kmin_{n-1}[c'] (c' < BWP), the rows below included (a function of kmin: no hand-off)
+  for (int e = lane; e < NS * AS; e += 64) A[e] = INFINITY;
+  for (int e = lane; e < AS; e += 64) {
+    const int cc = RPS * q - 32 + e;
+    slot(nt - 1)[e] = cc >= 0 && cc < BWP ? kmin[(size_t)(nt - 1) * BWP + cc] : INFINITY;
+  }
+  if (h == 0) R[(size_t)(nt - 1) * RP + c] = c <= B && c < BWP ? kmin[(size_t)(nt - 1) * BWP + c] : INFINITY;
+  if (nt < 2) return;
+  bool stop = false;
+  // the segments whose rows lie within 32 below this one (q-1, and q-2 for 16-row segments) have published step s
+  // (token nt-1-s); false past the spin limit (err set)
+  auto wait_below = [&](int s) {
+    const int need = nt - 1 - s;
+    for (int d = 1; d * RPS <= 32 && q - d >= 0; ++d) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(done + q - d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    return true;
+  };
+  // the 32 rows below the segment (R_s[RPS·q-32 .. RPS·q-1], rows < 0 stay +Inf) for steps s in [s0, s1] into their
+  // ring slots: lane l moves rows RPS·q-32+2l, +1 (16 bytes, LDS-DMA, sc1)
+  auto halo = [&](int s0, int s1) {
+    if (q == 0) return;
+    const int row = RPS * q - 32 + 2 * lane;
+    for (int s = s0; s <= s1; ++s) {
+      if (lane < 16 && row >= 0) {
+        const void *g = pi_uniform(R + (size_t)s * RP);
+        const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)slot(s)));
+        const unsigned voff = 8u * (unsigned)row;
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 sc1\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(g), "s"(m0)
+                     : "memory");
+      }
+    }
+  };
+  int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
+  glds_copy_asm(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, lane, 64);
+  if (lo + 1 <= nt - 2) {  // the first chunk's rows below (step nt-1's are computed above)
+    stop = !wait_below(lo + 1);
+    halo(lo + 1, nt - 2);
+  }
+  vm_drain();
+  for (int qq = 0; hi >= 0 && !stop; ++qq) {
+    const double *Kc = Kbuf + (size_t)(qq & 1) * CH * BWP;
+    const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
+    if (nhi >= 0) {  // the next chunk: its class rows, and (once the segments below have them) its rows below
+      glds_copy_asm(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((qq + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8, lane, 64);
+      if (!wait_below(nlo + 1)) {
+        stop = true;
+        break;
+      }
+      halo(nlo + 1, nhi + 1);
+    }
+    // this lane's class values of a step (read one step ahead: they are not on the recursion's chain)
+    auto kload = [&](double (&kv)[CB], int i) {
+      const double2 *kr = reinterpret_cast<const double2 *>(Kc + (size_t)(i - lo) * BWP + CB * h);
+#pragma unroll
+      for (int t = 0; t < CB / 2; ++t) {
+        const double2 y = kr[t];
+        kv[2 * t] = y.x;
+        kv[2 * t + 1] = y.y;
+      }
+    };
+    double kv[CB];
+    kload(kv, hi);
+    for (int i = hi; i >= lo; --i) {
+      asm volatile("" ::: "memory");
+      double kn[CB];
+      if (i > lo) kload(kn, i - 1);
+      const double *Ain = slot(i + 1) + u - CB * h - (CB - 1);  // R_{i+1}[c - CB·h - (CB-1) .. c - CB·h]
+      double wv[CB];
+#pragma unroll
+      for (int t = 0; t < CB; ++t) wv[t] = Ain[t];
+      double m[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+#pragma unroll
+      for (int bb = 0; bb < CB; ++bb) m[bb & 3] = pvmin(m[bb & 3], kv[bb] + wv[CB - 1 - bb]);
+      double rv = pvmin(pvmin(m[0], m[1]), pvmin(m[2], m[3]));
+      rv = pvmin(rv, pv_dpp<0xB1>(rv));                      // the lane group's other class parts
+      if constexpr (LPR == 4) rv = pvmin(rv, pv_dpp<0x4E>(rv));
+      if (h == 0) {
+        slot(i)[u] = rv;
+        const double out = c <= B ? rv : INFINITY;
+        __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(out), (unsigned)__double2hiint(out)},
+                                              Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
+      }
+      if (i > lo) {
+#pragma unroll
+        for (int t = 0; t < CB; ++t) kv[t] = kn[t];
+      }
+    }
+    // this chunk's rows have landed: publish its last step for the segments above
+    vm_drain();
+    if (lane == 0) __hip_atomic_store(done + q, nt - 1 - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hi = nhi;
+    lo = nlo;
+  }
+}
+
+// rows c_from .. RP-1 of R (beyond the rows k_pinf_recur_xr / _mc compute, all above B): +Inf for every step
 __global__ void k_pinf_rfill(ProblemDev P, PinfDev D, int c_from) {
   const int k = blockIdx.y, RP = P.RP, nt = P.nt, n = RP - c_from;
   double *R = D.R + (size_t)k * nt * RP;
@@ -453,17 +633,31 @@ __global__ void k_pinf_rfill(ProblemDev P, PinfDev D, int c_from) {
 }
 
 int pinf_chunk_recur(int BWP) { return BWP <= 16 ? 64 : 32; }
-#ifndef PINF_RECUR_SPLIT
-#define PINF_RECUR_SPLIT 1  // few subproblems: G lanes per row pair (A/B builds: 0)
-#endif
-#ifndef PINF_RECUR_XR
-#define PINF_RECUR_XR 1     // C4's B = 256: eight waves and the extra row split by classes (k_pinf_recur_xr)
-#endif
-#ifndef PINF_RECUR_G
-#define PINF_RECUR_G 4      // lanes per row pair when split (2 or 4)
-#endif
 
-hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ncu) {
+int pinf_recur_segments(const ProblemDev &P) { return (P.B + 1 + 64 / PINF_RECUR_MC_LANES - 1) / (64 / PINF_RECUR_MC_LANES); }
+
+hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ncu, int32_t *flags,
+                             unsigned spin_limit, bool *segmented) {
+  if (segmented) *segmented = false;
+  // few subproblems, classes <= 32, tall enough: row segments of 32 on several CUs (k_pinf_recur_mc); the flags
+  // (K·nseg + 1 words, zeroed by the caller) carry the hand-off and the error word
+  {
+    constexpr int LPR = PINF_RECUR_MC_LANES, RPS = 64 / LPR;  // lanes per row, rows per segment
+    const int nseg = (P.B + 1 + RPS - 1) / RPS;
+    if (PINF_RECUR_MC && flags && segmented && D.BWP >= 2 * LPR && D.BWP <= 32 && nseg >= 3 && P.K * nseg <= ncu &&
+        RPS * nseg <= P.RP && (size_t)P.nt * P.RP * 8 < (1ull << 31)) {
+      constexpr int CH = PINF_MC_CHUNK;
+      const size_t lds = (size_t)(2 * CH * (32 + RPS) + 2 * CH * D.BWP) * sizeof(double);
+      if (RPS * nseg < P.RP) hipLaunchKernelGGL(k_pinf_rfill, dim3(64, P.K), dim3(256), 0, s, P, D, RPS * nseg);
+      switch (D.BWP) {
+        case 8: hipLaunchKernelGGL((k_pinf_recur_mc<8, LPR>), dim3(P.K * nseg), dim3(64), lds, s, P, D, nseg, flags, spin_limit); break;
+        case 16: hipLaunchKernelGGL((k_pinf_recur_mc<16, LPR>), dim3(P.K * nseg), dim3(64), lds, s, P, D, nseg, flags, spin_limit); break;
+        default: hipLaunchKernelGGL((k_pinf_recur_mc<32, LPR>), dim3(P.K * nseg), dim3(64), lds, s, P, D, nseg, flags, spin_limit); break;
+      }
+      *segmented = true;
+      return hipGetLastError();
+    }
+  }
   int pairs = ((P.RP / 2 + 63) / 64) * 64;  // one thread (G = 1) or lane quad (G = 4) per two budget rows
   if (pairs > 512) pairs = 512;
   // few subproblems (fewer workgroups than a quarter of the CUs): four lanes per row pair; a batch keeps one lane

@@ -12,6 +12,7 @@
 #   exe:path[,args]    a binary built in this container (e.g. scripts/ubench/pass_occ)
 #   with:VAR=value     export VAR for the steps that follow (e.g. with:MIOC_LIB=<a variant build>)
 #   pyprof:script[,args]  rocprofv3 --kernel-trace --stats over python scripts/<script> args -> pyprof/
+#   pypmc:c1+c2:script[,args]  ONE rocprofv3 --pmc pass over python scripts/<script> args -> pypmc<n>/
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:?usage: gpu.sh <out> <step>...}
@@ -53,6 +54,12 @@ for step in "$@"; do
     py)
       timeout -k 10 600 python -u scripts/$args > "$log" 2>&1
       rc=$?; tail -40 "$log" ;;
+    pypmc)
+      ctr=${rest%%:*}
+      sargs=${rest#*:}
+      timeout -s KILL 300 rocprofv3 --pmc ${ctr//+/ } -d "$O/pypmc$n" -o pmc --output-format csv \
+        -- python3 scripts/${sargs//,/ } > "$log" 2>&1
+      rc=$?; tail -3 "$log"; find "$O/pypmc$n" -name "*counter_collection.csv" ;;
     pyprof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/pyprof$n" -o prof --output-format csv \
         -- python3 scripts/$args > "$log" 2>&1
