@@ -421,7 +421,7 @@ def pmc_valu_of(kernel, avg_s, steps):
         if not files:
             return None
         path = max(files, key=lambda f: int(re.search(r"round(\d+)_", os.path.basename(f)).group(1)))
-        how = "committed pass of this round's final build (duration-matched)"
+        how = "committed PMC pass (not this run; its dispatches are matched to this line's kernel time within 20 %)"
     per = {}
     with open(path) as fh:
         for r in csv.DictReader(fh):
