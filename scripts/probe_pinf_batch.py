@@ -1,6 +1,7 @@
 """p=Inf collapse on K restarts (C2 / C3 shapes): per-kernel times of bellman (prep + recursion) and backtrack
-(start + walk), whole-batch wall time, subproblems/s.  python probe_pinf_batch.py CFG K [K ...]"""
-import os, sys, time
+(start + walk), whole-batch wall time, subproblems/s, and a digest of u / Φ* (equal across library builds; MIOC_LIB
+selects one).  python probe_pinf_batch.py CFG K [K ...]"""
+import hashlib, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")); sys.path.insert(0, ROOT)
 import numpy as np
@@ -29,6 +30,7 @@ for K in [int(x) for x in sys.argv[2:]]:
         ctx.synchronize()
         walls.append(time.perf_counter() - t0)
     st = [ctx.kernel_stats(w) for w in (0, 2, 1)]
-    print(f"{sys.argv[1]} K={K}: wall {min(walls) * 1e3:.2f} ms -> {K / min(walls):.1f} subproblems/s | " +
+    dg = hashlib.sha256(du.cpu().numpy().tobytes() + dphi.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(f"{os.path.basename(os.environ.get('MIOC_LIB', 'libmioc.so'))} {sys.argv[1]} K={K} digest {dg}: wall {min(walls) * 1e3:.2f} ms -> {K / min(walls):.1f} subproblems/s | " +
           " | ".join(f"{n} {ms:.2f} ms/{c}" for ms, c, n in st), flush=True)
     ctx.close()
