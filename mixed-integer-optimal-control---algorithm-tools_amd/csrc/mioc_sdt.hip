@@ -75,9 +75,6 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_SPREAD
 #define SDT_SPREAD 0                     // persistent driver: the next row's loads issued between the passes (SdPipe; measured slower)
 #endif
-#ifndef SDT_WIDE
-#define SDT_WIDE 0                       // 8^4: the persistent driver's 1024-thread row body (k_sdt_run_wide)
-#endif
 #ifndef SDT_BF
 #define SDT_BF 1                         // row body: straddle pairs and +Inf stamps without branches (in-wave LDS order)
 #endif
@@ -1071,7 +1068,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
 template <int M, bool SC1>
 __device__ __forceinline__ void sd_issue_loads(double (&v)[8], const uint32_t *pin, int cp, const double *Sin,
                                                int sbytes, const double *r0) {
-  constexpr int L = 1 << (3 * M), T = L / 8;
+  constexpr int L = 1 << (3 * M);
   const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -1143,7 +1140,7 @@ __device__ __forceinline__ void sdt_row0(const ProblemDev &P, const LevelsDev &L
                                          const double *Sin_all, double *Sout_all, uint16_t *__restrict__ UU_all,
                                          size_t s_stride, size_t uu_stride_k, const int *lb_g, int32_t *loaded,
                                          int token) {
-  constexpr int L = 1 << (3 * M), T = L / 8;
+  constexpr int L = 1 << (3 * M);
   const int tid = threadIdx.x, B = P.B;
   const double beta = Lv.beta;
   const double *Sin = Sin_all + (size_t)k * s_stride;
@@ -1464,7 +1461,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_row0(ProblemDev P, Lev
                                                             const double *__restrict__ V, double *__restrict__ S_all,
                                                             size_t kstride, size_t r0off, uint16_t *__restrict__ UU_all,
                                                             size_t uu_stride_k) {
-  constexpr int L = 1 << (3 * M), T = L / 8;
+  constexpr int L = 1 << (3 * M);
   const int i = (int)blockIdx.x, k = (int)blockIdx.y, tid = threadIdx.x, nt = P.nt, B = P.B;
   const uint32_t *pi = perm_all + ((size_t)k * nt + i) * L;
   const bool term = i == nt - 1;
@@ -1921,593 +1918,6 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   SD_TL_FLUSH(h.g0);
 }
 
-// ---- the 1024-thread persistent driver for 8^4 grids (SDT_WIDE) ---------------------------------------------
-// k_sdt_run's row body with four values per lane instead of eight: 16 waves, four per SIMD, so that one wave's
-// latencies (LDS round trips, the statistics chains, barrier skew) hide behind three other waves instead of one.
-//   * Lane pair (2l, 2l+1) owns pass line l (512 lines per pass): lane 2l holds x = 0..3 of the line, lane 2l+1
-//     x = 7..4 (mirrored), so the cross-half step of every pass is one DPP swap (quad_perm [1,0,3,2]) and one merge at
-//     cost 1: 3 + 1 + 3 merges per lane, 14 per line as before, and any binary merge tree certifies (§3.5).
-//   * Position pairs 2(tid + 1024q) + {0, 1}, q = 0, 1 (two 16-byte loads and two 8-byte straddle loads per lane);
-//     targets l | x << 9 for the lane's four x; three stores per lane (two Φ pairs, four U entries), so the row's
-//     counted wait is vmcnt(3).
-//   * Passes 0 and 1 stay wave-local (a wave's 32 lines of either pass cover one block of 256 ranks); pass 2's lines
-//     span two such blocks, so a workgroup barrier follows pass 1 as well as pass 2.
-// The hand-off protocol, the pipeline order and every value are those of k_sdt_run (the C4 fixture and parity tests
-// run with either driver).
-namespace {
-constexpr int SW_L = 4096, SW_T = 1024, SW_NW = 16;
-constexpr size_t sw_slot_offset() { return sd_slot_offset<4>(); }
-constexpr size_t sw_dfuo_offset() { return sw_slot_offset() + 2 * (size_t)SW_L * sizeof(uint32_t); }
-constexpr size_t sw_out_offset() { return sw_dfuo_offset() + ((sd_dfuo_stride<4>() * SW_NW + 255) & ~(size_t)255); }
-constexpr size_t sw_lds_total() { return sw_out_offset() + (size_t)SW_L * sizeof(double); }
-
-struct SwRaw {
-  sd_u32x4 a[2];
-  sd_u32x2 b[2];
-  uint2 e[2];
-  unsigned mask;  // per pair q: bit 3q the first element has no source row, 3q+1 the second, 3q+2 it straddles
-};
-__device__ __forceinline__ int sw_p2(int tid, int q) { return 2 * (tid + SW_T * q); }
-__device__ __forceinline__ void sw_issue(SwRaw &w, __amdgpu_buffer_rsrc_t rs, const uint32_t *pin, int cp,
-                                         unsigned boff, unsigned r0, unsigned rowb) {
-  const int tid = threadIdx.x;
-  uint2 e[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) e[q] = *reinterpret_cast<const uint2 *>(pin + sw_p2(tid, q));
-  constexpr unsigned OOB = 0xFFFFFFF0u;
-  unsigned oa[2], ob[2], mask = 0;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int p2 = sw_p2(tid, q);
-    const int ra = cp - (int)(e[q].x >> 16), rb = cp - (int)(e[q].y >> 16);
-    oa[q] = ra >= 1 ? boff + (unsigned)ra * rowb + (unsigned)p2 * 8u : ra == 0 ? r0 + (unsigned)p2 * 8u : OOB;
-    ob[q] = rb == ra ? OOB
-            : rb >= 1 ? boff + (unsigned)rb * rowb + (unsigned)(p2 + 1) * 8u
-            : rb == 0 ? r0 + (unsigned)(p2 + 1) * 8u
-                      : OOB;
-    mask |= ((unsigned)(ra < 0) | (unsigned)(rb < 0) << 1 | (unsigned)(ra != rb) << 2) << (3 * q);
-  }
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa[q], 0, 16);
-    w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob[q], 0, 16);
-    w.e[q] = e[q];
-  }
-  w.mask = mask;
-}
-__device__ __forceinline__ void sw_take(double (&v)[4], const SwRaw &w) {
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const unsigned m = w.mask >> (3 * q);
-    const double a0 = __hiloint2double((int)w.a[q].y, (int)w.a[q].x);
-    const double a1 = __hiloint2double((int)w.a[q].w, (int)w.a[q].z);
-    const double b1 = __hiloint2double((int)w.b[q].y, (int)w.b[q].x);
-    v[2 * q] = (m & 1) ? INFINITY : a0;
-    v[2 * q + 1] = (m & 2) ? INFINITY : (m & 4) ? b1 : a1;
-  }
-}
-// one step's sphere order (16 KB) into an LDS slot: one 1 KiB LDS-DMA chunk per wave (as sd_perm_dma_asm)
-// a wave-uniform pointer as an SGPR pair (readfirstlane of both halves: the "s" operands below need it provably)
-__device__ __forceinline__ const void *sw_uniform(const void *p) {
-  const unsigned long long x = (unsigned long long)p;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x), hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
-  return (const void *)(((unsigned long long)hi << 32) | lo);
-}
-// (the global address as a uniform SGPR base plus a 32-bit lane offset: no 64-bit VGPR address to keep live)
-__device__ __forceinline__ void sw_perm_dma(const uint32_t *src_, uint32_t *slot) {
-  const void *src = sw_uniform(src_);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const unsigned voff = (unsigned)(wave * 1024 + lane * 16);
-  const unsigned m0 = __builtin_amdgcn_readfirstlane(
-      (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)slot) + (unsigned)wave * 1024u);
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(src), "s"(m0)
-               : "memory");
-}
-// df(:, s), u_old(:, s) and the reuse flag into this wave's LDS words (as sd_dfuo_dma)
-// (three LDS-DMA dword loads with uniform SGPR bases, exec-masked by lane: lane l lands at M0 + 4l in every one)
-__device__ __forceinline__ void sw_dfuo_dma(const double *df, const double *uo, const int32_t *flag, unsigned char *sds) {
-  constexpr int M = 4;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const unsigned m0 = __builtin_amdgcn_readfirstlane(
-      (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)(sds + sw_dfuo_offset())) +
-      wave * (unsigned)sd_dfuo_stride<M>());
-  auto dma = [&](const void *base_, unsigned voff) {
-    const void *base = sw_uniform(base_);
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(base), "s"(m0)
-                 : "memory");
-  };
-  if (lane < 2 * M)
-    dma(df, 4u * (unsigned)lane);
-  else if (lane < 4 * M)
-    dma(uo, 4u * (unsigned)(lane - 2 * M));
-  else if (lane == 4 * M && flag)
-    dma(flag, 0u);
-}
-// the exact scan of the listed targets at 1024 threads (as sd_scan: the reference loop, ties to the lower rank)
-template <bool COOP>
-__device__ __forceinline__ void sw_scan(const uint16_t *list, int nl, const double *psi, const double *a,
-                                        const int *base, double beta, uint16_t *UU, double *outnat, double *redv,
-                                        int *redj) {
-  constexpr int M = 4, L = SW_L, T = SW_T, NW = SW_NW;
-  const int tid = sd_tid(), lane = tid & 63, w = tid >> 6;
-  auto target = [&](int r, int *xl) {
-    double t1 = 0.0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      xl[m] = (r >> (3 * m)) & 7;
-      t1 = t1 + a[m] * (double)(base[m] + xl[m]);  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
-    }
-    return t1;
-  };
-  auto wave_min = [&](double &bv, int &bj) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double ov = __shfl_xor(bv, off);
-      const int oj = __shfl_xor(bj, off);
-      if (oj >= 0 && (bj < 0 || ov < bv || (ov == bv && oj < bj))) {
-        bv = ov;
-        bj = oj;
-      }
-    }
-  };
-  if constexpr (COOP) {
-    for (int e = 0; e < nl; ++e) {
-      const int r = list[e];
-      int xl[M];
-      const double t1 = target(r, xl);
-      // sources j = tid + 1024·s: the low three coordinates from tid & 511, the top one (tid >> 9) + 2s
-      const unsigned dpre = sd_l1(sd_bytes(tid & 511), sd_bytes(r & 511));
-      double bv = INFINITY;
-      int bj = -1;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int j = tid + T * s;
-        const double val = (t1 + beta * (double)(dpre + (unsigned)abs((tid >> 9) + 2 * s - xl[M - 1]))) + psi[j];
-        if (val < bv) {
-          bv = val;
-          bj = j;
-        }
-      }
-      wave_min(bv, bj);
-      if (lane == 0) {
-        redv[e * NW + w] = bv;
-        redj[e * NW + w] = bj;
-      }
-    }
-    sd_bar();
-    if (tid < nl) {
-      double bv = INFINITY;
-      int bj = -1;
-      for (int q = 0; q < NW; ++q) {
-        const double ov = redv[tid * NW + q];
-        const int oj = redj[tid * NW + q];
-        if (oj >= 0 && (bj < 0 || ov < bv || (ov == bv && oj < bj))) {
-          bv = ov;
-          bj = oj;
-        }
-      }
-      const int r = list[tid];
-      if (bj >= 0) UU[r] = (uint16_t)bj;
-      outnat[r] = bj >= 0 ? bv : INFINITY;
-    }
-  } else {
-    for (int e = w; e < nl; e += NW) {
-      const int r = list ? (int)list[e] : e;
-      if (!list && !__builtin_isnan(outnat[r])) continue;  // overflowed list: every NaN-marked rank
-      int xl[M];
-      const double t1 = target(r, xl);
-      const unsigned pr = sd_bytes(r);
-      double bv = INFINITY;
-      int bj = -1;
-      for (int t = 0; t < L / 64; ++t) {
-        const int j = lane + 64 * t;
-        const unsigned d = sd_l1(sd_bytes(j), pr);
-        const double val = (t1 + beta * (double)d) + psi[j];
-        if (val < bv) {
-          bv = val;
-          bj = j;
-        }
-      }
-      wave_min(bv, bj);
-      if (lane == 0) {
-        if (bj >= 0) UU[r] = (uint16_t)bj;
-        outnat[r] = bj >= 0 ? bv : INFINITY;
-      }
-    }
-  }
-}
-}  // namespace
-
-__global__ __launch_bounds__(1024, 1) void k_sdt_run_wide(ProblemDev P, LevelsDev Lv, PyrGeom G,
-                                                         const uint32_t *__restrict__ perm_all, double *S_all,
-                                                         size_t kstride, int NB, uint16_t *__restrict__ UU_all,
-                                                         size_t uu_stride_k, int32_t *__restrict__ counters,
-                                                         int32_t *flags, int nwg, unsigned spin_limit,
-                                                         const double *__restrict__ df_all,
-                                                         const double *__restrict__ uo_all,
-                                                         const int32_t *__restrict__ same2) {
-  constexpr int M = 4, L = SW_L, T = SW_T, NW = SW_NW, Smax = 7 * M;
-  extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
-  __shared__ SdtShared<NW> sh;
-  const int B = P.B, R = B + 1, nt = P.nt, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int32_t *done = flags, *loaded = flags + P.K * R, *err = flags + 2 * P.K * R;
-  const int W = nwg / P.K;  // workgroups per subproblem (the host guarantees 1 <= W <= B)
-  const int k = (int)blockIdx.x / W, wl = (int)blockIdx.x - k * W;
-  if (k >= P.K) return;
-  const int base_ = B / W, extra = B - base_ * W;  // rows 1..B, the longer chunks highest
-  const int lo = 1 + wl * base_ + max(0, wl - (W - extra)), hi = lo + base_ + (wl >= W - extra ? 1 : 0);
-  double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
-  double *dtv = psi + L;                                // [L] transform values (swizzled)
-  uint16_t *uu = reinterpret_cast<uint16_t *>(dtv + L);  // [L] the U row (natural order)
-  uint16_t *list = uu + L;                              // [SD_LCAP] targets for the exact scan
-  uint32_t *slot = reinterpret_cast<uint32_t *>(sds + sw_slot_offset());
-  double *outv = reinterpret_cast<double *>(sds + sw_out_offset());  // [L] the outputs (natural order)
-  auto pslot = [&](int step) { return slot + (step & 1) * L; };
-  double *reg = S_all + (size_t)k * kstride;
-  const unsigned rowb = (unsigned)L * 8u, bufb = (unsigned)R * rowb, r0b = (unsigned)NB * bufb;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(r0b + (unsigned)nt * rowb), 0x00020000);
-  int32_t *dk = done + (size_t)k * R, *lk = loaded + (size_t)k * R;
-  const uint32_t *pk = perm_all + (size_t)k * nt * L;
-  const int g0 = k * R + lo;
-  (void)g0;
-  if (tid == 0) {
-    sh.stop = 0;
-    sh.cnt[0] = sh.cnt[1] = 0;
-  }
-  // prologue: both sphere orders of the first step, df / u_old, the first row's loads
-  sw_perm_dma(pk + (size_t)(nt - 1) * L, pslot(nt - 1));
-  sw_perm_dma(pk + (size_t)(nt - 2) * L, pslot(nt - 2));
-  sw_dfuo_dma(df_all + ((size_t)k * nt + nt - 2) * M, uo_all + ((size_t)k * nt + nt - 2) * M,
-              nt >= 3 ? same2 + (size_t)k * nt + nt - 3 : nullptr, sds);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  sd_bar();
-  SwRaw raw;
-  sw_issue(raw, rs, pslot(nt - 1), lo, (unsigned)((nt - 1) % NB) * bufb, r0b + (unsigned)(nt - 1) * rowb, rowb);
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), as k_sdt_run's prologue
-  const double beta = Lv.beta, inv = Lv.inv_beta;
-  int status = 0, pcp = -1, pi = 0;
-  bool stop = false;
-#pragma nounroll
-  for (int i = nt - 2; i >= 0 && !stop; --i) {
-#pragma nounroll
-    for (int cp = lo; cp < hi && !stop; ++cp) {
-      const bool last_row = cp + 1 == hi;
-      const int ncp = last_row ? lo : cp + 1, ni = last_row ? i - 1 : i;
-      const bool has_next = ni >= 0;
-      SD_TL_AT(cp == lo ? g0 : 1 << 30, i, nt, 0);
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // this row's loads and DMAs; the previous row's 3 stores may fly
-      double v[4];
-      sw_take(v, raw);
-      SD_TL_AT(cp == lo ? g0 : 1 << 30, i, nt, 7);
-      // the distance-0 source of a one-row workgroup: its own output of the previous row, still in LDS
-      if (hi - lo == 1 && pcp >= 0 && tid == 0 && (raw.e[0].x >> 16) == 0)
-        v[0] = status == 1 ? INFINITY : outv[raw.e[0].x & 0xFFFFu];
-      uint2 ein[2] = {raw.e[0], raw.e[1]};
-      // ======================================= the row body ==========================================
-      const int ot = sd_tid(), line = ot >> 1, hf = ot & 1;
-      const double *dfi = reinterpret_cast<const double *>(sds + sw_dfuo_offset()) + (2 * M + 2) * w;
-      const double *uoi = dfi + M;
-      double a[M];
-      int lb[M], uo[M];
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        a[m] = P.dt * dfi[m];
-        lb[m] = G.base[m];
-        uo[m] = __builtin_amdgcn_readfirstlane((int)uoi[m]);
-      }
-      double pre = 0.0;
-      int bpre = 0;
-#pragma unroll
-      for (int m = 0; m < M - 1; ++m) {
-        const int nu = lb[m] + ((line >> (3 * m)) & 7);
-        pre = pre + a[m] * (double)nu;  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
-        bpre += abs(nu - uo[m]);
-      }
-      int xs[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) xs[s] = hf ? 7 - s : s;
-      unsigned valid = 0;
-      int nv = 0;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bool in = bpre <= B - cp - abs(lb[M - 1] + xs[s] - uo[M - 1]);
-        valid |= (unsigned)in << s;
-        nv += __popcll(__ballot(in));
-      }
-      double qa = beta * (double)Smax;
-#pragma unroll
-      for (int m = 0; m < M; ++m) qa += fabs(a[m]) * (double)max(abs(lb[m]), abs(lb[m] + 7));
-      double ref, base, g, tol;
-      bool scale_ok;
-      auto scale = [&](double lo_, double hi_) {
-        const double rsc = (hi_ - lo_) * inv + (double)Smax;
-        scale_ok = rsc < 0x1p31;
-        const int E = ilogb(fmin(rsc, 0x1p31) * (1.0 + 0x1p-20) + 1.0) + 2;
-        base = ldexp(1.0, E);
-        g = ldexp(1.0, E - SD_GRID);
-        tol = 3.0 * g + 0x1p-49 * (qa + fmax(fabs(lo_), fabs(hi_))) * inv;
-        ref = lo_;
-      };
-      auto stamp = [&](double x, int j) {
-        const double y = (x - ref) * inv + base;
-        return __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | (j << SD_CB));
-      };
-      auto stamp_inf = [&](double x, int j) {
-        const double y = stamp(x, j);
-        const unsigned m = x < INFINITY ? ~0u : 0u;
-        return __hiloint2double((int)(((unsigned)__double2hiint(y) & m) | (0x7FF00000u & ~m)),
-                                (int)((unsigned)__double2loint(y) & m));
-      };
-      // ---- Ψ by rank, the row's range and counts ----
-      double pmn = INFINITY, pmx = -INFINITY;
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const double x = v[2 * q + hh];
-          psi[(hh ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
-          const bool fin = x < INFINITY;
-          nv += __popcll(__ballot(fin)) << 16;
-          pmn = sd_min(pmn, x);
-          pmx = sd_max(pmx, __hiloint2double(fin ? __double2hiint(x) : (int)0xFFF00000, __double2loint(x)));
-        }
-      sd_wave_stats(pmn, pmx);
-      if (lane == 0) {
-        sh.rmn[w] = pmn;
-        sh.rmx[w] = pmx;
-        sh.rnv[w] = nv;
-      }
-      sd_bar();
-      // (every wave has left the previous row, including its read of the scan-list length)
-      if (tid == 0) sh.nlist = 0;
-      // ---- early(): `loaded` is published in go(); this wave's dependency polls ----
-      SD_TL_AT(cp == lo ? g0 : 1 << 30, i, nt, 1);
-      int32_t *fp = lk + cp;
-      int need = INT32_MIN;
-      {
-        const int s = lane < 32 ? lane + 1 : lane - 31;
-        if (lane < 32) {
-          const int r = ncp - s;
-          if (has_next && s <= 7 * M && r >= 1 && r < lo && nt - 2 - ni > 0) {
-            fp = dk + r;
-            need = nt - 2 - ni;  // token(ni + 1)
-          }
-        } else {
-          const int r = cp + s;
-          if (s <= 7 * M && r <= B && r >= hi && nt - i - NB > 0) {
-            fp = lk + r;
-            need = nt - i - NB;  // token(i + NB - 1)
-          }
-        }
-      }
-      int val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        pmn = sd_min(pmn, sh.rmn[q]);
-        pmx = sd_max(pmx, sh.rmx[q]);
-      }
-      nv = 0;
-#pragma unroll
-      for (int q = 0; q < NW; ++q) nv += sh.rnv[q];
-      const int nf = nv >> 16;
-      nv &= 0xFFFF;
-      const bool empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || !(pmn < INFINITY))) != 0;
-      scale(pmn, pmx);
-      const bool sparse = !empty && nf <= SD_SPARSE;
-      const bool direct = !empty && !sparse && (nv <= SD_FEW || !scale_ok || !(tol < base * 0x1p-20));
-      int spj[SD_SPARSE];
-      double spv[SD_SPARSE];
-      if (sparse) {
-        if (tid == 0) sh.nsp = 0;
-        sd_bar();
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh)
-            if (v[2 * q + hh] < INFINITY) {
-              const int e = atomicAdd(&sh.nsp, 1);
-              sh.spj[e] = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
-              sh.spv[e] = v[2 * q + hh];
-            }
-        sd_bar();
-#pragma unroll
-        for (int e = 0; e < SD_SPARSE; ++e) {
-          spj[e] = sh.spj[e];
-          spv[e] = sh.spv[e];
-        }
-      }
-      const bool transform = !direct && !empty && !sparse;
-      if (transform) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
-            dtv[sd_swz(j)] = stamp_inf(v[2 * q + hh], j);
-          }
-      }
-      sd_bar();
-      // ---- go(): `loaded`, the polls matched, the next row's loads, sphere order and df / u_old ----
-      SD_TL_AT(cp == lo ? g0 : 1 << 30, i, nt, 2);
-      {
-        bool ready = __all(val >= need);
-        if (tid == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned spins = 0;
-        while (!ready) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
-            if (lane == 0) {
-              __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              sh.stop = 1;
-            }
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ready = __all(val >= need);
-        }
-      }
-      SD_TL_AT(cp == lo ? g0 : 1 << 30, i, nt, 3);
-      if (has_next) {
-        const int same = *reinterpret_cast<const volatile int32_t *>(sds + sw_dfuo_offset() + w * sd_dfuo_stride<M>() +
-                                                                      16 * M);
-        sw_issue(raw, rs, slot + ((ni + 1) & 1) * L, ncp, (unsigned)((ni + 1) % NB) * bufb,
-                 r0b + (unsigned)(ni + 1) * rowb, rowb);
-        if (ni != i && !(SDT_PERM_SKIP && same)) sw_perm_dma(pk + (size_t)ni * L, slot + (ni & 1) * L);
-        sw_dfuo_dma(df_all + ((size_t)k * nt + ni) * M, uo_all + ((size_t)k * nt + ni) * M,
-                    ni >= 1 ? same2 + (size_t)k * nt + ni - 1 : nullptr, sds);
-      }
-      SD_TL_AT(cp == lo ? g0 : 1 << 30, i, nt, 4);
-      // ---- the passes: lane pair per line, four values per lane ----
-      double o[4];
-      if (transform) {
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-          int pos[4];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            pos[s] = sd_swz(sd_rank(line, m, xs[s]));
-            o[s] = dtv[pos[s]];
-          }
-#pragma unroll
-          for (int s = 1; s < 4; ++s) o[s] = sd_merge(o[s], o[s - 1] + 1.0, tol);
-          // the partner's slot 3 (the other half's sweep end, one unit away)
-          const double pb = __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(o[3]), 0xB1, 0xF, 0xF, true),
-                                             __builtin_amdgcn_mov_dpp(__double2loint(o[3]), 0xB1, 0xF, 0xF, true));
-          o[3] = sd_merge(o[3], pb + 1.0, tol);
-#pragma unroll
-          for (int s = 2; s >= 0; --s) o[s] = sd_merge(o[s], o[s + 1] + 1.0, tol);
-          if (m + 1 < M) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) dtv[pos[s]] = o[s];
-            if (m == 0)
-              sd_wave_sync();
-            else
-              sd_bar();
-          }
-        }
-      }
-      if (!empty) {
-        unsigned listed = 0;
-        if (!direct && !sparse) {
-          int jx[4];
-          double pv[4];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) jx[s] = (__double2loint(o[s]) >> SD_CB) & ((1 << SD_RB) - 1);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) pv[s] = psi[jx[s]];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const int r = line | (xs[s] << (3 * (M - 1))), j = jx[s];
-            const bool fin = (valid >> s & 1) && o[s] < INFINITY;
-            const bool flg = (__double2loint(o[s]) & SD_CNT) != 0;
-            const double dd = o[s] - stamp(pv[s], j);
-            const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + xs[s]);
-            const double valr = (t1 + beta * dd) + pv[s];  // R(l, j*), HelpFunctions.jl:63-71
-            listed |= (unsigned)(fin && flg) << s;
-            uu[r] = (uint16_t)(fin && !flg ? j : 0xFFFF);
-            outv[r] = fin ? (flg ? __longlong_as_double(0x7FF8000000000000ll) : valr) : INFINITY;
-          }
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const int r = line | (xs[s] << (3 * (M - 1)));
-            double ov = INFINITY;
-            int uj = 0xFFFF;
-            if (direct) {
-              listed |= valid & (1u << s);
-            } else if (valid >> s & 1) {  // sparse: the reference loop over the finite sources, ties to the lower rank
-              const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + xs[s]);
-              double bv = INFINITY;
-              int bj = 0xFFFF;
-#pragma unroll
-              for (int e = 0; e < SD_SPARSE; ++e) {
-                if (e < nf) {
-                  const int j = spj[e];
-                  const unsigned d = sd_l1(sd_bytes(j), sd_bytes((unsigned)line) | (unsigned)xs[s] << (8 * (M - 1)));
-                  const double valr = (t1 + beta * (double)d) + spv[e];
-                  if (valr < bv || (valr == bv && j < bj)) {
-                    bv = valr;
-                    bj = j;
-                  }
-                }
-              }
-              ov = bv;
-              uj = bj;
-            }
-            uu[r] = (uint16_t)uj;
-            outv[r] = (listed >> s & 1) ? __longlong_as_double(0x7FF8000000000000ll) : ov;
-          }
-        }
-        if (listed) {
-          int e = atomicAdd(&sh.nlist, __popc(listed));
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-            if (listed >> s & 1) {
-              if (e < SD_LCAP) list[e] = (uint16_t)(line | (xs[s] << (3 * (M - 1))));
-              ++e;
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // late drain: the previous row's stores have landed
-        SD_TL_AT(cp == lo ? g0 : 1 << 30, i, nt, 5);
-        sd_bar();
-        if (tid == 0 && pcp >= 0) __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pcp = cp;
-        pi = i;
-        const int nl = sh.nlist;
-        if (nl) {
-          if (nl <= SD_COOP)
-            sw_scan<true>(list, nl, psi, a, lb, beta, uu, outv, sh.redv, sh.redj);
-          else if (nl <= SD_LCAP)
-            sw_scan<false>(list, nl, psi, a, lb, beta, uu, outv, sh.redv, sh.redj);
-          else
-            sw_scan<false>(nullptr, L, psi, a, lb, beta, uu, outv, sh.redv, sh.redj);
-          sd_bar();
-          if (tid == 0) sh.cnt[direct ? 1 : 0] += nl;
-        }
-      } else {  // the row is +Inf, U unwritten
-#pragma unroll
-        for (int s = 0; s < 4; ++s) outv[line | (xs[s] << (3 * (M - 1)))] = INFINITY;
-        reinterpret_cast<unsigned long long *>(uu)[ot] = ~0ull;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        SD_TL_AT(cp == lo ? g0 : 1 << 30, i, nt, 5);
-        sd_bar();
-        if (tid == 0 && pcp >= 0) __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pcp = cp;
-        pi = i;
-      }
-      // ---- Φ_i row c' in the sphere order of u_old(i), and the U row: three stores per lane ----
-      {
-        const uint32_t *pout = pslot(i);
-        double *Sout = reg + (size_t)(i % NB) * R * L + (size_t)cp * L;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const uint2 e = *reinterpret_cast<const uint2 *>(pout + sw_p2(ot, q));
-          sd_store16<true>(Sout, L * 8, sw_p2(ot, q), __double_as_longlong(outv[e.x & 0xFFFFu]),
-                           __double_as_longlong(outv[e.y & 0xFFFFu]));
-        }
-        uint16_t *UU = UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L;
-        reinterpret_cast<unsigned long long *>(UU)[ot] = reinterpret_cast<const unsigned long long *>(uu)[ot];
-      }
-      SD_TL_AT(cp == lo ? g0 : 1 << 30, i, nt, 6);
-      status = empty ? 1 : 0;
-      stop = sh.stop != 0;
-    }
-  }
-  if (tid == 0) {
-    if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
-    if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
-  }
-  SD_TL_FLUSH(g0);
-}
-
-bool sdt_wide(const PyrGeom &G) { return SDT_WIDE && G.M == 4; }
-size_t sdt_wide_lds_bytes() { return sw_lds_total(); }
 
 int sdt_slab_shift(const PyrGeom &G) { return SDT_SLAB ? 3 * (G.M - 1) : 0; }
 bool sdt_seam_lists(const PyrGeom &G) { return G.M == 4 && sd_strad<4>(); }
@@ -2551,23 +1961,12 @@ hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &L
                   (void *)&S,     (void *)&kstride,  (void *)&NB,        (void *)&UU,
                   (void *)&uu_stride_k, (void *)&counters, (void *)&flags, (void *)&nwg, (void *)&spin_limit,
                   (void *)&P.df,  (void *)&P.uold, (void *)&same2, (void *)&strad};
-  if (sdt_wide(G)) {  // SDT_WIDE: the 1024-thread row body (its own LDS layout)
-    void *wargs[] = {(void *)&P,     (void *)&Lv,       (void *)&G,         (void *)&perm,
-                     (void *)&S,     (void *)&kstride,  (void *)&NB,        (void *)&UU,
-                     (void *)&uu_stride_k, (void *)&counters, (void *)&flags, (void *)&nwg, (void *)&spin_limit,
-                     (void *)&P.df,  (void *)&P.uold, (void *)&same2};
-    return hipLaunchKernel((const void *)k_sdt_run_wide, dim3(nwg), dim3(1024), wargs, sdt_wide_lds_bytes(), s);
-  }
   if (G.M == 4) return hipLaunchKernel((const void *)k_sdt_run<4>, dim3(nwg), dim3(512), args, lds, s);
   return hipLaunchKernel((const void *)k_sdt_run<3>, dim3(nwg), dim3(64), args, lds, s);
 }
 
 int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds) {
   int n = 0;
-  if (sdt_wide(G))
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_sdt_run_wide, 1024, sdt_wide_lds_bytes()) == hipSuccess
-               ? n
-               : 0;
   hipError_t e = G.M == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_sdt_run<4>, 512, lds)
                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_sdt_run<3>, 64, lds);
   return e == hipSuccess ? n : 0;
