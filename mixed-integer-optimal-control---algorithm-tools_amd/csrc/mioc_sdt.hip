@@ -78,6 +78,12 @@ constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, 
 #ifndef SDT_BF
 #define SDT_BF 1                         // row body: straddle pairs and +Inf stamps without branches (in-wave LDS order)
 #endif
+#ifndef SDT_P0STAMP
+// row body: the first phase writes the raw Ψ to the transform buffer as well and pass 0 stamps the values it reads,
+// so the stamp scatter and its barrier go; the next row's loads issue right after the statistics' reduction
+// (A/B builds: 0, the separate stamp phase)
+#define SDT_P0STAMP 1
+#endif
 #ifndef SDT_PRED_PROBE
 #define SDT_PRED_PROBE 0                 // diagnostic build: count where a same-binade predicted scale would miss
 #endif
@@ -623,12 +629,17 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   // ---- one pass of the transform: forward and backward sweep along the 8 levels of dimension m, unit step 1.0;
   // this thread's line is read from and (but for the last pass) written back to the swizzled LDS values ---------
   double o[8];
+  constexpr bool P0 = SDT_P0STAMP && !(PERSIST && SDT_PRED);
   auto pass = [&](int m) {
     int pos[8];
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
       pos[x] = sd_swz(sd_rank((int)threadIdx.x, m, x));  // tid-only: hoisted out of the row loop
       o[x] = dtv[pos[x]];
+    }
+    if (P0 && m == 0) {  // (SDT_P0STAMP) the raw Ψ of ranks 8·tid + x: stamp them here
+#pragma unroll
+      for (int x = 0; x < 8; ++x) o[x] = stamp_inf(o[x], sd_rank((int)threadIdx.x, 0, x));
     }
 #if SDT_PASS_SPLIT
     // two independent chains (prefix f over sources <= x, strict suffix b over sources > x: disjoint candidate
@@ -802,7 +813,11 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       for (int hh = 0; hh < 2; ++hh) {
         const double x = v[2 * q + hh];  // (sd_strad: +Inf for a straddling second element, written by its loader)
         // (SDT_BF: written anyway -- the straddle lane is in this wave and writes after it, in-wave LDS order)
-        if (SDT_BF || !(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) psi[(hh ? ein[q].y : ein[q].x) & 0xFFFFu] = x;
+        if (SDT_BF || !(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) {
+          const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
+          psi[j] = x;
+          if constexpr (P0) dtv[sd_swz(j)] = x;  // (SDT_P0STAMP) raw, stamped by pass 0
+        }
         const bool fin = x < INFINITY;
         nv += __popcll(__ballot(fin)) << 16;
         pmn = sd_min(pmn, x);  // +Inf is neutral
@@ -812,7 +827,10 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       const double x = (srank & 0x10000) ? INFINITY : xs;
       const bool fin = srank >= 0 && x < INFINITY;
       nv += __popcll(__ballot(fin)) << 16;
-      if (srank >= 0) psi[srank & 0xFFFF] = x;
+      if (srank >= 0) {
+        psi[srank & 0xFFFF] = x;
+        if constexpr (P0) dtv[sd_swz(srank & 0xFFFF)] = x;
+      }
       pmn = sd_min(pmn, fin ? x : INFINITY);
       pmx = sd_max(pmx, fin ? x : -INFINITY);
     }
@@ -906,7 +924,11 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     }
   }
   const bool transform = !direct && !empty && !sparse;  // uniform
-  if constexpr (!PRED) {
+  if constexpr (P0) {
+    // (SDT_P0STAMP) no stamp phase: every wave is past its last read of `pin` (barrier 1)
+    h.go();
+    if (!transform) h.load_part(-1);
+  } else if constexpr (!PRED) {
     if (transform) {
       // ---- stamp: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) | j --------------------------------------------
 #pragma unroll
