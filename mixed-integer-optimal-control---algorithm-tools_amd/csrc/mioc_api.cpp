@@ -481,7 +481,7 @@ int run_bellman(mioc_ctx *ctx) {
     // row segments on several CUs need their hand-off flags (and a timed-out wait redoes the DP in one workgroup)
     int32_t *pflags = nullptr;
     if (!ctx->force_steps) {
-      const size_t fbytes = ((size_t)K * (RP / 16 + 1) + 1) * sizeof(int32_t);
+      const size_t fbytes = ((size_t)K * pinf_recur_segments(P) + 1) * sizeof(int32_t);
       rc = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, fbytes, "p=Inf segment flags");
       if (rc) return rc;
       HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, fbytes, ctx->stream));

@@ -28,10 +28,10 @@ namespace mioc {
 #define PINF_RECUR_MC 1     // few subproblems: row segments on several CUs (k_pinf_recur_mc)
 #endif
 #ifndef PINF_MC_CHUNK
-#define PINF_MC_CHUNK 32       // k_pinf_recur_mc: steps per segment hand-off (16: 24.2 ms at C4, 32: 21.9 ms)
+#define PINF_MC_CHUNK 64       // k_pinf_recur_mc: steps per segment hand-off (C4, 8-row segments: 16: 23.3 ms, 32: 19.9 ms, 64: 19.6 ms)
 #endif
 #ifndef PINF_RECUR_MC_LANES
-#define PINF_RECUR_MC_LANES 4  // k_pinf_recur_mc: lanes per budget row (4: 16 rows per segment; 2: 32)
+#define PINF_RECUR_MC_LANES 8  // k_pinf_recur_mc: lanes per budget row (8: 8 rows per segment, C4 19.8 ms; 4: 16 rows, 21.9 ms; 2: 32)
 #endif
 #ifndef PINF_RECUR_XR
 #define PINF_RECUR_XR 1     // C4's B = 256: eight waves and the extra row split by classes (k_pinf_recur_xr)
@@ -507,7 +507,8 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
   constexpr int RPS = 64 / LPR;      // rows per segment (one wave)
   constexpr int AS = 32 + RPS;       // step array: the 32 rows below the segment, then its own
   constexpr int CH = PINF_MC_CHUNK;  // steps per hand-off
-  static_assert(BWP >= 8 && BWP <= 32 && CB >= 2 && CB % 2 == 0 && (LPR == 2 || LPR == 4), "k_pinf_recur_mc shape");
+  static_assert(BWP >= 8 && BWP <= 32 && CB >= 2 && CB % 2 == 0 && (LPR == 2 || LPR == 4 || LPR == 8),
+                "k_pinf_recur_mc shape");
   const int RP = P.RP, B = P.B, nt = P.nt, K = P.K;
   const int k = (int)blockIdx.x / nseg, q = (int)blockIdx.x - k * nseg;
   const int lane = (int)threadIdx.x, r = lane / LPR, h = lane % LPR, c = RPS * q + r, u = r + 32;
@@ -604,7 +605,8 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
       for (int bb = 0; bb < CB; ++bb) m[bb & 3] = pvmin(m[bb & 3], kv[bb] + wv[CB - 1 - bb]);
       double rv = pvmin(pvmin(m[0], m[1]), pvmin(m[2], m[3]));
       rv = pvmin(rv, pv_dpp<0xB1>(rv));                      // the lane group's other class parts
-      if constexpr (LPR == 4) rv = pvmin(rv, pv_dpp<0x4E>(rv));
+      if constexpr (LPR >= 4) rv = pvmin(rv, pv_dpp<0x4E>(rv));
+      if constexpr (LPR == 8) rv = pvmin(rv, pv_dpp<0x141>(rv));  // row_half_mirror: lane i <-> 7 - i, the other quad
       if (h == 0) {
         slot(i)[u] = rv;
         const double out = c <= B ? rv : INFINITY;
@@ -634,6 +636,20 @@ __global__ void k_pinf_rfill(ProblemDev P, PinfDev D, int c_from) {
 
 int pinf_chunk_recur(int BWP) { return BWP <= 16 ? 64 : 32; }
 
+namespace {
+// k_pinf_recur_mc for one class width: false where the width leaves a lane fewer than two classes
+template <int BWP, int LPR>
+bool launch_pinf_mc(hipStream_t s, const ProblemDev &P, const PinfDev &D, int nseg, int32_t *flags,
+                    unsigned spin_limit, size_t lds) {
+  if constexpr (BWP >= 2 * LPR) {
+    hipLaunchKernelGGL((k_pinf_recur_mc<BWP, LPR>), dim3(P.K * nseg), dim3(64), lds, s, P, D, nseg, flags, spin_limit);
+    return true;
+  } else {
+    return false;
+  }
+}
+}  // namespace
+
 int pinf_recur_segments(const ProblemDev &P) { return (P.B + 1 + 64 / PINF_RECUR_MC_LANES - 1) / (64 / PINF_RECUR_MC_LANES); }
 
 hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ncu, int32_t *flags,
@@ -649,13 +665,13 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
       constexpr int CH = PINF_MC_CHUNK;
       const size_t lds = (size_t)(2 * CH * (32 + RPS) + 2 * CH * D.BWP) * sizeof(double);
       if (RPS * nseg < P.RP) hipLaunchKernelGGL(k_pinf_rfill, dim3(64, P.K), dim3(256), 0, s, P, D, RPS * nseg);
-      switch (D.BWP) {
-        case 8: hipLaunchKernelGGL((k_pinf_recur_mc<8, LPR>), dim3(P.K * nseg), dim3(64), lds, s, P, D, nseg, flags, spin_limit); break;
-        case 16: hipLaunchKernelGGL((k_pinf_recur_mc<16, LPR>), dim3(P.K * nseg), dim3(64), lds, s, P, D, nseg, flags, spin_limit); break;
-        default: hipLaunchKernelGGL((k_pinf_recur_mc<32, LPR>), dim3(P.K * nseg), dim3(64), lds, s, P, D, nseg, flags, spin_limit); break;
+      const bool ok = D.BWP == 8    ? launch_pinf_mc<8, LPR>(s, P, D, nseg, flags, spin_limit, lds)
+                      : D.BWP == 16 ? launch_pinf_mc<16, LPR>(s, P, D, nseg, flags, spin_limit, lds)
+                                    : launch_pinf_mc<32, LPR>(s, P, D, nseg, flags, spin_limit, lds);
+      if (ok) {
+        *segmented = true;
+        return hipGetLastError();
       }
-      *segmented = true;
-      return hipGetLastError();
     }
   }
   int pairs = ((P.RP / 2 + 63) / 64) * 64;  // one thread (G = 1) or lane quad (G = 4) per two budget rows
