@@ -36,6 +36,9 @@ namespace mioc {
 #ifndef PINF_RECUR_XR
 #define PINF_RECUR_XR 1     // C4's B = 256: eight waves and the extra row split by classes (k_pinf_recur_xr)
 #endif
+#ifndef PINF_PREP_REGS
+#define PINF_PREP_REGS 1    // class tables: M a template constant, a thread's levels in registers (A/B builds: 0)
+#endif
 #ifndef PINF_RECUR_G
 #define PINF_RECUR_G 4      // lanes per row pair when split (2 or 4)
 #endif
@@ -122,6 +125,87 @@ __global__ __launch_bounds__(256) void k_pinf_prep(ProblemDev P, LevelsDev Lv, P
   }
 }
 
+// The same tables with M a compile-time constant and each thread's (at most PREP_PR) levels kept in registers between
+// the two passes: a level's values are loaded and its K and class computed once, with Δt·df(:, i) and u_old(:, i) in
+// registers (the loop above reloads both per level and per pass).  Same keys, same atomics, same three tables.
+constexpr int PREP_PR = 16;
+template <int M>
+__global__ __launch_bounds__(256) void k_pinf_prep_m(ProblemDev P, LevelsDev Lv, PinfDev D) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int BW = D.BW;
+  uint64_t *skmin = reinterpret_cast<uint64_t *>(smem);
+  uint64_t *sk2 = skmin + BW;
+  int32_t *sfirst = reinterpret_cast<int32_t *>(sk2 + BW);
+  const int i = blockIdx.x, k = blockIdx.y, tid = threadIdx.x;
+  for (int b = tid; b < BW; b += blockDim.x) {
+    skmin[b] = ~0ull;
+    sk2[b] = ~0ull;
+    sfirst[b] = INT_MAX;
+  }
+  const double *dfi = P.df + ((size_t)k * P.nt + i) * M;
+  const double *uoi = P.uold + ((size_t)k * P.nt + i) * M;
+  const bool term = (i == P.nt - 1);
+  __shared__ unsigned long long s_kab;
+  if (tid == 0) s_kab = 0ull;
+  double a[M], uo[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    a[m] = P.dt * dfi[m];  // the factor p_t1 forms per level: the same rounding
+    uo[m] = uoi[m];
+  }
+  __syncthreads();
+  uint64_t key[PREP_PR];
+  int bb[PREP_PR];
+  unsigned long long kab = 0ull;
+#pragma unroll
+  for (int j = 0; j < PREP_PR; ++j) {
+    const int r = tid + 256 * j;
+    key[j] = ~0ull;
+    bb[j] = BW;  // no class (outside the tracked budgets, or past the level set)
+    if (r < Lv.L) {
+      const double *nuv = Lv.nuval + (size_t)r * M;
+      double nv[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) nv[m] = nuv[m];
+      int b = 0;
+#pragma unroll
+      for (int m = 0; m < M; ++m) b += (int)fabs(nv[m] - uo[m]);  // p_bt
+      if (b < BW) {
+        double t = 0.0;
+#pragma unroll
+        for (int m = 0; m < M; ++m) t = t + a[m] * nv[m];  // p_t1
+        const double v = term ? t : t + Lv.beta;           // fl(T1 + β·1.0)
+        key[j] = okey(v);
+        bb[j] = b;
+        atomicMin(reinterpret_cast<unsigned long long *>(&skmin[b]), (unsigned long long)key[j]);
+        const unsigned long long av = (unsigned long long)__double_as_longlong(fabs(v));
+        kab = av > kab ? av : kab;
+      }
+    }
+  }
+  atomicMax(&s_kab, kab);
+  __syncthreads();
+  if (tid == 0) D.kabs[(size_t)k * P.nt + i] = __longlong_as_double((long long)s_kab);
+#pragma unroll
+  for (int j = 0; j < PREP_PR; ++j) {
+    const int b = bb[j];
+    if (b < BW) {
+      if (key[j] == skmin[b])
+        atomicMin(&sfirst[b], tid + 256 * j);
+      else
+        atomicMin(reinterpret_cast<unsigned long long *>(&sk2[b]), (unsigned long long)key[j]);
+    }
+  }
+  __syncthreads();
+  const size_t row = ((size_t)k * P.nt + i) * D.BWP;
+  for (int b = tid; b < D.BWP; b += blockDim.x) {
+    const bool in = b < BW;
+    D.kmin[row + b] = in ? from_okey(skmin[b]) : INFINITY;
+    D.k2[row + b] = in ? from_okey(sk2[b]) : INFINITY;
+    D.kfirst[row + b] = (!in || sfirst[b] == INT_MAX) ? -1 : sfirst[b];
+  }
+}
+
 // Small level sets (L <= 64, BWP <= 16: the SOS1 shapes of C1-C3): one THREAD per (step, subproblem) walks the L
 // levels in rank order and keeps the class keys in registers -- the same three quantities as k_pinf_prep (first
 // minimum key, smallest other key, first rank at the minimum; keys compare as okey, so -0.0 < +0.0 as there).
@@ -182,6 +266,15 @@ hipError_t launch_pinf_prep(hipStream_t s, const ProblemDev &P, const LevelsDev 
   }
   dim3 grid(P.nt, P.K);
   size_t lds = (size_t)D.BW * 20 + 16;
+  if (PINF_PREP_REGS && Lv.L <= 256 * PREP_PR && P.M >= 2 && P.M <= 4) {
+    if (P.M == 4)
+      hipLaunchKernelGGL(k_pinf_prep_m<4>, grid, dim3(256), lds, s, P, Lv, D);
+    else if (P.M == 3)
+      hipLaunchKernelGGL(k_pinf_prep_m<3>, grid, dim3(256), lds, s, P, Lv, D);
+    else
+      hipLaunchKernelGGL(k_pinf_prep_m<2>, grid, dim3(256), lds, s, P, Lv, D);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_pinf_prep, grid, dim3(256), lds, s, P, Lv, D);
   return hipGetLastError();
 }

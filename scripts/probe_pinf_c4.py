@@ -1,5 +1,5 @@
 """C4 at p = Inf (one subproblem, full L and B, nt from argv) across library builds, each in its own process:
-k_pinf_recur time per launch (HIP events), the whole bellman + backtrack wall time, and a digest of u / Φ* at three
+k_pinf_recur time per launch (HIP events), k_pinf_prep's, the whole bellman + backtrack wall time, and a digest of u / Φ* at three
 budgets, which must agree across builds.  Usage: python scripts/probe_pinf_c4.py NT LIB [LIB ...]"""
 import hashlib, json, math, os, subprocess, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -18,7 +18,7 @@ def one(nt, lib):
     with native.Context(0) as ctx:
         ctx.set_levels(lt); ctx.set_cost(math.inf, cfg.beta)
         ctx.set_option(native.MIOC_OPT_TIMING, 1)
-        best, wall = None, None
+        best, wall, prep = None, None, None
         for _ in range(3):
             ctx.reset_stats()
             t0 = time.perf_counter()
@@ -26,15 +26,21 @@ def one(nt, lib):
             ctx.synchronize()
             w = time.perf_counter() - t0
             ms, n, name = ctx.kernel_stats(0)
+            pms, pn, _ = ctx.kernel_stats(2)  # k_pinf_prep
             best = ms / n if best is None else min(best, ms / n)
+            prep = pms / max(pn, 1) if best == ms / n else prep
             wall = w if wall is None else min(wall, w)
         h = hashlib.sha256()
-        for Bp in (cfg.B, cfg.B // 2, 7):
-            u, phi, _ = ctx.backtrack(Bp)
-            h.update(np.ascontiguousarray(u).tobytes()); h.update(np.float64(phi).tobytes())
+        try:  # (a timing-only build with wrong tables may have no finite path: digest "error")
+            for Bp in (cfg.B, cfg.B // 2, 7):
+                u, phi, _ = ctx.backtrack(Bp)
+                h.update(np.ascontiguousarray(u).tobytes()); h.update(np.float64(phi).tobytes())
+        except native.MiocNativeError:
+            h = None
         print(json.dumps({"lib": os.path.basename(lib), "nt": nt, "kernel": name, "ms": round(best, 3),
-                          "us_per_step": round(1e3 * best / (nt - 1), 4), "bellman_wall_ms": round(1e3 * wall, 3),
-                          "digest": h.hexdigest()[:16]}), flush=True)
+                          "us_per_step": round(1e3 * best / (nt - 1), 4), "prep_ms": round(prep, 3),
+                          "bellman_wall_ms": round(1e3 * wall, 3),
+                          "digest": h.hexdigest()[:16] if h else "error"}), flush=True)
 
 
 if __name__ == "__main__":
