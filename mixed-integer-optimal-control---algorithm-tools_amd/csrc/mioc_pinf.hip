@@ -683,20 +683,25 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
         kv[2 * t + 1] = y.y;
       }
     };
-    double kv[CB];
-    kload(kv, hi);
-    for (int i = hi; i >= lo; --i) {
+    // one step: the class values kv of step i (loaded a step earlier), kn <- those of step i-1
+    auto step = [&](int i, const double (&kv)[CB], double (&kn)[CB]) {
       asm volatile("" ::: "memory");
-      double kn[CB];
       if (i > lo) kload(kn, i - 1);
       const double *Ain = slot(i + 1) + u - CB * h - (CB - 1);  // R_{i+1}[c - CB·h - (CB-1) .. c - CB·h]
       double wv[CB];
 #pragma unroll
       for (int t = 0; t < CB; ++t) wv[t] = Ain[t];
-      double m[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+      double m[4];  // four accumulators, each started by its first candidate
 #pragma unroll
-      for (int bb = 0; bb < CB; ++bb) m[bb & 3] = pvmin(m[bb & 3], kv[bb] + wv[CB - 1 - bb]);
-      double rv = pvmin(pvmin(m[0], m[1]), pvmin(m[2], m[3]));
+      for (int bb = 0; bb < CB; ++bb) {
+        const double cand = kv[bb] + wv[CB - 1 - bb];
+        m[bb & 3] = bb < 4 ? cand : pvmin(m[bb & 3], cand);
+      }
+      double rv;
+      if constexpr (CB >= 4)
+        rv = pvmin(pvmin(m[0], m[1]), pvmin(m[2], m[3]));
+      else
+        rv = pvmin(m[0], m[1]);
       rv = pvmin(rv, pv_dpp<0xB1>(rv));                      // the lane group's other class parts
       if constexpr (LPR >= 4) rv = pvmin(rv, pv_dpp<0x4E>(rv));
       if constexpr (LPR == 8) rv = pvmin(rv, pv_dpp<0x141>(rv));  // row_half_mirror: lane i <-> 7 - i, the other quad
@@ -706,10 +711,13 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
         __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(out), (unsigned)__double2hiint(out)},
                                               Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
       }
-      if (i > lo) {
-#pragma unroll
-        for (int t = 0; t < CB; ++t) kv[t] = kn[t];
-      }
+    };
+    // two steps per trip, the class-value registers alternating (no copies between steps)
+    double ka[CB], kb[CB];
+    kload(ka, hi);
+    for (int i = hi; i >= lo; i -= 2) {
+      step(i, ka, kb);
+      if (i - 1 >= lo) step(i - 1, kb, ka);
     }
     // this chunk's rows have landed: publish its last step for the segments above
     vm_drain();
