@@ -422,14 +422,22 @@ __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && c0 == 2 * tid) g_pinf_stamps[threadIdx.x >> 6][0] += t1 - t0;
 #endif
         // row 2t:   R_{i+1}[2t - b]   = w[CB - 1 - bb];   row 2t+1: R_{i+1}[2t + 1 - b] = w[CB - bb]
-        double m0[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, m1[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+        // four accumulators per row, each started by its first candidate
+        double m0[4], m1[4];
 #pragma unroll
         for (int b2 = 0; b2 < CB; ++b2) {
-          m0[b2 & 3] = pvmin(m0[b2 & 3], kv[b2] + w[CB - 1 - b2]);
-          m1[b2 & 3] = pvmin(m1[b2 & 3], kv[b2] + w[CB - b2]);
+          const double c0 = kv[b2] + w[CB - 1 - b2], c1 = kv[b2] + w[CB - b2];
+          m0[b2 & 3] = b2 < 4 ? c0 : pvmin(m0[b2 & 3], c0);
+          m1[b2 & 3] = b2 < 4 ? c1 : pvmin(m1[b2 & 3], c1);
         }
-        double r0 = pvmin(pvmin(m0[0], m0[1]), pvmin(m0[2], m0[3]));
-        double r1 = pvmin(pvmin(m1[0], m1[1]), pvmin(m1[2], m1[3]));
+        double r0, r1;
+        if constexpr (CB >= 4) {
+          r0 = pvmin(pvmin(m0[0], m0[1]), pvmin(m0[2], m0[3]));
+          r1 = pvmin(pvmin(m1[0], m1[1]), pvmin(m1[2], m1[3]));
+        } else {
+          r0 = pvmin(m0[0], m0[1]);
+          r1 = pvmin(m1[0], m1[1]);
+        }
         if constexpr (G >= 2) {  // the class parts of the lane group (quad_perm xor 1, then xor 2)
           r0 = pvmin(r0, pv_dpp<0xB1>(r0));
           r1 = pvmin(r1, pv_dpp<0xB1>(r1));
