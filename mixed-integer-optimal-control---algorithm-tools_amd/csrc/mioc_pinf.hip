@@ -31,7 +31,7 @@ namespace mioc {
 #define PINF_MC_CHUNK 64       // k_pinf_recur_mc: steps per segment hand-off (C4, 8-row segments: 16: 23.3 ms, 32: 19.9 ms, 64: 19.6 ms)
 #endif
 #ifndef PINF_RECUR_MC_LANES
-#define PINF_RECUR_MC_LANES 8  // k_pinf_recur_mc: lanes per budget row (8: 8 rows per segment, C4 19.8 ms; 4: 16 rows, 21.9 ms; 2: 32)
+#define PINF_RECUR_MC_LANES 8  // k_pinf_recur_mc: lanes per budget row (8: 8 rows per segment; 16: 4 rows, 8 % slower at C4; 4: 16 rows, 11 %; 2: 32)
 #endif
 #ifndef PINF_RECUR_XR
 #define PINF_RECUR_XR 1     // C4's B = 256: eight waves and the extra row split by classes (k_pinf_recur_xr)
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
   constexpr int RPS = 64 / LPR;      // rows per segment (one wave)
   constexpr int AS = 32 + RPS;       // step array: the 32 rows below the segment, then its own
   constexpr int CH = PINF_MC_CHUNK;  // steps per hand-off
-  static_assert(BWP >= 8 && BWP <= 32 && CB >= 2 && CB % 2 == 0 && (LPR == 2 || LPR == 4 || LPR == 8),
+  static_assert(BWP >= 8 && BWP <= 32 && CB >= 2 && CB % 2 == 0 && (LPR == 2 || LPR == 4 || LPR == 8 || LPR == 16),
                 "k_pinf_recur_mc shape");
   const int RP = P.RP, B = P.B, nt = P.nt, K = P.K;
   const int k = (int)blockIdx.x / nseg, q = (int)blockIdx.x - k * nseg;
@@ -712,7 +712,8 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
         rv = pvmin(m[0], m[1]);
       rv = pvmin(rv, pv_dpp<0xB1>(rv));                      // the lane group's other class parts
       if constexpr (LPR >= 4) rv = pvmin(rv, pv_dpp<0x4E>(rv));
-      if constexpr (LPR == 8) rv = pvmin(rv, pv_dpp<0x141>(rv));  // row_half_mirror: lane i <-> 7 - i, the other quad
+      if constexpr (LPR >= 8) rv = pvmin(rv, pv_dpp<0x141>(rv));  // row_half_mirror: lane i <-> 7 - i, the other quad
+      if constexpr (LPR == 16) rv = pvmin(rv, pv_dpp<0x140>(rv));  // row_mirror: lane i <-> 15 - i, the other half
       if (h == 0) {
         slot(i)[u] = rv;
         const double out = c <= B ? rv : INFINITY;
