@@ -31,7 +31,7 @@ namespace mioc {
 #define PINF_MC_CHUNK 64       // k_pinf_recur_mc: steps per segment hand-off (C4, 8-row segments: 16: 23.3 ms, 32: 19.9 ms, 64: 19.6 ms)
 #endif
 #ifndef PINF_RECUR_MC_LANES
-#define PINF_RECUR_MC_LANES 8  // k_pinf_recur_mc: lanes per budget row (8: 8 rows per segment; 16: 4 rows, 8 % slower at C4; 4: 16 rows, 11 %; 2: 32)
+#define PINF_RECUR_MC_LANES 8  // k_pinf_recur_mc: lanes per budget row (8: 8 rows per segment; 16: 4 rows, 8 % slower at C4; 4: 16 rows, 11 % slower with the one-step loop; 2: 32)
 #endif
 #ifndef PINF_RECUR_XR
 #define PINF_RECUR_XR 1     // C4's B = 256: eight waves and the extra row split by classes (k_pinf_recur_xr)
