@@ -934,7 +934,7 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
   extern __shared__ __attribute__((aligned(16))) double wsm[];
   const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
   const int M = P.M, nt = P.nt, RP = P.RP, BWP = D.BWP, CH = D.CH, W = D.W;
-  const bool walker = tid < 64;  // wave 0 walks; the other waves stage
+  const bool walker = __builtin_amdgcn_readfirstlane(tid) < 64;  // wave 0 walks (wave-uniform); the others stage
   const Start st = start[k];
   if (st.status != MIOC_OK) return;
   int32_t *rk = ranks + (size_t)k * nt;
@@ -1013,10 +1013,11 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
     const int32_t *KfB = Kf + (size_t)buf * CH * BWP;
     const double *RbB = Rb + (size_t)buf * CH * W;
     const int blo = s_lo[buf];
-    const bool inb = lane < BWP;
-    for (int i = i0; walker && !dead && i < i1; ++i) {
+    const unsigned long long clsm = BWP >= 64 ? ~0ull : (1ull << BWP) - 1;  // the lanes that are classes
+    // one walk step; TERM: the terminal step j = nt - 1 (compiled apart, so the other steps carry no term selects)
+    auto step = [&](int i, auto TERM) {
       const int row = i - i0, j = i + 1, cp = c - br;
-      const bool term = (j == nt - 1);
+      constexpr bool term = decltype(TERM)::value;  // the last step (j = nt - 1): its own instance
       // Branch-free: every lane reads an in-bounds slot and masks afterwards.  The class row does not
       // depend on the walk, so its three reads issue beside the window read.
       const int lb = lane & (BWP - 1), xi = cp - lane;
@@ -1025,17 +1026,17 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
       const int kfr = KfB[row * BWP + lb];
       const int xo = xi - blo;
       const double xr = RbB[(size_t)row * W + (xo > 0 ? (xo < W ? xo : W - 1) : 0)];
-      const double km = inb ? kmr : INFINITY;
-      const double k2 = inb ? k2r : INFINITY;
-      const int kf = inb ? kfr : INT_MAX;
-      const double x = term ? (lane == cp ? 0.0 : INFINITY) : (inb && xi >= 0 ? xr : INFINITY);
+      // lanes >= BWP compute on wrapped class slots; their bits leave the ballots (clsm) instead of masked values
+      const double km = kmr, k2 = k2r;
+      const int kf = kfr;
+      const double x = term ? (lane == cp ? 0.0 : INFINITY) : (xi >= 0 ? xr : INFINITY);
       const bool ok = km < INFINITY && x < INFINITY;
       const double V = term ? km : km + x;
       const double V2 = term ? k2 : k2 + x;
       const bool match = ok && (Kr + V == target);
       const bool amb = match && k2 < INFINITY && (Kr + V2 == target);
-      const unsigned long long mm = __ballot(match);
-      const unsigned long long am = __ballot(amb);
+      const unsigned long long mm = __ballot(match) & clsm;
+      const unsigned long long am = __ballot(amb) & clsm;
       int win, winb;
       double winV, winK;
       if (mm != 0 && am == 0) {
@@ -1082,7 +1083,7 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
         if (bal == 0) {  // inconsistent tables: cannot happen for a consistent DP
           if (lane == 0) atomicAdd(nfallback + 1, 1);
           dead = true;  // stop walking, but keep joining the staging barriers
-          break;
+          return;
         }
         const int src = __builtin_ffsll((long long)bal) - 1;
         win = m2;
@@ -1096,6 +1097,12 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
       target = winV;
       Kr = winK;
       br = winb;
+    };
+    for (int i = i0; walker && !dead && i < i1; ++i) {
+      if (i == nt - 2)
+        step(i, std::true_type{});
+      else
+        step(i, std::false_type{});
     }
     PI_T(w1);
     if (tid == 0) s_c[(q + 1) & 1] = c;  // the walker's budget for the next staging decision
