@@ -714,12 +714,12 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
       if constexpr (LPR >= 4) rv = pvmin(rv, pv_dpp<0x4E>(rv));
       if constexpr (LPR >= 8) rv = pvmin(rv, pv_dpp<0x141>(rv));  // row_half_mirror: lane i <-> 7 - i, the other quad
       if constexpr (LPR == 16) rv = pvmin(rv, pv_dpp<0x140>(rv));  // row_mirror: lane i <-> 15 - i, the other half
-      if (h == 0) {
-        slot(i)[u] = rv;
-        const double out = c <= B ? rv : INFINITY;
-        __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(out), (unsigned)__double2hiint(out)},
-                                              Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
-      }
+      // every lane of the row group holds rv: all of them store it (one address per group, so the same lines and
+      // bytes move), with no exec-mask switch on the chain (one lane storing: 16.1 ms at C4, all of them: 15.1 ms)
+      slot(i)[u] = rv;
+      const double out = c <= B ? rv : INFINITY;
+      __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(out), (unsigned)__double2hiint(out)},
+                                            Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
     };
     // two steps per trip, the class-value registers alternating (no copies between steps)
     double ka[CB], kb[CB];
