@@ -716,9 +716,10 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
       if constexpr (LPR == 16) rv = pvmin(rv, pv_dpp<0x140>(rv));  // row_mirror: lane i <-> 15 - i, the other half
       // every lane of the row group holds rv: all of them store it (one address per group, so the same lines and
       // bytes move), with no exec-mask switch on the chain (one lane storing: 16.1 ms at C4, all of them: 15.1 ms)
+      // (rows above B of the top segment store their finite value too: k_pinf_rfill sets them to +Inf after the
+      // launch, and no segment's window reads them)
       slot(i)[u] = rv;
-      const double out = c <= B ? rv : INFINITY;
-      __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(out), (unsigned)__double2hiint(out)},
+      __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(rv), (unsigned)__double2hiint(rv)},
                                             Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
     };
     // two steps per trip, the class-value registers alternating (no copies between steps)
@@ -774,11 +775,12 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
         RPS * nseg <= P.RP && (size_t)P.nt * P.RP * 8 < (1ull << 31)) {
       constexpr int CH = PINF_MC_CHUNK;
       const size_t lds = (size_t)(2 * CH * (32 + RPS) + 2 * CH * D.BWP) * sizeof(double);
-      if (RPS * nseg < P.RP) hipLaunchKernelGGL(k_pinf_rfill, dim3(64, P.K), dim3(256), 0, s, P, D, RPS * nseg);
       const bool ok = D.BWP == 8    ? launch_pinf_mc<8, LPR>(s, P, D, nseg, flags, spin_limit, lds)
                       : D.BWP == 16 ? launch_pinf_mc<16, LPR>(s, P, D, nseg, flags, spin_limit, lds)
                                     : launch_pinf_mc<32, LPR>(s, P, D, nseg, flags, spin_limit, lds);
       if (ok) {
+        // rows above B (the top segment's finite values, and the rows no segment computes): +Inf, after the launch
+        if (P.B + 1 < P.RP) hipLaunchKernelGGL(k_pinf_rfill, dim3(64, P.K), dim3(256), 0, s, P, D, P.B + 1);
         *segmented = true;
         return hipGetLastError();
       }
