@@ -80,6 +80,8 @@ extern "C" {
 #define MIOC_OPT_PINF_WALK 8 /* p=Inf backtrack: 0 (default) the segmented walk -- one subproblem's path spread
                                 over many workgroups -- for batches of at most 64 subproblems with >= 512 steps,
                                 else one serial walk per subproblem; 1: segmented walk forced; -1: serial walk */
+#define MIOC_OPT_SDT_PAIR 9 /* persistent separable transform on 8^4 grids: 1 (default) two workgroups per budget
+                               row (two row items in flight per CU; K·B <= CUs), 0: one workgroup per row */
 
 typedef struct mioc_ctx mioc_ctx;
 
@@ -142,7 +144,10 @@ int32_t mioc_backtrack_batch_device(mioc_ctx *ctx, int64_t B_use, double *d_u_ou
 /* The same with one budget per subproblem: d_B_use[k] (device, K int32, each 0 <= B_use[k] <= B) -- the
  * per-restart trust-region radii after halving (multi-trust.jl:108-110, B_new = floor(Δᵏ/Δt) per restart).
  * The budgets are validated on the device (no host read-back): a B_use[k] outside [0, B] makes d_status[k] =
- * MIOC_ESTATE and leaves subproblem k's u row NaN; the call itself returns MIOC_OK. */
+ * MIOC_ESTATE and leaves subproblem k's u row NaN; the call itself returns MIOC_OK.  The first backtrack after a DP
+ * whose workgroups hand rows to each other inside one launch (persistent separable DP, segmented fused separable
+ * DP, segmented p=Inf recursion: small batches) synchronises the stream once, to read that DP's timeout word and
+ * redo the DP if a wait timed out; later backtracks of the same DP enqueue without a synchronisation. */
 int32_t mioc_backtrack_batch_budgets_device(mioc_ctx *ctx, const int32_t *d_B_use, double *d_u_out, double *d_phi_star,
                                             int32_t *d_status);
 int32_t mioc_synchronize(mioc_ctx *ctx);

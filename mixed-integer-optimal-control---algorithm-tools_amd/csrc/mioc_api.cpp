@@ -104,6 +104,7 @@ void free_all(mioc_ctx *ctx) {
                   ctx->pinf.kabs, ctx->pinf.ftab, ctx->pinf.fseg, ctx->pinf.fneed,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
                   ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm, ctx->d_same2, ctx->d_strad,
+                  ctx->d_pack,  ctx->d_pseam,
                   ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own, ctx->d_ode_state};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -281,7 +282,7 @@ int run_bellman(mioc_ctx *ctx) {
     // precomputed (k_sdt_chain, k_sdt_row0), NB staging buffers
     const size_t run_lds = sdt_lds_bytes(ctx->pyr);
     int nwg = 0;
-    bool persist = false;
+    bool persist = false, pair = false;
     // (B + 1)·L·8 < 2^31: the persistent kernel addresses a staging block with 32-bit buffer offsets
     // ... and every b̃ within the kernel's dependency window (7 per dimension: u_old on the level grid); a u_old
     // off the grid reaches rows further back than the window waits for, so those problems take per-step launches
@@ -289,11 +290,14 @@ int run_bellman(mioc_ctx *ctx) {
         s_stride * sizeof(double) < (1ull << 31) && bmax <= 7 * ctx->pyr.M && !ctx->force_steps) {
       int ncu = 0;
       HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+      // 8^4 grids with every budget row on its own CU: two workgroups per row (k_sdt_pair, mioc_sdt2.hip); else one
+      // workgroup per CU over contiguous row chunks (k_sdt_run)
+      pair = ctx->opt_sdt_pair && sdt_pair_supported(ctx->pyr, (int)K, ctx->B, ncu, sdt_pair_blocks_per_cu());
       const int bpc = std::min(sdt_run_blocks_per_cu(ctx->pyr, run_lds), 1);  // one row workgroup per CU
       const size_t slots = (size_t)ncu * (size_t)std::max(bpc, 0);
       const size_t per_k = std::min<size_t>((size_t)ctx->B, K ? slots / K : 0);  // workgroups per subproblem
-      nwg = (int)(per_k * K);
-      persist = per_k >= 1;
+      nwg = pair ? (int)(2 * K * (size_t)ctx->B) : (int)(per_k * K);
+      persist = pair || per_k >= 1;
     }
     // persistent layout: per subproblem NB staging buffers of (B+1)·L, then row 0 of every step (nt·L), one region
     // addressed by one buffer resource (< 4 GiB); per-step layout: two buffers of K blocks of (B+1)·L
@@ -303,8 +307,9 @@ int run_bellman(mioc_ctx *ctx) {
     const size_t kstride = persist ? (size_t)nbuf * s_stride + nt * L : s_stride;
     if (persist && kstride * sizeof(double) >= (1ull << 32)) persist = false;  // (then also kstride = s_stride)
     const size_t ks = persist ? kstride : s_stride;
-    const size_t fw = (size_t)sdt_flag_words(ctx->pyr);
-    const size_t runflag_bytes = ((2 * K * (size_t)(ctx->B + 1) * fw + 1) * sizeof(int32_t) + 15) / 16 * 16;
+    // flags: done and loaded per row (k_sdt_run) or per row and step parity (k_sdt_pair), then the error word
+    const size_t nflag = (pair ? 4 : 2) * K * (size_t)(ctx->B + 1);
+    const size_t runflag_bytes = ((nflag + 1) * sizeof(int32_t) + 15) / 16 * 16;
     if (persist) {
       int rcf = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, runflag_bytes, "persistent row flags");
       if (!rcf) rcf = grow(ctx, &ctx->d_chain, &ctx->chain_cap, K * nt * sizeof(double), "row 0 chain");
@@ -321,37 +326,36 @@ int run_bellman(mioc_ctx *ctx) {
     if (rc) return rc;
     rc = grow(ctx, &ctx->d_perm, &ctx->perm_cap, K * nt * L * sizeof(uint32_t), "sphere orders");
     if (!rc) rc = grow(ctx, &ctx->d_same2, &ctx->same2_cap, K * nt * sizeof(int32_t), "sphere-order reuse flags");
-    const bool slab = algo == MIOC_ALGO_SEPARABLE && sdt_slab_shift(ctx->pyr) > 0;
-    const bool seams = persist && sdt_seam_lists(ctx->pyr);
+    const bool seams = persist && !pair && sdt_seam_lists(ctx->pyr);
     if (!rc && seams) rc = grow(ctx, &ctx->d_strad, &ctx->strad_cap, K * nt * 8 * 32 * sizeof(uint16_t), "seam lists");
+    if (!rc && pair) rc = grow(ctx, &ctx->d_pack, &ctx->pack_cap, K * nt * (L / 2) * sizeof(uint32_t), "packed orders");
+    if (!rc && pair) rc = grow(ctx, &ctx->d_pseam, &ctx->pseam_cap, K * nt * 128 * sizeof(uint32_t), "packed seams");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
     double *term = persist ? ctx->d_stage + ((nt - 1) % nbuf) * s_stride : st[(nt - 1) & 1];
-    HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm,
-                                  slab ? sdt_slab_shift(ctx->pyr) : 0, ctx->d_same2, seams ? ctx->d_strad : nullptr));
+    HIP_TRY(ctx, launch_pyr_order(ctx->stream, P, ctx->pyr, ctx->d_perm, ctx->d_same2, seams ? ctx->d_strad : nullptr,
+                                  ctx->d_counters));
     HIP_TRY(ctx, launch_pyr_terminal(ctx->stream, P, Lv, ctx->d_perm, term, ks));
     if (algo == MIOC_ALGO_SEPARABLE && persist) {
       // the whole DP as one persistent launch: rows handed between resident workgroups by flags
       HIP_TRY(ctx, launch_sdt_prep(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_chain, ctx->d_stage, ks,
                                    (size_t)nbuf * s_stride, (uint16_t *)ctx->d_U, uu_stride_k));
+      if (pair) HIP_TRY(ctx, launch_sdt_pack(ctx->stream, P, ctx->d_perm, ctx->d_pack, ctx->d_pseam, ctx->d_counters));
       HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, runflag_bytes, ctx->stream));
-      ev_begin(ctx, 0, "k_sdt_run");
-      const hipError_t le = launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_same2, ctx->d_strad,
-                                           ctx->d_stage, ks, nbuf,
-                                           (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags, nwg,
-                                           ctx->spin_limit, run_lds);
-      if (le == hipErrorCooperativeLaunchTooLarge) {  // (kept for a grid the runtime refuses): one launch per step
-        (void)hipGetLastError();
-        ev_end(ctx, 0, 0);
-        ctx->n_persist_fallbacks += 1;
-        ctx->force_steps = true;
-        const int rcs = run_bellman(ctx);
-        ctx->force_steps = false;
-        return rcs;
-      }
-      HIP_TRY(ctx, le);
+      ctx->last_sdt_kernel = pair ? "k_sdt_pair" : "k_sdt_run";
+      ev_begin(ctx, 0, ctx->last_sdt_kernel);
+      // (the grid is nwg <= CUs x resident workgroups per CU by construction above; a wait that never ends anyway --
+      // another process holding CUs -- is caught by the spin limit and redone per step by check_run)
+      if (pair)
+        HIP_TRY(ctx, launch_sdt_pair(ctx->stream, P, Lv, ctx->pyr, ctx->d_pack, ctx->d_pseam, ctx->d_stage, ks, nbuf,
+                                     (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags,
+                                     ctx->spin_limit));
+      else
+        HIP_TRY(ctx, launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_same2, ctx->d_strad, ctx->d_stage,
+                                    ks, nbuf, (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags, nwg,
+                                    ctx->spin_limit, run_lds));
       ev_end(ctx, 0, 1);
-      HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + 2 * K * (size_t)(ctx->B + 1) * fw, sizeof(int32_t),
+      HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + nflag, sizeof(int32_t),
                                   hipMemcpyDeviceToHost, ctx->stream));
       ctx->run_pending = true;
     } else if (algo == MIOC_ALGO_SEPARABLE) {
@@ -490,8 +494,10 @@ int run_bellman(mioc_ctx *ctx) {
       pflags = ctx->d_runflags;
     }
     bool segmented = false;
-    HIP_TRY(ctx, launch_pinf_recur(ctx->stream, P, D, ctx->ncu, pflags, ctx->spin_limit, &segmented));
+    const char *variant = "k_pinf_recur";
+    HIP_TRY(ctx, launch_pinf_recur(ctx->stream, P, D, ctx->ncu, pflags, ctx->spin_limit, &segmented, &variant));
     ev_end(ctx, 0, 1);
+    ctx->stat_name[0] = variant;  // the timing window is named after the recursion kernel that ran
     if (segmented) {
       const int nseg = pinf_recur_segments(P);
       HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + (size_t)K * nseg, sizeof(int32_t),
@@ -698,6 +704,10 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
     ctx->opt_nb = (int)value;
     return MIOC_OK;
   }
+  if (option == MIOC_OPT_SDT_PAIR) {
+    ctx->opt_sdt_pair = value != 0;
+    return MIOC_OK;
+  }
   if (option == MIOC_OPT_PINF_WALK) {
     if (value < -1 || value > 1) return fail(ctx, MIOC_EINVAL, "p=Inf walk option must be -1, 0 or 1");
     ctx->opt_pinf_walk = (int)value;
@@ -891,8 +901,10 @@ int32_t mioc_backtrack_batch_budgets_device(mioc_ctx *ctx, const int32_t *d_B_us
   if (!d_u_out || !d_B_use) return fail(ctx, MIOC_EINVAL, "null pointer");
   if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "backtrack called before bellman");
   // the per-subproblem budgets must lie in [0, B]: checked by the start kernels on the device (start_budget), which
-  // report an out-of-range B_use[k] as status[k] = MIOC_ESTATE -- no host read-back, so the device TRM loop
-  // (trm_batch.py) enqueues its trials without a synchronisation
+  // report an out-of-range B_use[k] as status[k] = MIOC_ESTATE -- no host read-back of the budgets.  (The first
+  // backtrack after a DP that spans several workgroups with in-launch hand-offs -- the persistent separable DP, the
+  // segmented fused separable DP, the segmented p=Inf recursion -- still synchronises once to read that DP's
+  // timeout word, run_backtrack/check_run; every later backtrack of the same DP enqueues without one.)
   ctx->Bvec = d_B_use;
   rc = run_backtrack(ctx, ctx->B, d_u_out, d_phi_star, d_status);
   ctx->Bvec = nullptr;
@@ -1263,14 +1275,16 @@ int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
   // slot 6: the separable transform's persistent DPs redone with per-step launches (cooperative launch refused or a
   // dependency wait timed out) -- its kernels write no c[6]; the pyramid's value-collision count otherwise
   // slot 8: row segments per subproblem of the last fused separable DP (0: the one-lane-per-row kernel)
-  const int64_t c6 = ctx->algo == MIOC_ALGO_SEPARABLE || ctx->algo == MIOC_ALGO_FUSED_SEPARABLE
+  const int64_t c6 = ctx->algo == MIOC_ALGO_SEPARABLE || ctx->algo == MIOC_ALGO_FUSED_SEPARABLE ||
+                             ctx->algo == MIOC_ALGO_PINF
                          ? ctx->n_persist_fallbacks
                          : c[6];
   // slot 9: after a p=Inf segmented walk, its subproblems left to the serial walk (-1: the serial walk ran alone)
   int32_t fserial = -1;
   if (ctx->algo == MIOC_ALGO_PINF && ctx->last_pinf_fwalk && ctx->pinf.fneed)
     HIP_TRY(ctx, hipMemcpy(&fserial, ctx->pinf.fneed + ctx->K, sizeof fserial, hipMemcpyDeviceToHost));
-  const int64_t all[10] = {c[0], c[1], f[2], f[3], c[4], c[5], c6, ctx->occupancy,
+  // slot 3: internal-consistency failures of the backtrack (f[3]) and of the DP's tables (c[3]: seam-list overflow)
+  const int64_t all[10] = {c[0], c[1], f[2], (int64_t)f[3] + c[3], c[4], c[5], c6, ctx->occupancy,
                            ctx->algo == MIOC_ALGO_FUSED_SEPARABLE ? ctx->last_fsep_seg : 0, fserial};
   for (int32_t q = 0; q < n && q < 10; ++q) counters[q] = all[q];
   return MIOC_OK;

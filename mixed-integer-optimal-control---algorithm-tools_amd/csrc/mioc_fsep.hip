@@ -529,10 +529,8 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
         // branch-free: a target outside the trust region writes this row's pad word (column L) instead
         double *const dst = v ? Fw + (bx0 * FS + x0) : padw;
         *dst = o[t];
-#ifndef FSEP_EXP_NOU  // timing experiment only (no argmin table): without the U byte stores
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(jw[t >> 2] >> (8 * (t & 3))), Ur,
                                              v && o[t] < INFINITY ? ub + x0 * R + bx0 : 0x40000000, 0, 0);
-#endif
       }
     }
     FS_T(w1);

@@ -291,9 +291,7 @@ __global__ __launch_bounds__(512) void k_fused_run(ProblemDev P, LevelsDev Lv, d
         }
         ov[t] = best;
         const int c = cp + bt[l];  // U goes to HBM at once; the value waits for the barrier
-#ifndef FU_NOU
         if (c <= B && best < INFINITY) Ui[(size_t)l * R + c] = (uint8_t)arg;
-#endif
       }
     }
     FU_T(s1);

@@ -105,11 +105,12 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
                          const int32_t *ranks, double *u_out, double *phi_star, int32_t *status);
 
 // ---- L1-ball pyramid (mioc_pyramid.hip) + staging-layout backtrack (mioc_generic.hip) -------------
-// slab_shift: 0 = sphere order (pyramid); sdt_slab_shift(G) for the separable transform (slab-major, see k_pyr_order)
-// same2 (nullable): [K][nt] int32, u_old(s) == u_old(s + 2) bit for bit (0 for s >= nt - 2); strad (nullable, slab
-// mode): [K][nt][8 slabs][32] uint16, the in-slab offsets of the second elements of seam-straddling position pairs
-hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int slab_shift,
-                            int32_t *same2 = nullptr, uint16_t *strad = nullptr);
+// same2 (nullable): [K][nt] int32, u_old(s) == u_old(s + 2) bit for bit (0 for s >= nt - 2); strad (nullable):
+// [K][nt][8 waves][32] uint16, per wave of the persistent separable driver the in-wave offsets of the second elements
+// of seam-straddling position pairs
+// counters (nullable): [3] += seams a wave's list could not hold (an internal-consistency failure, must stay 0)
+hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm,
+                            int32_t *same2 = nullptr, uint16_t *strad = nullptr, int32_t *counters = nullptr);
 hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm, double *S,
                                size_t s_stride);
 hipError_t launch_pyr_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
@@ -119,8 +120,6 @@ size_t pyr_lds_bytes(const PyrGeom &G);
 // separable L1 transform (mioc_sdt.hip): same staging layout, 8^M grids (M = 3, 4), beta > 0
 bool sdt_supported(const PyrGeom &G);
 bool sdt_seam_lists(const PyrGeom &G);  // the persistent driver loads straddling pair elements by seam lists (k_pyr_order)
-int sdt_slab_shift(const PyrGeom &G);  // the sphere-order mode the separable transform's kernels were built for
-int sdt_flag_words(const PyrGeom &G);  // persistent driver: hand-off flags per row (one per wave under SDT_SLAB)
 size_t sdt_lds_bytes(const PyrGeom &G);
 constexpr int kSdtMaxBuffers = 192;  // persistent separable transform: staging buffers S_i, step i in buffer i % NB
 constexpr int kSdtDefaultBuffers = 128;  // (C4: 128 x 8.4 MB + the 2.1 GB row-0 array, under the 4 GiB buffer range)
@@ -139,6 +138,17 @@ hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &L
                           size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, unsigned spin_limit,
                           size_t lds);
 int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds);
+// the two-workgroups-per-row persistent driver (mioc_sdt2.hip, 8^4 grids): the sphere orders packed per position pair
+// ([K][nt][2048] uint32 pair words, [K][nt][4][32] seam words), then the DP; flags [K][B+1][2] done, [K][B+1][2]
+// loaded, err (zeroed by the caller)
+bool sdt_pair_supported(const PyrGeom &G, int K, int B, int ncu, int bpc);
+size_t sdt_pair_lds_bytes();
+int sdt_pair_blocks_per_cu();
+hipError_t launch_sdt_pack(hipStream_t s, const ProblemDev &P, const uint32_t *perm, uint32_t *pack, uint32_t *seams,
+                           int32_t *counters);
+hipError_t launch_sdt_pair(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
+                           const uint32_t *pack, const uint32_t *seams, double *S, size_t kstride, int NB, uint16_t *UU,
+                           size_t uu_stride_k, int32_t *counters, int32_t *flags, unsigned spin_limit);
 hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
                                 const double *S0, size_t s_stride, int Bu, Start *start);
 hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,
@@ -190,8 +200,10 @@ void pinf_plan(int RP, int nt, PinfDev &D);
 hipError_t launch_pinf_prep(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D);
 // ncu: the device's CUs; flags (K·ceil((B+1)/32) + 1 zeroed words, or null): lets few subproblems run in row segments
 // on several CUs, *segmented then says so (the caller checks the error word after it, check_run)
+// variant (nullable): the name of the recursion kernel launched (k_pinf_recur_mc, k_pinf_recur_xr or k_pinf_recur),
+// which names the timing window (mioc_kernel_stats)
 hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ncu, int32_t *flags,
-                             unsigned spin_limit, bool *segmented);
+                             unsigned spin_limit, bool *segmented, const char **variant = nullptr);
 int pinf_recur_segments(const ProblemDev &P);  // row segments of k_pinf_recur_mc per subproblem (its error word's offset)
 hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D, int Bu,
                              Start *start);
@@ -305,8 +317,14 @@ struct mioc_ctx {
   uint32_t *d_perm = nullptr;      // [K][nt][L] sphere order of u_old(i): rank | (L1 distance << 16)
   int32_t *d_same2 = nullptr;      // [K][nt] u_old(i) == u_old(i+2) (the persistent separable driver's order reuse)
   size_t same2_cap = 0;
-  uint16_t *d_strad = nullptr;     // [K][nt][8][32] seam-straddling pairs per slab (slab-major sphere orders)
+  uint16_t *d_strad = nullptr;     // [K][nt][8][32] seam-straddling pairs per wave (k_sdt_run's 8-wave layout)
   size_t strad_cap = 0;
+  uint32_t *d_pack = nullptr;      // [K][nt][2048] packed position pairs (k_sdt_pair)
+  size_t pack_cap = 0;
+  uint32_t *d_pseam = nullptr;     // [K][nt][4][32] seam words (k_sdt_pair)
+  size_t pseam_cap = 0;
+  int opt_sdt_pair = 1;            // 8^4 persistent separable DP: two workgroups per row (MIOC_OPT_SDT_PAIR)
+  const char *last_sdt_kernel = "";  // the persistent separable kernel of the last DP (k_sdt_pair / k_sdt_run)
   size_t perm_cap = 0;
   bool opt_persist = true;         // separable transform: one persistent launch (MIOC_OPT_PERSIST)
   bool force_steps = false;        // redo of a persistent DP whose waits timed out: per-step launches

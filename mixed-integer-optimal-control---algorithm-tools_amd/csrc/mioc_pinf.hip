@@ -764,8 +764,9 @@ bool launch_pinf_mc(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ns
 int pinf_recur_segments(const ProblemDev &P) { return (P.B + 1 + 64 / PINF_RECUR_MC_LANES - 1) / (64 / PINF_RECUR_MC_LANES); }
 
 hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &D, int ncu, int32_t *flags,
-                             unsigned spin_limit, bool *segmented) {
+                             unsigned spin_limit, bool *segmented, const char **variant) {
   if (segmented) *segmented = false;
+  if (variant) *variant = "k_pinf_recur";
   // few subproblems, classes <= 32, tall enough: row segments of 32 on several CUs (k_pinf_recur_mc); the flags
   // (K·nseg + 1 words, zeroed by the caller) carry the hand-off and the error word
   {
@@ -782,6 +783,7 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
         // rows above B (the top segment's finite values, and the rows no segment computes): +Inf, after the launch
         if (P.B + 1 < P.RP) hipLaunchKernelGGL(k_pinf_rfill, dim3(64, P.K), dim3(256), 0, s, P, D, P.B + 1);
         *segmented = true;
+        if (variant) *variant = "k_pinf_recur_mc";
         return hipGetLastError();
       }
     }
@@ -797,6 +799,7 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
     const size_t lds = (size_t)(2 * (D.BWP + P.RP) + 2 * CH * D.BWP + 2 * 8) * sizeof(double);
     if (32 * 8 + 1 < P.RP) hipLaunchKernelGGL(k_pinf_rfill, dim3(64, P.K), dim3(256), 0, s, P, D, 32 * 8 + 1);
     hipLaunchKernelGGL((k_pinf_recur_xr<32, 8>), dim3(P.K), dim3(512), lds, s, P, D, CH);
+    if (variant) *variant = "k_pinf_recur_xr";
     return hipGetLastError();
   }
   if (G * pairs > 1024) pairs = 1024 / G;

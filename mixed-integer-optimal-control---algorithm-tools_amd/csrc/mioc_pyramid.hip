@@ -820,12 +820,9 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
 // row c' - s of S_i (the sphere s) form one contiguous run per sphere.  Inside a sphere the ranks ascend (a
 // stable counting sort), so the order is a function of u_old(i) alone: steps with equal u_old share one table,
 // which the persistent separable-transform driver uses to skip reloading it.
-// slab_shift > 0 (separable transform): slab-major -- the ranks are grouped first by their top grid coordinate
-// j >> slab_shift (the slab a row workgroup's wave owns), then by sphere, then ascending; every slab is one contiguous
-// block of L/8 positions, so the wave that owns a slab loads exactly its slab's sources (mioc_sdt.hip).
-__global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all, int slab_shift,
-                                                   int32_t *same2, uint16_t *strad) {
-  constexpr int NK = 8 * 64;        // bucket keys: slab << 6 | min(distance, 63)
+__global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all, int32_t *same2,
+                                                   uint16_t *strad, int32_t *counters) {
+  constexpr int NK = 64;            // bucket keys: min(distance, 63)
   __shared__ int start[NK];         // the next free position of each bucket
   __shared__ int wcnt[4][NK + 1];   // ranks of the current chunk per wave and bucket (NK: the inactive lanes)
   const int i = blockIdx.x, k = blockIdx.y, L = G.ncol * G.n[0], M = G.M;
@@ -852,7 +849,7 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
     }
     return min(d, 0xFFFF);
   };
-  auto key = [&](int j, int d) { return (slab_shift ? (j >> slab_shift) << 6 : 0) | min(d, 63); };
+  auto key = [&](int j, int d) { return min(d, 63); };
   for (int j = tid; j < L; j += blockDim.x) atomicAdd(&start[key(j, dist(j))], 1);
   __syncthreads();
   if (tid == 0) {
@@ -865,14 +862,14 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
   }
   __syncthreads();
   // chunks of 256 consecutive ranks in order; inside a chunk, a rank's place among its bucket's ranks is the number of
-  // lower lanes of its wave with the same key (10 ballots) plus those of the lower waves
+  // lower lanes of its wave with the same key (7 ballots) plus those of the lower waves
   for (int c = 0; c < L; c += 256) {
     const int j = c + tid;
     const bool act = j < L;
     const int d = act ? dist(j) : 0, b = act ? key(j, d) : NK;
     unsigned long long same = ~0ull;
 #pragma unroll
-    for (int q = 0; q < 10; ++q) {
+    for (int q = 0; q < 7; ++q) {
       const unsigned long long m = __ballot((b >> q) & 1);
       same &= ((b >> q) & 1) ? m : ~m;
     }
@@ -894,29 +891,31 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
   }
   // strad (the persistent separable driver at 8^4, 8 waves of 512 positions): per wave, the in-wave offsets of the odd
   // positions whose distance differs from position p-1's -- the second elements of the 16-byte position pairs that
-  // straddle a sphere seam -- 0xFFFF-padded to 32.  A wave's positions (sd_seam_pos, mioc_sdt.hip): slab mode, the
-  // slab p / (L/8) (at most 21 seams in a slab: 22 distances); else positions 2(64w + l + (L/8)·q) + {0, 1} at offset
-  // 128q + 2l + {0, 1} (at most 28 seams in the whole order: 29 distances)
+  // straddle a sphere seam -- 0xFFFF-padded to 32.  A wave's positions (sd_seam_pos, mioc_sdt.hip): positions
+  // 2(64w + l + (L/8)·q) + {0, 1} at offset 128q + 2l + {0, 1} (at most 28 seams in the whole order: 29 distances)
   if (strad) {
     uint16_t *st = strad + ((size_t)k * P.nt + i) * 8 * 32;
-    const int SL = L / 8, T = L / 8;
+    const int T = L / 8;
     for (int e = tid; e < 8 * 32; e += blockDim.x) st[e] = 0xFFFFu;
     if (tid < 8) start[tid] = 0;  // per-wave counts
     __syncthreads();
     for (int p = 2 * tid + 1; p < L; p += 2 * blockDim.x)
       if ((perm[p] >> 16) != (perm[p - 1] >> 16)) {
         const int u = (p - 1) >> 1, t = u % T;
-        const int wv = slab_shift ? p / SL : t >> 6;
-        const int o = slab_shift ? p - wv * SL : 128 * (u / T) + 2 * (t & 63) + 1;
+        const int wv = t >> 6;
+        const int o = 128 * (u / T) + 2 * (t & 63) + 1;
         const int e = atomicAdd(&start[wv], 1);
-        if (e < 32) st[wv * 32 + e] = (uint16_t)o;
+        if (e < 32)
+          st[wv * 32 + e] = (uint16_t)o;
+        else if (counters)  // the list cannot hold this seam: a loud internal-consistency failure (diagnostics [3])
+          atomicAdd(&counters[3], 1);
       }
   }
 }
 
-hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int slab_shift,
-                            int32_t *same2, uint16_t *strad) {
-  hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm, slab_shift, same2, strad);
+hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int32_t *same2,
+                            uint16_t *strad, int32_t *counters) {
+  hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm, same2, strad, counters);
   return hipGetLastError();
 }
 

@@ -36,74 +36,17 @@
 #include <cstdint>
 
 #include "mioc_internal.h"
+#include "mioc_sdt_common.h"
 
 namespace mioc {
 
-constexpr int SD_RB = 12;                // payload rank bits (L <= 4096)
-constexpr int SD_CB = 6;                 // payload near-tie count bits, below the rank (at most 56 merges per value)
-constexpr int SD_CNT = (1 << SD_CB) - 1; // near-tie count mask: nonzero = flagged
-constexpr int SD_PAY = (1 << (SD_CB + SD_RB)) - 1;  // payload mask: 18 low mantissa bits
-constexpr int SD_GRID = 52 - SD_CB - SD_RB;         // g = 2^(E - SD_GRID) for the binade [2^E, 2^(E+1))
-constexpr int SD_COOP = 8;               // listed targets up to this many: whole-workgroup scans, else one wave each
-constexpr int SD_FEW = 4;                // rows with at most this many targets go straight to the exact scan
-constexpr int SD_SPARSE = 4;             // rows with at most this many finite sources: direct minimum over them
-constexpr int SD_LCAP = 512;             // listed targets kept in LDS; beyond, the scan sweeps every rank
-#ifndef SDT_RUN_MINW
-#define SDT_RUN_MINW 2                   // persistent kernel: waves per SIMD the registers must allow (4: two workgroups per CU, but the row code then spills)
-#endif
-#ifndef SDT_PASS_SPLIT
-#define SDT_PASS_SPLIT 0                 // passes as two independent half-chains + a combine (experiment)
-#endif
-#ifndef SDT_WAVE_LOCAL
-#define SDT_WAVE_LOCAL 1                 // passes over the low M-1 dimensions sync per wave; outputs in their own buffer
-#endif
-#ifndef SDT_PERM_SKIP
-#define SDT_PERM_SKIP 1                  // persistent driver: no sphere-order reload where u_old repeats (see go())
-#endif
-#ifndef SDT_PREFETCH
-#define SDT_PREFETCH 1                   // load the sphere orders ahead of the dependency wait
-#endif
-#ifndef SDT_PRED
-#define SDT_PRED 0                       // persistent driver: stamp with a per-row predicted scale (see sdt_body)
-#endif
-#ifndef SDT_STRAD
-#define SDT_STRAD 1                      // persistent driver: per-wave seam lists instead of one straddle load per pair
-#endif
-#ifndef SDT_HOIST
-#define SDT_HOIST 0                      // persistent driver: read the next row's sphere-order entries early (SdPipe)
-#endif
-#ifndef SDT_SPREAD
-#define SDT_SPREAD 0                     // persistent driver: the next row's loads issued between the passes (SdPipe; measured slower)
-#endif
-#ifndef SDT_BF
-#define SDT_BF 1                         // row body: straddle pairs and +Inf stamps without branches (in-wave LDS order)
-#endif
-#ifndef SDT_P0STAMP
-// row body: the first phase writes the raw Ψ to the transform buffer as well and pass 0 stamps the values it reads,
-// so the stamp scatter and its barrier go; the next row's loads issue right after the statistics' reduction
-// (A/B builds: 0, the separate stamp phase)
-#define SDT_P0STAMP 1
-#endif
-#ifndef SDT_PRED_PROBE
-#define SDT_PRED_PROBE 0                 // diagnostic build: count where a same-binade predicted scale would miss
-#endif
-#ifndef SDT_SLAB
-#define SDT_SLAB 0                       // slab-major sphere order: a wave loads and stamps only its own slab (sdt_body)
-#endif
-constexpr int SD_PRED_ROWS = 64;         // rows of a workgroup's chunk that keep a predicted scale (the others: none)
-constexpr int SD_STRAD_N = 32;           // seam list entries per wave (<= 21 seams in a slab, <= 28 in a sphere order)
+constexpr int SD_STRAD_N = 32;           // seam list entries per wave (<= 28 seams in a sphere order)
 // the persistent driver at M = 4: the position pairs that straddle a sphere seam get their second element from one
 // straddle load per lane (a per-wave list of the wave's seams, k_pyr_order) instead of one masked 8-byte load per pair
 // and lane (SdRaw)
-// hand-off flags per row: SDT_SLAB's row flow hands off per slab (wave w of a row reads and writes only slab w's
-// positions), so every wave has its own `done` / `loaded` flag; else one per row
-template <int M>
-__host__ __device__ constexpr int sd_flag_words() {
-  return SDT_PRED && SDT_SLAB ? (1 << (3 * M - 3)) / 64 : 1;
-}
 template <int M>
 __host__ __device__ constexpr bool sd_strad() {
-  return SDT_STRAD && M == 4;
+  return M == 4;
 }
 
 // Diagnostic build only (make stamps -> libmioc_stamps.so): per-workgroup phase clocks of the last launch.
@@ -183,116 +126,25 @@ __shared__ unsigned long long sd_tl_lds[64][8];
   } while (0)
 #endif
 
-// v_min_f64 without llvm.minnum's canonicalising v_max_f64 x,x on every operand (inputs are finite or +Inf)
-__device__ __forceinline__ double sd_min(double a, double b) {
-  double r;
-  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ double sd_max(double a, double b) {
-  double r;
-  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 
-// The thread index as a value the compiler cannot hoist out of the persistent driver's row loop: everything the
-// row body derives from it (LDS addresses of the passes, swizzles, store offsets) is recomputed per row instead of
-// being kept live in VGPRs across the whole loop, which would leave the body no registers (spills to scratch join
-// the vector-memory queue the driver keeps busy).
-__device__ __forceinline__ int sd_tid() {
-  int t = (int)threadIdx.x;
-  asm volatile("" : "+v"(t));
-  return t;
-}
-
-// LDS-only workgroup barrier: __syncthreads() would also wait for every outstanding global load and store of
-// the wave, which the persistent driver keeps in flight across the row body on purpose
-__device__ __forceinline__ void sd_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// merge two disjoint candidate sets (their minima a, b): the smaller keeps its payload; a near tie counts
-// one.  |a - b| is exact (one binade), +Inf - +Inf is NaN and never flags.
-__device__ __forceinline__ double sd_merge(double a, double b, double tol) {
-  const double m = sd_min(a, b);
-  const bool close = fabs(a - b) <= tol;
-  return __hiloint2double(__double2hiint(m), (int)((unsigned)__double2loint(m) + (close ? 1u : 0u)));  // v_addc
-}
-
-// Wave-wide reductions through DPP (no LDS round trip, unlike __shfl_xor's ds_bpermute): four steps leave every
-// lane with its 16-lane row's result (quad_perm xor 1, xor 2, row_half_mirror, row_mirror), then the four row
-// results are read as scalars.  bound_ctrl: every lane has a source under these controls, so no old value is
-// needed (and no register initialised for it).
-template <int CTRL>
-__device__ __forceinline__ int sd_dpp_i(int x) {
-  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true);
-}
-template <int CTRL>
-__device__ __forceinline__ double sd_dpp_d(double x) {
-  return __hiloint2double(sd_dpp_i<CTRL>(__double2hiint(x)), sd_dpp_i<CTRL>(__double2loint(x)));
-}
-__device__ __forceinline__ double sd_rdl(double x, int l) {
-  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l), __builtin_amdgcn_readlane(__double2loint(x), l));
-}
-// (min and max without llvm.minnum's canonicalisation: the operands are finite or ±Inf, never NaN)
-__device__ __forceinline__ void sd_wave_stats(double &mn, double &mx) {
-#define SD_STEP(C)                             \
-  mn = sd_min(mn, sd_dpp_d<C>(mn));            \
-  mx = sd_max(mx, sd_dpp_d<C>(mx));
-  SD_STEP(0xB1) SD_STEP(0x4E) SD_STEP(0x141) SD_STEP(0x140)
-#undef SD_STEP
-  mn = sd_min(sd_min(sd_rdl(mn, 0), sd_rdl(mn, 16)), sd_min(sd_rdl(mn, 32), sd_rdl(mn, 48)));
-  mx = sd_max(sd_max(sd_rdl(mx, 0), sd_rdl(mx, 16)), sd_max(sd_rdl(mx, 32), sd_rdl(mx, 48)));
-}
-
-// LDS position of rank r (3 bits per dimension): XOR swizzle so that each 32-lane half of a pass reads
-// 32 distinct 8-byte bank slots in every pass: slot = (x0 ^ x1) + 8·((x1 ^ x2) & 3)
-__device__ __forceinline__ int sd_swz(int r) { return r ^ ((r >> 3) & 7) ^ (((r >> 6) & 3) << 3); }
-
-// The first position of thread tid's q-th position pair (q < 4) in a staging row / sphere order.  SDT_SLAB: the
-// sphere orders are slab-major (k_pyr_order, slab = the top grid coordinate of the rank), so wave w's pairs cover
-// exactly slab w's block of L/8 positions, 128 consecutive positions per q (16 bytes per lane: coalesced); else
-// 2(tid + T·q) (the same for M = 3, one wave).
+// The first position of thread tid's q-th position pair (q < 4) in a staging row / sphere order: 2(tid + T·q), so a
+// wave's pairs are 128 consecutive positions per q (16 bytes per lane: coalesced).
 template <int M>
 __device__ __forceinline__ int sd_p2(int tid, int q) {
-  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
-  if constexpr (SDT_SLAB)
-    return (tid >> 6) * (L / NW) + 2 * ((tid & 63) + 64 * q);
-  else
-    return 2 * (tid + T * q);
+  constexpr int L = 1 << (3 * M), T = L / 8;
+  return 2 * (tid + T * q);
 }
-// The position of the level at distance 0 from u_old (when u_old is on the grid): the head of the first sphere --
-// position 0 of the sphere order, or (SDT_SLAB) the first position of u_old's slab.  Callers check b̃ == 0 there.
-// (sd_strad) the position of in-wave offset o (0 .. 511) of wave w: its slab under SDT_SLAB, else the wave's four runs
-// of 128 positions 2(64w + l + T·q) + {0, 1} (o = 128q + 2l + {0, 1}); k_pyr_order builds the seam lists with the same map
+// (sd_strad) the position of in-wave offset o (0 .. 511) of wave w: the wave's four runs of 128 positions
+// 2(64w + l + T·q) + {0, 1} (o = 128q + 2l + {0, 1}); k_pyr_order builds the seam lists with the same map
 template <int M>
 __device__ __forceinline__ int sd_seam_pos(int w, int o) {
-  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
-  if constexpr (SDT_SLAB)
-    return w * (L / NW) + o;
-  else
-    return 2 * T * (o >> 7) + 128 * w + (o & 127);
+  constexpr int L = 1 << (3 * M), T = L / 8;
+  return 2 * T * (o >> 7) + 128 * w + (o & 127);
 }
+// The position of the level at distance 0 from u_old (when u_old is on the grid): the head of the first sphere,
+// position 0 of the sphere order.  Callers check b̃ == 0 there.
+constexpr int kSdHeadPos = 0;
 
-template <int M>
-__device__ __forceinline__ int sd_headpos(const PyrGeom &G, double uo_top) {
-  constexpr int L = 1 << (3 * M);
-  if constexpr (SDT_SLAB)
-    return min(max((int)uo_top - G.base[M - 1], 0), 7) * (L / 8);
-  else
-    return 0;
-}
-
-// rank of element x of line q in the pass over dimension m (q enumerates the other coordinates, lowest
-// dimension fastest)
-__device__ __forceinline__ int sd_rank(int q, int m, int x) {
-  const int lo = q & ((1 << (3 * m)) - 1);
-  return lo | (x << (3 * m)) | ((q >> (3 * m)) << (3 * (m + 1)));
-}
-
-// L1 distance between two ranks of the 8^M grid with one v_sad_u8: a rank spread to one byte per dimension
-__device__ __forceinline__ unsigned sd_bytes(unsigned r) {
-  return (r & 7u) | ((r & 0x38u) << 5) | ((r & 0x1C0u) << 10) | ((r & 0xE00u) << 15);
-}
-__device__ __forceinline__ unsigned sd_l1(unsigned pa, unsigned pb) { return __builtin_amdgcn_sad_u8(pa, pb, 0u); }
 
 // Exact scan of the listed targets: the reference loop (HelpFunctions.jl:60-77) for one cell each.
 // COOP: the whole workgroup scans one target at a time (thread t: sources t + T·s, ascending), then a
@@ -397,11 +249,6 @@ __device__ __forceinline__ void sd_scan(const uint16_t *list, int nl, const doub
 // bytes an `sc1` load), so there its staging loads and stores are `sc1` buffer loads / stores (aux 16),
 // 16 bytes per lane where the layout allows (narrow `sc1` stores cost 2-3x per byte and write partial lines).
 // `base` is wave-uniform (a subproblem's staging block or one row of it), `bytes` its extent (< 2^31).
-typedef unsigned int sd_u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int sd_u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sd_rsrc(const double *base, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base), 0, bytes, 0x00020000);
-}
 template <bool SC1>
 __device__ __forceinline__ double sd_load8(const double *base, int bytes, int e) {
   if constexpr (SC1) {
@@ -449,10 +296,7 @@ struct SdtShared {
   int nsp;   // sparse rows: the finite sources (rank, Ψ)
   int spj[SD_SPARSE];
   double spv[SD_SPARSE];
-  int cnt[4];  // targets sent to the exact scan (near ties, direct rows), rows stamped twice (predicted scale
-              // missed); flushed to the global counters [0], [1], [4] once
-  int rfail[NW];  // per wave: a finite Ψ outside the row's predicted range (SDT_PRED)
-  double pred[SD_PRED_ROWS][2];  // per chunk row: the predicted range [lo, hi] of its Ψ (lo = +Inf: none yet)
+  int cnt[2];  // targets sent to the exact scan (near ties, direct rows); flushed to the global counters [0], [1]
 };
 
 template <int M>
@@ -473,18 +317,14 @@ __host__ __device__ constexpr size_t sd_dfuo_offset() {  // then df(:, i), u_old
   return sd_strad_offset<M>() + 2 * 8 * SD_STRAD_N * sizeof(uint16_t);
 }
 template <int M>
-__host__ __device__ constexpr size_t sd_out_offset() {  // then the row's outputs (natural order), SDT_WAVE_LOCAL
+__host__ __device__ constexpr size_t sd_out_offset() {  // then the row's outputs (natural order)
   return sd_dfuo_offset<M>() + ((sd_dfuo_stride<M>() * (((size_t)1 << (3 * M - 3)) / 64) + 255) & ~(size_t)255);
 }
 template <int M>
 __host__ __device__ constexpr size_t sd_lds_total() {
-  return SDT_WAVE_LOCAL ? sd_out_offset<M>() + ((size_t)1 << (3 * M)) * sizeof(double)
-                        : sd_dfuo_offset<M>() + sd_dfuo_stride<M>() * (((size_t)1 << (3 * M - 3)) / 64);
+  return sd_out_offset<M>() + ((size_t)1 << (3 * M)) * sizeof(double);
 }
 
-// Wave-local LDS ordering: this wave's LDS stores are complete before its next LDS reads (LDS instructions of one
-// wave execute in order; the wait also keeps the compiler from moving accesses across)
-__device__ __forceinline__ void sd_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // The sphere orders a step reads (step i+1, for the sources) and writes (step i, for the output row), as the
 // position pairs 2(tid + T·q) + {0, 1} of this thread, plus both heads (position 0).  Loaded at the start of
@@ -508,8 +348,8 @@ __device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restr
     pm.in[q] = *reinterpret_cast<const uint2 *>(pin + sd_p2<M>(tid, q));
     pm.out[q] = *reinterpret_cast<const uint2 *>(pout + sd_p2<M>(tid, q));
   }
-  pm.pin_h = sd_headpos<M>(G, P.uold[((size_t)k * nt + i + 1) * M + M - 1]);
-  pm.pout_h = sd_headpos<M>(G, P.uold[((size_t)k * nt + i) * M + M - 1]);
+  pm.pin_h = kSdHeadPos;
+  pm.pout_h = kSdHeadPos;
   pm.hin = pin[pm.pin_h];
   pm.hout = pout[pm.pout_h];
 }
@@ -519,14 +359,11 @@ __device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restr
 //            S_{i+1}[c' - b̃_j(i+1)][pos_{i+1}(j)] (+Inf where that row is below 0); loaded by the caller (the
 //            persistent driver issues these loads one row ahead, so they may still be in flight on entry).
 //   pin    : LDS copy of the sphere order of step i+1 (rank | b̃ << 16 by position), pout: of step i.
-//   h      : the driver's pipeline hooks (no-ops for one launch per step): h.poll() at the start (SDT_PRED: issue
-//            this wave's dependency polls without waiting); h.early() once every wave has consumed `v` (!SDT_PRED:
-//            publish `loaded`, issue the polls); h.drain() right before the first barrier after the last use of `v`
-//            and `pin` (this wave's stores of the previous row have landed); h.go() after that barrier (publish
-//            `loaded` (SDT_PRED) and the previous row, check the polls, issue the next row's loads, the next step's
-//            sphere order and df / u_old).  A timed-out wait sets sh.stop, which the driver reads after the row.
-//   prow   : (persistent driver, SDT_PRED) this row's predicted Ψ range [lo, hi] in LDS, refreshed here on a miss;
-//            null: none
+//   h      : the driver's pipeline hooks (no-ops for one launch per step): h.early() once every wave has consumed `v`
+//            (publish `loaded`, issue the polls); h.go() after the first barrier (check the polls, issue the next row's
+//            loads, the next step's sphere order and df / u_old); h.late_drain() before the barrier after the winners
+//            (this wave's stores of the previous row have landed), h.publish() after it (the previous row is done).  A
+//            timed-out wait sets sh.stop, which the driver reads after the row.
 //   smask, srank, xs: (sd_strad) the pairs q whose second element straddles a sphere seam (bit 3q+2 of smask: not
 //            this lane's to store), and this lane's straddle element (rank srank, value xs; srank < 0: none)
 // Returns 1 if the row is all +Inf (no target in the trust region or no finite source), else 0.
@@ -540,15 +377,15 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
                                          const uint32_t *pout,
                                          double *Sout, uint16_t *UU, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
                                          unsigned char *sds, Hooks &h, const double *__restrict__ df_all,
-                                         const double *__restrict__ uo_all, double *prow, unsigned smask = 0,
-                                         int srank = -1, double xs = 0.0) {
+                                         const double *__restrict__ uo_all, unsigned smask = 0, int srank = -1,
+                                         double xs = 0.0) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
   double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
   double *dtv = psi + L;                                // [L] transform values (swizzled)
   uint16_t *uu = reinterpret_cast<uint16_t *>(dtv + L);  // [L] the U row (natural order)
   // [L] the outputs (natural order): a buffer of their own, so that the winners of one wave need not wait for every
-  // other wave's last pass (SDT_WAVE_LOCAL); else the transform buffer after a barrier
-  double *outv = SDT_WAVE_LOCAL ? reinterpret_cast<double *>(sds + sd_out_offset<M>()) : dtv;
+  // other wave's last pass
+  double *outv = reinterpret_cast<double *>(sds + sd_out_offset<M>());
   uint16_t *list = uu + L;                              // [SD_LCAP] targets for the exact scan
   const int tid = sd_tid(), lane = tid & 63, w = tid >> 6;
   const int B = P.B;
@@ -565,7 +402,6 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   uint2 ein[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) ein[q] = ein_in[q];
-  if constexpr (PERSIST && SDT_PRED && !SDT_SLAB) h.poll();  // this wave's dependency polls, checked in go()
   // ---- this thread's targets: ranks tid | x << 3(M-1) (the lines of the last pass) -----------------
   double a[M];
   int lb[M], uo[M];
@@ -619,7 +455,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     const double y = (x - ref) * inv + base;
     return __hiloint2double(__double2hiint(y), (__double2loint(y) & ~SD_PAY) | (j << SD_CB));
   };
-  // the stamp, +Inf kept +Inf, without a branch (SDT_BF)
+  // the stamp, +Inf kept +Inf, without a branch
   auto stamp_inf = [&](double x, int j) {
     const double y = stamp(x, j);
     const unsigned m = x < INFINITY ? ~0u : 0u;
@@ -629,7 +465,6 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   // ---- one pass of the transform: forward and backward sweep along the 8 levels of dimension m, unit step 1.0;
   // this thread's line is read from and (but for the last pass) written back to the swizzled LDS values ---------
   double o[8];
-  constexpr bool P0 = SDT_P0STAMP && !(PERSIST && SDT_PRED);
   auto pass = [&](int m) {
     int pos[8];
 #pragma unroll
@@ -637,27 +472,10 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       pos[x] = sd_swz(sd_rank((int)threadIdx.x, m, x));  // tid-only: hoisted out of the row loop
       o[x] = dtv[pos[x]];
     }
-    if (P0 && m == 0) {  // (SDT_P0STAMP) the raw Ψ of ranks 8·tid + x: stamp them here
+    if (m == 0) {  // the raw Ψ of ranks 8·tid + x (written with Ψ by rank): stamp them here
 #pragma unroll
       for (int x = 0; x < 8; ++x) o[x] = stamp_inf(o[x], sd_rank((int)threadIdx.x, 0, x));
     }
-#if SDT_PASS_SPLIT
-    // two independent chains (prefix f over sources <= x, strict suffix b over sources > x: disjoint candidate
-    // sets), then one merge per point: half the dependency depth of the in-place sweeps, 20 merges instead of 14
-    {
-      double f[8], b[8];
-      f[0] = o[0];
-      b[7] = o[7];
-#pragma unroll
-      for (int x = 1; x < 8; ++x) {
-        f[x] = sd_merge(o[x], f[x - 1] + 1.0, tol);
-        if (x < 7) b[7 - x] = sd_merge(o[7 - x], b[8 - x] + 1.0, tol);
-      }
-#pragma unroll
-      for (int x = 0; x < 7; ++x) o[x] = sd_merge(f[x], b[x + 1] + 1.0, tol);
-      o[7] = f[7];
-    }
-#else
     // in place: after the forward sweep o[x] covers the sources at <= x; a backward merge of o[x] with
     // o[x+1] + 1 compares a source at <= x with itself shifted by >= 2, never within tol, so every
     // flagged tie is between two distinct sources (as in a merge of disjoint sets)
@@ -665,159 +483,24 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     for (int x = 1; x < 8; ++x) o[x] = sd_merge(o[x], o[x - 1] + 1.0, tol);
 #pragma unroll
     for (int x = 6; x >= 0; --x) o[x] = sd_merge(o[x], o[x + 1] + 1.0, tol);
-#endif
     if (m + 1 < M) {
 #pragma unroll
       for (int x = 0; x < 8; ++x) dtv[pos[x]] = o[x];
     }
   };
-  // SDT_SLAB: passes 0 .. M-2 run per wave: their lines keep the top grid coordinate (rank bits 3(M-1)..) = the wave
-  // index (the swizzle leaves those bits alone), so a wave reads only what it wrote itself
-  auto wave_passes = [&]() {
-#pragma unroll
-    for (int m = 0; m + 1 < M; ++m) {
-      sd_wave_sync();
-      pass(m);
-    }
-  };
   int nf;
   bool empty;
-  constexpr bool PRED = PERSIST && SDT_PRED;
-  constexpr bool SLAB = PRED && SDT_SLAB;
-  if constexpr (PRED) {
-    // Predicted scale (persistent driver): a row's Ψ move little from one step to the next.  prow holds the exact
-    // range [lo, hi] of this row's Ψ at its previous step; its scale has binade exponent E, and every range up to
-    // R(E) (the widest one whose exact scale still has exponent E) stamps on the same grid.  So the window
-    // [lo - r, hi + r], r = (R(E) - rs)/2 in β units, stamps at once -- no min/max reduction and no barrier before
-    // the stamps -- on the grid the row's own exact range would give whenever its range stays in the window (98 % of
-    // the C4 rows; SDT_PRED_PROBE).  Every finite Ψ is checked to lie in the window; then every bound of the
-    // certification holds as if the window were the row's own min and max (the binade holds it + Smax, tol covers
-    // |Ψ| up to its ends).  A miss (or no prediction yet) redoes the stamps from the exact min and max, which every
-    // wave reduces alongside its stamps anyway (they become the next step's prediction).
-    const double plo = prow ? prow[0] : INFINITY, phi = prow ? prow[1] : -INFINITY;
-    double wlo = plo, whi = phi;
-    if (plo <= phi) {
-      const double rs_p = (phi - plo) * inv + (double)Smax;
-      const int E = ilogb(fmin(rs_p, 0x1p31) * (1.0 + 0x1p-20) + 1.0) + 2;
-      // scale() below: exponent E for rs·(1 + 2^-20) + 1 < 2^(E-1); the last factor keeps the window's computed
-      // range below that bound through the roundings of (whi - wlo)·inv
-      const double R = (ldexp(1.0, E - 1) - 1.0) / (1.0 + 0x1p-20) * (1.0 - 0x1p-30);
-      const double room = fmax(R - rs_p, 0.0) * 0.5 * beta;
-      wlo = plo - room;
-      whi = phi + room;
-    }
-    scale(wlo, whi);
-    const bool miss = !(plo <= phi) || !scale_ok || !(tol < base * 0x1p-20);
-    bool bad = false;
-    double pmn = INFINITY, pmx = -INFINITY;  // the exact range, for the next step (and a miss)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
-        const double x = v[2 * q + hh];  // (sd_strad: +Inf for a straddling second element, written by its loader)
-        const bool fin = x < INFINITY;
-        nv += __popcll(__ballot(fin)) << 16;
-        bad |= fin && !(x >= wlo && x <= whi);
-        pmn = sd_min(pmn, x);
-        pmx = sd_max(pmx, fin ? x : -INFINITY);
-        // (SDT_BF: written anyway -- the straddle lane is in this wave and writes after it, in-wave LDS order)
-        if (SDT_BF || !(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) {
-          psi[j] = x;
-          dtv[sd_swz(j)] = SDT_BF ? stamp_inf(x, j) : fin ? stamp(x, j) : INFINITY;
-        }
-      }
-    if constexpr (sd_strad<M>()) {  // this lane's straddle element
-      const int js = srank & 0xFFFF;
-      const double x = (srank & 0x10000) ? INFINITY : xs;
-      const bool fin = srank >= 0 && x < INFINITY;
-      nv += __popcll(__ballot(fin)) << 16;
-      bad |= fin && !(x >= wlo && x <= whi);
-      pmn = sd_min(pmn, fin ? x : INFINITY);
-      pmx = sd_max(pmx, fin ? x : -INFINITY);
-      if (srank >= 0) {
-        psi[js] = x;
-        dtv[sd_swz(js)] = fin ? stamp(x, js) : INFINITY;
-      }
-    }
-    const bool wbad = __ballot(bad) != 0;
-    sd_wave_stats(pmn, pmx);
-    if (lane == 0) {
-      sh.rnv[w] = nv;
-      sh.rfail[w] = wbad;
-      sh.rmn[w] = pmn;
-      sh.rmx[w] = pmx;
-    }
-    if constexpr (SLAB) {
-      // SDT_SLAB: every Ψ this wave loaded lies in its own slab, so its stamps and passes 0 .. M-2 need no other
-      // wave: they run at once, on the predicted stamps (redone below on a miss; discarded if the row takes no
-      // transform); the row's first barrier comes only before the last pass, with the drain before it (late in the
-      // row: the previous row's stores have long landed) and the pipeline hooks after it
-      h.poll();  // this wave's dependency polls (about as long before go() as their round trip takes)
-      wave_passes();
-      h.wave_done();  // this wave's stores of the previous row have landed: its slab of that row is done
-      h.go();         // its polls matched -> its slab of the next row's loads and of the sphere-order copy
-      sd_bar();       // every wave's passes 0 .. M-2 and counts are in LDS
-    } else {
-      sd_bar();  // Ψ by rank, the stamps and the range of every wave are in LDS; every wave has consumed its loads
-      // `v` and `pin` are dead from here on: the driver may reuse the latter
-      h.go();
-    }
-    SD_STAMP(1);
-    nv = 0;
-    bool fail = miss;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) {
-      nv += sh.rnv[q];
-      fail |= sh.rfail[q] != 0;
-    }
-    nf = nv >> 16;
-    nv &= 0xFFFF;
-    // the row's exact range: the next step's prediction (wave 0), and the scale of a miss
-    const bool redo = __builtin_amdgcn_readfirstlane((int)(nv != 0 && nf > SD_SPARSE && nv > SD_FEW && fail)) != 0;
-    if (redo || (w == 0 && prow)) {
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        pmn = sd_min(pmn, sh.rmn[q]);
-        pmx = sd_max(pmx, sh.rmx[q]);
-      }
-      if (tid == 0 && prow) {  // read again by this thread at the row's next step
-        prow[0] = pmn;
-        prow[1] = pmx;
-      }
-    }
-    // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
-    empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || nf == 0)) != 0;  // uniform
-    if (redo) {
-      scale(pmn, pmx);
-      if (__builtin_amdgcn_readfirstlane((int)(scale_ok && tol < base * 0x1p-20))) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int j = tid + T * q;
-          const double x = psi[j];
-          dtv[sd_swz(j)] = x < INFINITY ? stamp(x, j) : INFINITY;
-        }
-        sd_bar();
-        if constexpr (SLAB) {
-          wave_passes();
-          sd_bar();
-        }
-      }
-      if (tid == 0) sh.cnt[2] += 1;  // rows stamped twice (diagnostics)
-    }
-  } else {
+  {
     double pmn = INFINITY, pmx = -INFINITY;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const double x = v[2 * q + hh];  // (sd_strad: +Inf for a straddling second element, written by its loader)
-        // (SDT_BF: written anyway -- the straddle lane is in this wave and writes after it, in-wave LDS order)
-        if (SDT_BF || !(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) {
-          const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
-          psi[j] = x;
-          if constexpr (P0) dtv[sd_swz(j)] = x;  // (SDT_P0STAMP) raw, stamped by pass 0
-        }
+        // written anyway: the straddle lane is in this wave and writes after it (in-wave LDS order)
+        const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
+        psi[j] = x;
+        dtv[sd_swz(j)] = x;  // raw, stamped by pass 0
         const bool fin = x < INFINITY;
         nv += __popcll(__ballot(fin)) << 16;
         pmn = sd_min(pmn, x);  // +Inf is neutral
@@ -829,7 +512,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       nv += __popcll(__ballot(fin)) << 16;
       if (srank >= 0) {
         psi[srank & 0xFFFF] = x;
-        if constexpr (P0) dtv[sd_swz(srank & 0xFFFF)] = x;
+        dtv[sd_swz(srank & 0xFFFF)] = x;
       }
       pmn = sd_min(pmn, fin ? x : INFINITY);
       pmx = sd_max(pmx, fin ? x : -INFINITY);
@@ -855,30 +538,6 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     SD_STAMP(1);
     // no target in the trust region, or nothing reachable: the row is +Inf and U unwritten (0xFFFF)
     empty = __builtin_amdgcn_readfirstlane((int)(nv == 0 || !(pmn < INFINITY))) != 0;  // uniform
-#if SDT_PRED_PROBE
-    // diagnostic build: would a scale predicted from this row's previous step hold?  The window keeps the previous
-    // step's binade exponent E and centres its range in the widest range E allows; counters [4] misses, [5] hits
-    // only one binade up (grid twice as coarse)
-    if (tid == 0 && prow && pmn < INFINITY) {
-      const double lo_p = prow[0], hi_p = prow[1];
-      if (lo_p <= hi_p) {
-        const double rs_p = (hi_p - lo_p) * inv + (double)Smax;
-        const int E = ilogb(fmin(rs_p, 0x1p31) * (1.0 + 0x1p-20) + 1.0) + 2;
-        auto fits = [&](int e) {
-          const double R = (ldexp(1.0, e - 1) - 1.0) / (1.0 + 0x1p-20) * (1.0 - 0x1p-40), ref = lo_p - 0.5 * (R - rs_p) * beta;
-          return pmn >= ref && (pmx - ref) * inv + (double)Smax < R;
-        };
-        if (!fits(E)) {
-          if (fits(E + 1))
-            sh.cnt[3] += 1;
-          else
-            sh.cnt[2] += 1;
-        }
-      }
-      prow[0] = pmn;
-      prow[1] = pmx;
-    }
-#endif
     scale(pmn, pmx);
   }
   // few finite sources (rows near c' = 0): every target's minimum over them, directly
@@ -890,31 +549,19 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   if (sparse) {
     if (tid == 0) sh.nsp = 0;
     sd_bar();
-    if constexpr (PRED) {  // `v` is dead: the finite sources from Ψ by rank
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const double x = psi[tid + T * q];
-        if (x < INFINITY) {
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        if (v[2 * q + hh] < INFINITY) {
           const int e = atomicAdd(&sh.nsp, 1);
-          sh.spj[e] = tid + T * q;
-          sh.spv[e] = x;
+          sh.spj[e] = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
+          sh.spv[e] = v[2 * q + hh];
         }
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-          if (v[2 * q + hh] < INFINITY) {
-            const int e = atomicAdd(&sh.nsp, 1);
-            sh.spj[e] = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
-            sh.spv[e] = v[2 * q + hh];
-          }
-      if (sd_strad<M>() && srank >= 0 && !(srank & 0x10000) && xs < INFINITY) {
-        const int e = atomicAdd(&sh.nsp, 1);
-        sh.spj[e] = srank & 0xFFFF;
-        sh.spv[e] = xs;
-      }
+    if (sd_strad<M>() && srank >= 0 && !(srank & 0x10000) && xs < INFINITY) {
+      const int e = atomicAdd(&sh.nsp, 1);
+      sh.spj[e] = srank & 0xFFFF;
+      sh.spv[e] = xs;
     }
     sd_bar();
 #pragma unroll
@@ -924,53 +571,19 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     }
   }
   const bool transform = !direct && !empty && !sparse;  // uniform
-  if constexpr (P0) {
-    // (SDT_P0STAMP) no stamp phase: every wave is past its last read of `pin` (barrier 1)
-    h.go();
-    if (!transform) h.load_part(-1);
-  } else if constexpr (!PRED) {
-    if (transform) {
-      // ---- stamp: V_j = trunc_g(base + (Ψ_j - Ψmin)/β) | j --------------------------------------------
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
-          const double x = v[2 * q + hh];
-          if constexpr (SDT_BF)
-            dtv[sd_swz(j)] = stamp_inf(x, j);
-          else if (!(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1)))
-            dtv[sd_swz(j)] = x < INFINITY ? stamp(x, j) : INFINITY;
-        }
-      if (sd_strad<M>() && srank >= 0) {
-        const int js = srank & 0xFFFF;
-        const double x = (srank & 0x10000) ? INFINITY : xs;
-        dtv[sd_swz(js)] = SDT_BF ? stamp_inf(x, js) : x < INFINITY ? stamp(x, js) : INFINITY;
-      }
-      sd_bar();
-      SD_STAMP(2);
-    } else {
-      sd_bar();
-    }
-    // `v` and `pin` are dead from here on: the driver may reuse the latter
-    h.go();
-    if (!transform) h.load_part(-1);  // (SDT_SPREAD) no passes to spread the loads over
-  }
+  // no stamp phase (pass 0 stamps): every wave is past its last read of `pin` (the first barrier)
+  h.go();
   if (transform) {
-    // ---- the M passes (SDT_SLAB: passes 0 .. M-2 already ran per wave, only the last pass is left) ----------------
+    // ---- the M passes: the lines of passes 0 .. M-2 keep the top grid coordinate (rank bits 3(M-1)..), which is the
+    // wave index (the swizzle leaves those bits alone), so a wave reads only what it wrote itself; only the last pass,
+    // which runs along the top coordinate, needs every wave's values
 #pragma unroll
-    for (int m = SLAB ? M - 1 : 0; m < M; ++m) {
+    for (int m = 0; m < M; ++m) {
       pass(m);
-      h.load_part(m);  // (SDT_SPREAD) the next row's loads, a part after each pass
-#if SDT_WAVE_LOCAL
-      // only the last pass, which runs along the top coordinate, needs every wave's values
       if (m + 2 < M)
         sd_wave_sync();
       else if (m + 1 < M)
         sd_bar();
-#else
-      sd_bar();  // last pass: every read of dtv is done before it becomes the output buffer
-#endif
       SD_STAMP(3 + m);
     }
   }
@@ -1282,11 +895,8 @@ __device__ __forceinline__ void sdt_rowB(const ProblemDev &P, const LevelsDev &L
 
 // per-step driver: no pipeline hooks
 struct SdHooksNone {
-  __device__ __forceinline__ void poll() {}
-  __device__ __forceinline__ void wave_done() {}
   __device__ __forceinline__ void early() {}
   __device__ __forceinline__ void go() {}
-  __device__ __forceinline__ void load_part(int) {}
   __device__ __forceinline__ void late_drain() {}
   __device__ __forceinline__ void publish() {}
 };
@@ -1311,18 +921,14 @@ __device__ __forceinline__ void sd_perm_dma(const uint32_t *src, uint32_t *slot)
 // The same copy for the persistent driver, as inline asm: the compiler then does not know these instructions
 // write LDS, and does not make every later LDS atomic wait (vmcnt(0)) for them -- and for the row loads queued
 // behind.  The driver orders them itself: they are issued before the next row's loads and complete under the
-// counted wait at that row's start, and every reader of the slot reads it after a later vmcnt(0) and a barrier
-// (SDT_SLAB: a later counted wait of its own wave).
-// OWN_SLAB (SDT_SLAB): wave w copies only the chunks of its own slab (positions [w·L/NW, (w+1)·L/NW)): the only
-// positions of the slot it reads itself, so no other wave needs to be past its reads of the old contents.
-template <int M, bool OWN_SLAB = false>
+// counted wait at that row's start, and every reader of the slot reads it after a later vmcnt(0) and a barrier.
+template <int M>
 __device__ __forceinline__ void sd_perm_dma_asm(const uint32_t *src, uint32_t *slot) {
-  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, NC = L * 4 / 1024, CPW = NC / NW;
-  static_assert(!OWN_SLAB || CPW * NW == NC, "slab chunks");
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, NC = L * 4 / 1024;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)slot);
 #pragma unroll
-  for (int c = OWN_SLAB ? wave * CPW : wave; OWN_SLAB ? c < (wave + 1) * CPW : c < NC; c += OWN_SLAB ? 1 : NW) {
+  for (int c = wave; c < NC; c += NW) {
     const char *g = (const char *)src + c * 1024 + lane * 16;
     const unsigned m0 = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)c * 1024u);
     unsigned keep;  // M0 is reserved to the compiler: saved and restored around the copy
@@ -1382,7 +988,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
   const int k = (int)blockIdx.y, tid = threadIdx.x;
-  if (tid == 0) sh.cnt[0] = sh.cnt[1] = sh.cnt[2] = 0;
+  if (tid == 0) sh.cnt[0] = sh.cnt[1] = 0;
   // B >= 1: block 0 takes rows 0 and B together, block x the row x (B workgroups, one per CU at B = 256)
   if (blockIdx.x == 0 && P.B >= 1) {
     SdPerm pm;
@@ -1406,7 +1012,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
     for (int q = 0; q < 4; ++q) ein[q] = *reinterpret_cast<const uint2 *>(slot + sd_p2<M>(tid, q));
     sdt_body<M, false>(P, Lv, G, k, cp, i, v, ein, slot, slot + L, Sout_all + (size_t)k * s_stride + (size_t)cp * L,
                        UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(P.B + 1) * L) + (size_t)cp * L, sh,
-                       sds, hooks, P.df, P.uold, nullptr);
+                       sds, hooks, P.df, P.uold);
     if (tid == 0) {
       if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
       if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
@@ -1432,7 +1038,7 @@ __global__ __launch_bounds__(256) void k_sdt_chain(ProblemDev P, PyrGeom G, doub
   const uint32_t *pk = perm_all + (size_t)k * nt * L;
   double *Vk = V + (size_t)k * nt;
   // the head of step i's sphere order (the level at distance 0 from u_old(i), if u_old(i) is on the grid)
-  auto head = [&](int i) { return pk[(size_t)i * L + sd_headpos<M>(G, P.uold[((size_t)k * nt + i) * M + M - 1])]; };
+  auto head = [&](int i) { return pk[(size_t)i * L + kSdHeadPos]; };
   auto j0 = [&](int i) { return (int)(head(i) & 0xFFFFu); };
   // Φ_i[j0(i), 0] exists only where u_old(i) is a level (the head at distance 0); an off-grid u_old(i) leaves
   // budget row 0 empty at step i, and then at every earlier step (+Inf propagates through the additions)
@@ -1489,7 +1095,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_row0(ProblemDev P, Lev
   const bool term = i == nt - 1;
   const int jn = term ? 0
                       : (int)(perm_all[((size_t)k * nt + i + 1) * L +
-                                       sd_headpos<M>(G, P.uold[((size_t)k * nt + i + 1) * M + M - 1])] &
+                                       kSdHeadPos] &
                               0xFFFFu);  // j0(i+1)
   const double vn = term ? 0.0 : V[(size_t)k * nt + i + 1];
   const SdEdge<M> E(P, G.base, k, i);
@@ -1520,23 +1126,22 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_row0(ProblemDev P, Lev
 }
 
 // The persistent driver's hand-off loads, branch-free (a divergent load makes the compiler wait for it before
-// the branches join): per position pair one 16-byte `sc1` load at the row of its first element and one 8-byte
-// `sc1` load at the row of its second where the pair straddles a sphere boundary, both through ONE buffer
-// resource spanning the subproblem's staging buffers and its row-0 array; out-of-range offsets (dropped by the
-// hardware) where a row is below 0 or no second load is needed.  `sd_take` selects once the data is in (at the
+// the branches join): per position pair one 16-byte `sc1` load at the row of its first element; at M = 4 (sd_strad)
+// the second elements of the pairs that straddle a sphere seam come with one straddle load per lane (the wave's seam
+// list), else one 8-byte `sc1` load per pair at the row of its second element where the pair straddles; all through
+// ONE buffer resource spanning the subproblem's staging buffers and its row-0 array; out-of-range offsets (dropped by
+// the hardware) where a row is below 0 or no second load is needed.  `sd_take` selects once the data is in (at the
 // next row's start).
 struct SdRaw {
-  unsigned oa[4], osv;  // (SDT_SPREAD) the offsets of the loads not yet issued
   sd_u32x4 a[4];
   sd_u32x2 b[4];  // (not sd_strad) the second elements of straddling pairs
-  sd_u32x2 sv;    // (sd_strad) this lane's straddle element, at position sp of its slab: rank srank
+  sd_u32x2 sv;    // (sd_strad) this lane's straddle element, at position sp of its wave: rank srank
   int srank;      // -1: no straddle element for this lane; bit 16: its source row is below 0 (+Inf)
   uint2 e[4];     // the sphere-order entries the offsets came from (the row body's `ein`)
   unsigned mask;  // per pair q: bit 3q the first element has no source row, 3q+1 the second, 3q+2 it straddles
 };
-// sl: (sd_strad) the seam list of the slot `pin` (SD_STRAD_N in-slab offsets per slab, 0xFFFF: none)
-// the LDS side of a row's loads: this thread's sphere-order entries of the slot `pin` and (sd_strad) its seam -- read
-// early (SDT_HOIST: right after the row's first barrier) so that the issue does not wait for LDS
+// the LDS side of a row's loads: this thread's sphere-order entries of the slot `pin` and (sd_strad) its seam, from
+// the slot's seam list `sl` (SD_STRAD_N in-wave offsets per wave, 0xFFFF: none)
 struct SdNext {
   uint2 e[4];
   unsigned sp;  // (sd_strad) in-wave offset of this lane's seam (0xFFFF: none)
@@ -1557,11 +1162,9 @@ __device__ __forceinline__ void sd_read_next(SdNext &n, const uint32_t *pin, con
     n.se = pin[sd_seam_pos<M>(wv, (int)(n.sp & (L / NW - 1)))];
   }
 }
-// SPREAD (sd_strad only): compute the offsets, issue nothing (sd_pipe_part issues the loads in three parts)
-template <int M, bool SPREAD = false>
+template <int M>
 __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t rs, const SdNext &n, int cp,
                                               unsigned boff, unsigned r0, const unsigned rowb) {
-  static_assert(!SPREAD || sd_strad<M>(), "spread issue needs the seam lists");
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64;
   const int tid = threadIdx.x;
   uint2 e[4];
@@ -1587,20 +1190,10 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
                       : OOB;
     mask |= ((unsigned)(ra < 0) | (unsigned)(rb < 0) << 1 | (unsigned)(ra != rb) << 2) << (3 * q);
   }
-  if constexpr (SPREAD) {  // sd_strad: issued later, in parts (sd_pipe_part)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w.oa[q] = oa[q];
-  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    if constexpr (!SPREAD) w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa[q], 0, 16);
-    if constexpr (!sd_strad<M>()) {
-#ifndef SDT_EXP_NOB64  // timing experiment only (wrong results): without the straddle loads
-      w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob[q], 0, 16);
-#else
-      w.b[q] = sd_u32x2{0u, 0u};
-#endif
-    }
+    w.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa[q], 0, 16);
+    if constexpr (!sd_strad<M>()) w.b[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, ob[q], 0, 16);
   }
   if constexpr (sd_strad<M>()) {
     const int P = sd_seam_pos<M>(tid >> 6, (int)(sp & (L / NW - 1)));
@@ -1608,29 +1201,13 @@ __device__ __forceinline__ void sd_issue_pipe(SdRaw &w, __amdgpu_buffer_rsrc_t r
     const bool has = sp != 0xFFFFu;
     const unsigned osv =
         !has || rsr < 0 ? OOB : rsr >= 1 ? boff + (unsigned)rsr * rowb + (unsigned)P * 8u : r0 + (unsigned)P * 8u;
-    if constexpr (SPREAD)
-      w.osv = osv;
-    else
-      w.sv = __builtin_amdgcn_raw_buffer_load_b64(rs, osv, 0, 16);
+    w.sv = __builtin_amdgcn_raw_buffer_load_b64(rs, osv, 0, 16);
     w.srank = has ? (int)(se & 0xFFFFu) | (rsr < 0 ? 0x10000 : 0) : -1;
   }
   w.mask = mask;
 }
-// (SDT_SPREAD) part `part` of the loads prepared by sd_issue_pipe<M, true>: 0 and 1 two pairs each, 2 the straddle
-// element; part < 0: all of them
-__device__ __forceinline__ void sd_pipe_part(SdRaw &w, __amdgpu_buffer_rsrc_t rs, int part) {
-  if (part <= 0) {
-    w.a[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, w.oa[0], 0, 16);
-    w.a[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, w.oa[1], 0, 16);
-  }
-  if (part < 0 || part == 1) {
-    w.a[2] = __builtin_amdgcn_raw_buffer_load_b128(rs, w.oa[2], 0, 16);
-    w.a[3] = __builtin_amdgcn_raw_buffer_load_b128(rs, w.oa[3], 0, 16);
-  }
-  if (part < 0 || part == 2) w.sv = __builtin_amdgcn_raw_buffer_load_b64(rs, w.osv, 0, 16);
-}
 // this lane's eight values; (sd_strad) the second element of a straddling pair is +Inf here -- its value comes with
-// the lane that loaded it as a straddle element, and the row body does not store it (the `skip` bits of the mask)
+// the lane that loaded it as a straddle element, which writes it after this lane (in-wave LDS order)
 template <int M>
 __device__ __forceinline__ void sd_take(double (&v)[8], const SdRaw &w) {
 #pragma unroll
@@ -1653,13 +1230,12 @@ __device__ __forceinline__ void sd_take(double (&v)[8], const SdRaw &w) {
 // resident workgroup (nwg / K per subproblem, one per CU); row 0 comes from R0 (k_sdt_row0).  A workgroup works
 // through its items (row, step) in the order step descending, row ascending, and runs one item ahead:
 //   item n:  wait for its Ψ (issued during item n-1) -> reductions, `loaded` published -> stamp, passes
-//            -> MID: drain item n-1's stores, publish item n-1 `done`; wait until item n+1's inputs are
-//               published (RAW) and nobody still reads what item n overwrites (WAR); issue item n+1's Ψ loads
-//               (and the next step's sphere order, LDS-DMA)
-//            -> certified winners, exact scans -> item n's five stores.
+//            -> MID: wait until item n+1's inputs are published (RAW) and nobody still reads what item n overwrites
+//               (WAR); issue item n+1's Ψ loads (and the next step's sphere order, LDS-DMA)
+//            -> certified winners; drain item n-1's stores, publish item n-1 `done`; exact scans -> item n's stores.
 // So the load latency of a row hides behind the second half of the previous row, the store drain behind the
-// first half of the next, and the row hand-off latency becomes pipeline skew: a row runs behind the rows below
-// it, by about half a step per row, which the NB staging buffers absorb (step i lives in buffer i % NB).
+// next row, and the row hand-off latency becomes pipeline skew: a row runs behind the rows below it, which the NB
+// staging buffers absorb (step i lives in buffer i % NB).
 //
 // Flags (relaxed agent-scope atomics, the measured-valid hand-off of MI355X_MICROARCH.md, Valid forms, row 1 of
 // its table: sc1 stores drained by every storing wave, then ONE lane's sc1 flag store behind a workgroup barrier;
@@ -1674,14 +1250,7 @@ __device__ __forceinline__ void sd_take(double (&v)[8], const SdRaw &w) {
 // The pipeline hooks of the persistent driver (the row body calls them, see sdt_body).
 template <int M>
 struct SdPipe {
-  static constexpr int L = 1 << (3 * M), FW = sd_flag_words<M>();
-  static constexpr bool SLAB = SDT_PRED && SDT_SLAB;
-  // SDT_SPREAD: the next row's loads are issued in parts between the passes (load_part), not all at go(), so that
-  // the CU's memory pipeline works on them while the row computes
-  static constexpr bool SPREAD = SDT_SPREAD && !SDT_PRED && sd_strad<M>();
-  // this wave's hand-off flag of row r (per slab under SDT_SLAB, else per row)
-  __device__ __forceinline__ int32_t *dflag(int r) const { return dk + r * FW + (FW > 1 ? (int)(threadIdx.x >> 6) : 0); }
-  __device__ __forceinline__ int32_t *lflag(int r) const { return lk + r * FW + (FW > 1 ? (int)(threadIdx.x >> 6) : 0); }
+  static constexpr int L = 1 << (3 * M);
   // the current row (cp, step i) and the next one (ncp, step ni)
   int cp, i, ncp, ni;
   bool has_next;
@@ -1698,8 +1267,8 @@ struct SdPipe {
   uint16_t *sslot;     // (sd_strad) the two slots' seam lists in LDS
   unsigned char *sds;
   SdtShared<(1 << (3 * M - 3)) / 64> *sh;
-  // carried from row to row: the previous row (its `done` is published at this row's go()), this wave's polls, the
-  // next row's loads in flight
+  // carried from row to row: the previous row (its `done` is published at this row's publish()), this wave's polls,
+  // the next row's loads in flight
   int pcp, pi;
   int32_t *fp;
   int need, val;
@@ -1707,39 +1276,23 @@ struct SdPipe {
   SdNext nx;  // the next row's sphere-order entries and seam (sd_read_next)
 
   // every wave polls its own dependency flags (lanes 0-31 RAW for the next row, 32-63 WAR for this row's stores; a
-  // lane without one polls a flag that always passes -- every lane loads, no branch), checked in go(): SDT_PRED at
-  // the row's start (`loaded` is published in go()), else once every wave has consumed this row's loads (early(),
-  // which publishes `loaded` first)
-  __device__ __forceinline__ void poll() {
-    if constexpr (SDT_PRED) {
-      SD_TL_AT(g0, i, nt, 1);
-      issue_polls();
-    }
-  }
+  // lane without one polls a flag that always passes -- every lane loads, no branch), once every wave has consumed
+  // this row's loads (early()); checked in go()
   __device__ __forceinline__ void early() {
-    if constexpr (!SDT_PRED) {
-      SD_TL_AT(g0, i, nt, 1);
-      issue_polls();
-      // SDT_HOIST: the next row's sphere-order entries and seam, while the row computes (both slots are complete
-      // after this row's first barrier, and neither is rewritten before go() has issued the loads)
-      if constexpr (SDT_HOIST)
-        if (has_next) sd_read_next<M>(nx, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N);
-    }
-  }
-  __device__ __forceinline__ void issue_polls() {
+    SD_TL_AT(g0, i, nt, 1);
     const int tid = threadIdx.x, lane = tid & 63, s = lane < 32 ? lane + 1 : lane - 31;
-    fp = lflag(cp);
+    fp = lk + cp;
     need = INT32_MIN;
     if (lane < 32) {
       const int r = ncp - s;
       if (has_next && s <= 7 * M && r >= 1 && r < lo && nt - 2 - ni > 0) {
-        fp = dflag(r);
+        fp = dk + r;
         need = nt - 2 - ni;  // token(ni + 1)
       }
     } else {
       const int r = cp + s;
       if (s <= 7 * M && r <= B && r >= hi && nt - i - NB > 0) {
-        fp = lflag(r);
+        fp = lk + r;
         need = nt - i - NB;  // token(i + NB - 1)
       }
     }
@@ -1748,28 +1301,12 @@ struct SdPipe {
   // after the row's first barrier (every wave has consumed this row's loads): publish `loaded`; this wave waits until
   // its polls match (re-polling), then issues the next row's loads -- the measured-valid consumer form: the polling
   // wave loads only after its own poll matched
-  // SDT_SLAB, at the row's start: this wave has consumed its loads of this row -- its slab's `loaded` flag
-  __device__ __forceinline__ void consumed() {
-    if constexpr (SLAB)
-      if ((threadIdx.x & 63) == 0) __hip_atomic_store(lflag(cp), nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // SDT_SLAB, mid-row: this wave's stores of the previous row have landed (its `loaded` store and its poll, younger,
-  // may be in flight) -- its slab's `done` flag for the previous row (the measured-valid form, per wave: the storing
-  // wave drains, then one lane of it stores the flag)
-  __device__ __forceinline__ void wave_done() {
-    SD_TL_AT(g0, i, nt, 2);
-    if constexpr (SLAB) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      if ((threadIdx.x & 63) == 0 && pcp >= 0)
-        __hip_atomic_store(dflag(pcp), nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
   __device__ __forceinline__ void go() {
-    if constexpr (!SLAB) SD_TL_AT(g0, i, nt, 2);
+    SD_TL_AT(g0, i, nt, 2);
     const int tid = threadIdx.x;
     // evaluated before the flag store below: the compiler's wait for `val` would otherwise cover that store
     bool ready = __all(val >= need);
-    if (!SLAB && tid == 0) __hip_atomic_store(lflag(cp), nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     while (!ready) {
       if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
@@ -1785,19 +1322,18 @@ struct SdPipe {
     }
     SD_TL_AT(g0, i, nt, 3);
     // the next row's loads; then (LDS-DMA, after them so that they do not wait for it) the next step's sphere order
-    // into the slot of step i+1 (every wave is past its last read of it: the barrier before go(); SDT_SLAB: each wave
-    // copies its own slab only) and the next row's df / u_old; all of it is older than this row's five stores, so the
-    // counted wait at the next row's start covers it
+    // into the slot of step i+1 (every wave is past its last read of it: the barrier before go()) and the next row's
+    // df / u_old; all of it is older than this row's five stores, so the counted wait at the next row's start covers it
     if (has_next) {
       // the reuse flag of the slot: same2[i-1] = (u_old(i-1) == u_old(i+1)), copied with this step's df / u_old (the
       // slot of step i+1 already holds the order of step ni = i-1 then: the order is a function of u_old alone,
       // k_pyr_order, and by induction every slot holds the order of the last step assigned to it)
       const int same = *reinterpret_cast<const volatile int32_t *>(sds + sd_dfuo_offset<M>() +
                                                                    (threadIdx.x >> 6) * sd_dfuo_stride<M>() + 16 * M);
-      if constexpr (!SDT_HOIST || SDT_PRED) sd_read_next<M>(nx, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N);
-      sd_issue_pipe<M, SPREAD>(raw, rs, nx, ncp, (unsigned)((ni + 1) % NB) * bufb, r0b + (unsigned)(ni + 1) * rowb, rowb);
-      if (ni != i && !(SDT_PERM_SKIP && same)) {
-        sd_perm_dma_asm<M, (SDT_PRED && SDT_SLAB)>(pk + (size_t)ni * L, slot + (ni & 1) * L);
+      sd_read_next<M>(nx, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N);
+      sd_issue_pipe<M>(raw, rs, nx, ncp, (unsigned)((ni + 1) % NB) * bufb, r0b + (unsigned)(ni + 1) * rowb, rowb);
+      if (ni != i && !same) {
+        sd_perm_dma_asm<M>(pk + (size_t)ni * L, slot + (ni & 1) * L);
         if constexpr (sd_strad<M>()) sd_strad_dma(sk + (size_t)ni * 8 * SD_STRAD_N, sslot + (ni & 1) * 8 * SD_STRAD_N);
       }
       sd_dfuo_dma<M>(dfa + ((size_t)k * nt + ni) * M, uoa + ((size_t)k * nt + ni) * M,
@@ -1805,20 +1341,15 @@ struct SdPipe {
     }
     SD_TL_AT(g0, i, nt, 4);
   }
-  // (SPREAD) after pass m of the row body (m < 0: the row takes no transform -- all at once)
-  __device__ __forceinline__ void load_part(int m) {
-    if constexpr (SPREAD)
-      if (has_next && m <= 2) sd_pipe_part(raw, rs, m);
-  }
   // late in the row, before the barrier after the winners: this wave's stores of the previous row have landed (they
   // have had the whole row: no wait), so after that barrier the previous row can be published
   __device__ __forceinline__ void late_drain() {
-    if constexpr (!SLAB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     SD_TL_AT(g0, i, nt, 5);
   }
   __device__ __forceinline__ void publish() {
-    if (!SLAB && threadIdx.x == 0 && pcp >= 0)
-      __hip_atomic_store(dflag(pcp), nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0 && pcp >= 0)
+      __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     pcp = cp;
     pi = i;
   }
@@ -1838,8 +1369,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
   const int B = P.B, R = B + 1, nt = P.nt, tid = threadIdx.x;
-  constexpr int FW = sd_flag_words<M>();
-  int32_t *done = flags, *loaded = flags + P.K * R * FW, *err = flags + 2 * P.K * R * FW;
+  int32_t *done = flags, *loaded = flags + P.K * R, *err = flags + 2 * P.K * R;
   const int W = nwg / P.K;  // workgroups per subproblem (the host guarantees 1 <= W <= B)
   const int k = (int)blockIdx.x / W, wl = (int)blockIdx.x - k * W;
   if (k >= P.K) return;
@@ -1847,7 +1377,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   const int lo = 1 + wl * base + max(0, wl - (W - extra)), hi = lo + base + (wl >= W - extra ? 1 : 0);
   uint32_t *slot = reinterpret_cast<uint32_t *>(sds + sd_slot_offset<M>());
   // the row body's outputs (natural order) after a row
-  double *dtv = SDT_WAVE_LOCAL ? reinterpret_cast<double *>(sds + sd_out_offset<M>()) : reinterpret_cast<double *>(sds) + L;
+  double *dtv = reinterpret_cast<double *>(sds + sd_out_offset<M>());
   auto pslot = [&](int step) { return slot + (step & 1) * L; };  // sphere order of `step`
   // this subproblem's region: NB staging buffers of R rows, then row 0 of every step (k_sdt_row0); one buffer
   // resource over all of it (the host checks it is below 4 GiB)
@@ -1855,7 +1385,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   SdPipe<M> h;
   h.lo = lo, h.hi = hi, h.B = B, h.NB = NB, h.nt = nt, h.k = k, h.g0 = k * R + lo;
   h.spin_limit = spin_limit, h.rowb = (unsigned)L * 8u, h.bufb = (unsigned)R * h.rowb, h.r0b = (unsigned)NB * h.bufb;
-  h.dk = done + (size_t)k * R * FW, h.lk = loaded + (size_t)k * R * FW, h.err = err;
+  h.dk = done + (size_t)k * R, h.lk = loaded + (size_t)k * R, h.err = err;
   h.pk = perm_all + (size_t)k * nt * L, h.slot = slot;
   h.rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(h.r0b + (unsigned)nt * h.rowb), 0x00020000);
   h.dfa = df_all, h.uoa = uo_all, h.sm = same2, h.sds = sds, h.sh = &sh;
@@ -1864,11 +1394,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   h.pcp = -1, h.pi = 0;
   if (tid == 0) {
     sh.stop = 0;
-    sh.cnt[0] = sh.cnt[1] = sh.cnt[2] = sh.cnt[3] = 0;
-  }
-  if (tid < SD_PRED_ROWS) {  // no predicted scale yet (the prologue's barrier orders these before every use)
-    sh.pred[tid][0] = INFINITY;
-    sh.pred[tid][1] = -INFINITY;
+    sh.cnt[0] = sh.cnt[1] = 0;
   }
   // prologue: both sphere orders of the first step, df / u_old, and the first row's loads (the terminal row was
   // written by an earlier launch)
@@ -1906,15 +1432,10 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       double v[8];
       sd_take<M>(v, h.raw);
-      h.consumed();  // (SDT_SLAB) this wave's slab of the row's loads is in: its `loaded` flag
-#ifndef SDT_TL_ISSUE
       SD_TL(7);
-#endif
       // one row per workgroup: a sphere-0 source at distance 0 (u_old(i+1) on the level grid: position 0 with b̃ = 0)
       // is this workgroup's own output of the previous row, still in LDS (the loaded copy predates it); an off-grid
-      // u_old(i+1) has b̃ >= 1 everywhere and no such source
-      // (the head of the sphere order is the first position of some wave's lane 0: position 0, or (SDT_SLAB) the first
-      // position of u_old(i+1)'s slab)
+      // u_old(i+1) has b̃ >= 1 everywhere and no such source (position 0 is lane 0 of wave 0)
       if (hi - lo == 1 && h.pcp >= 0 && (tid & 63) == 0 && (h.raw.e[0].x >> 16) == 0)
         v[0] = status == 1 ? INFINITY : dtv[h.raw.e[0].x & 0xFFFFu];
       uint2 ein[4];
@@ -1924,8 +1445,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, ein, pslot(i + 1), pslot(i),
                                  reg + (size_t)(i % NB) * R * L + (size_t)cp * L,
                                  UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L, sh,
-                                 sds, h, df_all, uo_all, cp - lo < SD_PRED_ROWS ? sh.pred[cp - lo] : nullptr,
-                                 h.raw.mask, h.raw.srank, xs);
+                                 sds, h, df_all, uo_all, h.raw.mask, h.raw.srank, xs);
       SD_TL(6);
       stop = sh.stop != 0;  // written before a barrier the row has passed since (every path has one)
     }
@@ -1933,17 +1453,12 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   if (tid == 0) {
     if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
     if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
-    if (sh.cnt[2]) atomicAdd(&counters[4], sh.cnt[2]);
-    if (sh.cnt[3]) atomicAdd(&counters[5], sh.cnt[3]);
   }
   SD_FLUSH();
   SD_TL_FLUSH(h.g0);
 }
 
-
-int sdt_slab_shift(const PyrGeom &G) { return SDT_SLAB ? 3 * (G.M - 1) : 0; }
 bool sdt_seam_lists(const PyrGeom &G) { return G.M == 4 && sd_strad<4>(); }
-int sdt_flag_words(const PyrGeom &G) { return G.M == 4 ? sd_flag_words<4>() : sd_flag_words<3>(); }
 
 bool sdt_supported(const PyrGeom &G) {
   if (G.M != 3 && G.M != 4) return false;

@@ -108,15 +108,55 @@ static double switch_cost(const or_levels *lv, const int64_t *off, int32_t rl, i
 }
 
 /*
+ * One target level rl of recursion step i (1-based, HelpFunctions.jl:49-77): reads the front r (buffer of step
+ * i+1), writes column gidx[rl] of the front w and of U_i.  Different rl touch disjoint columns.
+ */
+static int bellman_target(const or_levels *lv, const int64_t *off, const int64_t *gidx, const double *df,
+                          const double *u_old, int64_t i, int64_t B, int p_kind, int64_t p_int, double beta,
+                          const double *wtab, int64_t wtab_len, double dt, const double *r, double *w, int32_t *Ui,
+                          int64_t rl) {
+    const int64_t M = lv->M, L = lv->L, R = B + 1;
+    const int32_t *l = lv->tuples + rl * M;
+    double t1 = 0.0;
+    int64_t bt = 0;
+    int rc;
+    for (int64_t m = 0; m < M; ++m) {
+        int64_t numl = lv->values[off[m] + l[m] - 1];
+        t1 += dt * df[m + M * (i - 1)] * (double)numl;
+        int64_t e;
+        if ((rc = to_int_exact((double)numl - u_old[m + M * (i - 1)], &e)) != OR_OK) return rc;
+        bt += e;
+    }
+    for (int64_t rj = 0; rj < L; ++rj) {
+        int err = OR_OK;
+        double t2 = t1 + switch_cost(lv, off, (int32_t)rl, (int32_t)rj, p_kind, p_int, beta, wtab, wtab_len, &err);
+        if (err != OR_OK) return err;
+        const double *rcol = r + R * gidx[rj];
+        double *wcol = w + R * gidx[rl];
+        int32_t *ucol = Ui + R * gidx[rl];
+        for (int64_t b = 0; b <= B - bt; ++b) {
+            double val = t2 + rcol[b];
+            if (wcol[b + bt] > val) { /* strict: first j in iterator order wins ties */
+                ucol[b + bt] = (int32_t)rj;
+                wcol[b + bt] = val;
+            }
+        }
+    }
+    return OR_OK;
+}
+
+/*
  * bellman_TRM!(∇f, u_old, B, β, p, Δt, nu, U, Φ, iterator)        HelpFunctions.jl:20-83
  * phi : (B+1) x Lgrid x 2 column-major (c fastest), exactly the reference's Φ
  * U   : (B+1) x Lgrid x (n-1) column-major; stores the iterator RANK of j (the reference stores
  *       the tuple j itself; rank <-> tuple is the bijection given by `tuples`).  Cells the
  *       reference never writes keep their previous contents (callers pre-fill with -1).
+ * threads > 1: the target levels of each step split over OpenMP threads (every target writes only its own columns,
+ * so the result is bit-identical to threads = 1; used to generate the larger golden fixtures).
  */
-int oracle_bellman(const or_levels *lv, const double *df, const double *u_old, int64_t n, int64_t B,
-                   int p_kind, int64_t p_int, double beta, const double *wtab, int64_t wtab_len,
-                   double dt, double *phi, int32_t *U) {
+static int bellman_impl(const or_levels *lv, const double *df, const double *u_old, int64_t n, int64_t B,
+                        int p_kind, int64_t p_int, double beta, const double *wtab, int64_t wtab_len,
+                        double dt, double *phi, int32_t *U, int threads) {
     const int64_t M = lv->M, L = lv->L, Lg = grid_size(lv), R = B + 1;
     if (n < 1 || B < 0 || M < 1 || L < 1) return OR_EINVAL;
     int64_t *off = (int64_t *)malloc(sizeof(int64_t) * M);
@@ -151,39 +191,38 @@ int oracle_bellman(const or_levels *lv, const double *df, const double *u_old, i
         const double *r = phi + R * Lg * (i % 2);  /* Φ[..., i%2+1]     */
         int32_t *Ui = U + R * Lg * (i - 1);
         for (int64_t k = 0; k < R * Lg; ++k) w[k] = INFINITY;
-        for (int64_t rl = 0; rl < L; ++rl) {
-            const int32_t *l = lv->tuples + rl * M;
-            double t1 = 0.0;
-            int64_t bt = 0;
-            for (int64_t m = 0; m < M; ++m) {
-                int64_t numl = lv->values[off[m] + l[m] - 1];
-                t1 += dt * df[m + M * (i - 1)] * (double)numl;
-                int64_t e;
-                if ((rc = to_int_exact((double)numl - u_old[m + M * (i - 1)], &e)) != OR_OK) goto done;
-                bt += e;
+        if (threads <= 1) {
+            for (int64_t rl = 0; rl < L; ++rl)
+                if ((rc = bellman_target(lv, off, gidx, df, u_old, i, B, p_kind, p_int, beta, wtab, wtab_len, dt, r,
+                                         w, Ui, rl)) != OR_OK)
+                    goto done;
+        } else {
+            int bad = OR_OK; /* error codes are negative: the smallest one seen */
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 16) reduction(min : bad)
+            for (int64_t rl = 0; rl < L; ++rl) {
+                const int e = bellman_target(lv, off, gidx, df, u_old, i, B, p_kind, p_int, beta, wtab, wtab_len, dt,
+                                             r, w, Ui, rl);
+                if (e < bad) bad = e;
             }
-            for (int64_t rj = 0; rj < L; ++rj) {
-                int err = OR_OK;
-                double t2 = t1 + switch_cost(lv, off, (int32_t)rl, (int32_t)rj, p_kind, p_int, beta, wtab,
-                                             wtab_len, &err);
-                if (err != OR_OK) { rc = err; goto done; }
-                const double *rcol = r + R * gidx[rj];
-                double *wcol = w + R * gidx[rl];
-                int32_t *ucol = Ui + R * gidx[rl];
-                for (int64_t b = 0; b <= B - bt; ++b) {
-                    double val = t2 + rcol[b];
-                    if (wcol[b + bt] > val) { /* strict: first j in iterator order wins ties */
-                        ucol[b + bt] = (int32_t)rj;
-                        wcol[b + bt] = val;
-                    }
-                }
-            }
+            if ((rc = bad) != OR_OK) goto done;
         }
     }
 done:
     free(off);
     free(gidx);
     return rc;
+}
+
+int oracle_bellman(const or_levels *lv, const double *df, const double *u_old, int64_t n, int64_t B,
+                   int p_kind, int64_t p_int, double beta, const double *wtab, int64_t wtab_len,
+                   double dt, double *phi, int32_t *U) {
+    return bellman_impl(lv, df, u_old, n, B, p_kind, p_int, beta, wtab, wtab_len, dt, phi, U, 1);
+}
+
+int oracle_bellman_mt(const or_levels *lv, const double *df, const double *u_old, int64_t n, int64_t B,
+                      int p_kind, int64_t p_int, double beta, const double *wtab, int64_t wtab_len,
+                      double dt, double *phi, int32_t *U, int threads) {
+    return bellman_impl(lv, df, u_old, n, B, p_kind, p_int, beta, wtab, wtab_len, dt, phi, U, threads);
 }
 
 /* Julia findmin/argmin order on Float64: NaN first (treated smallest), then isless (-0.0 < +0.0) */

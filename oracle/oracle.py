@@ -111,6 +111,8 @@ class OracleC:
                                      ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int64,
                                      ctypes.c_double, ctypes.c_void_p, ctypes.c_int64, ctypes.c_double,
                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_bellman_mt.restype = ctypes.c_int
+        L.oracle_bellman_mt.argtypes = L.oracle_bellman.argtypes + [ctypes.c_int]
         L.oracle_backtrack.restype = ctypes.c_int
         L.oracle_backtrack.argtypes = [ctypes.POINTER(_OrLevels), ctypes.c_void_p, ctypes.c_int64,
                                        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
@@ -132,8 +134,9 @@ class OracleC:
         s = _OrLevels(lv.M, lv.counts.ctypes.data, lv.values.ctypes.data, lv.L, lv.tuples.ctypes.data)
         return s
 
-    def bellman(self, lv, df, u_old, B, p_kind, beta, dt, p_int=1, wtab=None):
-        """Returns (phi, U) in the reference layouts: phi (B+1, Lgrid, 2), U (B+1, Lgrid, n-1) (Fortran)."""
+    def bellman(self, lv, df, u_old, B, p_kind, beta, dt, p_int=1, wtab=None, threads=1):
+        """Returns (phi, U) in the reference layouts: phi (B+1, Lgrid, 2), U (B+1, Lgrid, n-1) (Fortran).
+        threads > 1: the target levels of each step split over OpenMP threads (bit-identical result)."""
         df = np.asfortranarray(df, dtype=np.float64)
         u_old = np.asfortranarray(u_old, dtype=np.float64)
         M, n = df.shape
@@ -141,9 +144,9 @@ class OracleC:
         phi = np.zeros((R, lv.Lgrid, 2), dtype=np.float64, order="F")
         U = np.full((R, lv.Lgrid, max(n - 1, 0)), -1, dtype=np.int32, order="F")
         wt = None if wtab is None else np.ascontiguousarray(wtab, dtype=np.float64)
-        rc = self.lib.oracle_bellman(ctypes.byref(self._lv(lv)), _ptr(df), _ptr(u_old), n, B, p_kind,
-                                     p_int, beta, _ptr(wt), 0 if wt is None else wt.size, dt, _ptr(phi),
-                                     _ptr(U))
+        args = (ctypes.byref(self._lv(lv)), _ptr(df), _ptr(u_old), n, B, p_kind, p_int, beta, _ptr(wt),
+                0 if wt is None else wt.size, dt, _ptr(phi), _ptr(U))
+        rc = self.lib.oracle_bellman_mt(*args, int(threads)) if threads > 1 else self.lib.oracle_bellman(*args)
         if rc != 0:
             raise OracleError(rc)
         return phi, U

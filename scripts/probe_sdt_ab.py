@@ -1,7 +1,8 @@
 """A/B timing of k_sdt_run (C4 inputs at full L and B, truncated nt) across library builds, each in its own process.
 Prints per library: µs per DP step (HIP events, best of REPS calls) and a digest of u / Φ* at three budgets and of
 the argmin tables of a few steps, which must agree across builds.
-Usage: python scripts/probe_sdt_ab.py NT LIB [LIB ...]   (SDT_NB=n: staging buffers)"""
+Usage: python scripts/probe_sdt_ab.py NT LIB [LIB ...]   (SDT_NB=n: staging buffers; LIB#0 / LIB#1: MIOC_OPT_SDT_PAIR
+off / on for that run, e.g. lib/libmioc.so#0 times the one-workgroup-per-row k_sdt_run)"""
 import hashlib, json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")
@@ -11,7 +12,8 @@ REPS = 3
 NB = int(os.environ.get("SDT_NB", "0"))  # staging buffers (MIOC_OPT_SDT_BUFFERS), 0: the library default
 
 
-def one(nt, lib):
+def one(nt, spec):
+    lib, _, pair = spec.partition("#")
     os.environ["MIOC_LIB"] = lib
     sys.path.insert(0, PKG); sys.path.insert(0, ROOT)
     import numpy as np
@@ -25,6 +27,8 @@ def one(nt, lib):
         ctx.set_option(native.MIOC_OPT_TIMING, 1); ctx.set_option(native.MIOC_OPT_PERSIST, 1)
         if NB:
             ctx.set_option(native.MIOC_OPT_SDT_BUFFERS, NB)
+        if pair:
+            ctx.set_option(native.MIOC_OPT_SDT_PAIR, int(pair))
         best = None
         for _ in range(REPS):
             ctx.reset_stats()
@@ -38,7 +42,7 @@ def one(nt, lib):
             h.update(np.ascontiguousarray(u).tobytes()); h.update(np.float64(phi).tobytes())
         for i in (0, 1, nt // 2, nt - 3):
             h.update(np.ascontiguousarray(ctx.argmin_table(i), dtype=np.int32).tobytes())
-        print(json.dumps({"lib": os.path.basename(lib), "nt": nt, "kernel": name, "ms": round(best, 3),
+        print(json.dumps({"lib": os.path.basename(spec), "nt": nt, "kernel": name, "ms": round(best, 3),
                           "us_per_step": round(1e3 * best / (nt - 1), 3), "diag": list(ctx.diagnostics()[:7]),
                           "digest": h.hexdigest()[:16]}), flush=True)
 

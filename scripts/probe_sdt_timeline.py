@@ -1,10 +1,10 @@
 """Timeline of the pipelined persistent separable-transform kernel (diagnostic build libmioc_stamps_tl.so, `make
 stamps_tl`): for every row and the 64 steps from nt/2 down, s_memrealtime (100 MHz) at 8 points of the row body:
-0 start, 7 loads taken, 1 dependency polls issued (after the first barrier; SDT_PRED builds: after the stamps), 2 go()
+0 start, 7 loads taken, 1 dependency polls issued (after the first barrier), 2 go()
 (the first barrier passed), 3 polls matched, 4 next row's loads and copies issued, 5 previous row's stores drained (late,
 before the winners' barrier), 6 stores issued.  Prints the phase durations, the step period and the pipeline skew between neighbouring rows.
 Usage: python scripts/probe_sdt_timeline.py [nt] [NB]  [save.npy] [--lib another timeline build]
-(SDT_PRED builds: point 1 is the row's poll issue, right after its loads are taken.)"""
+"""
 import ctypes
 import os
 import sys

@@ -1,6 +1,6 @@
-"""GPU parity of the C4 (BASELINE roofline) shape on the code the bench times: k_sdt_run<4> (the persistent
-separable transform, 8^4 = 4096 levels, B = 256, p = 1), against the CPU oracle -- never against another device
-algorithm.
+"""GPU parity of the C4 (BASELINE roofline) shape on the code the bench times: k_sdt_pair (the persistent separable
+transform with two workgroups per budget row, 8^4 = 4096 levels, B = 256, p = 1) -- and the one-workgroup-per-row
+k_sdt_run<4> and the per-step k_sdt_step -- against the CPU oracle, never against another device algorithm.
 
   * a committed oracle fixture at the full L = 4096, B = 256 with nt = 64 (63 recursion steps: every rotation of
     the four staging buffers and row B's two-step lag, many times): sha256 of every step's argmin table U in the
@@ -24,10 +24,12 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _ctx(lt, beta, algo, persist=1):
+def _ctx(lt, beta, algo, persist=1, pair=1):
     ctx = native.Context(0)
     ctx.set_levels(lt)
     ctx.set_cost(1, beta)
+    ctx.set_option(native.MIOC_OPT_SDT_PAIR, pair)
+    ctx.set_option(native.MIOC_OPT_TIMING, 1)
     ctx.set_option(native.MIOC_OPT_ALGO, algo)
     ctx.set_option(native.MIOC_OPT_PERSIST, persist)
     return ctx
@@ -37,19 +39,22 @@ def _hash(t):
     return np.frombuffer(hashlib.sha256(np.ascontiguousarray(t, dtype=np.int32).tobytes()).digest(), dtype=np.uint8)
 
 
-@pytest.mark.parametrize("variant", ["persistent", "steps"])
+@pytest.mark.parametrize("variant", ["pair", "persistent", "steps"])
 def test_c4_nt64_fixture(variant):
     """The separable transform writes U exactly like the reference: the rank where the reference writes it, and
-    nothing (-1) elsewhere, so every step's table hashes to the oracle's."""
+    nothing (-1) elsewhere, so every step's table hashes to the oracle's.  pair: k_sdt_pair (the bench's kernel),
+    persistent: k_sdt_run, steps: one k_sdt_step launch per step."""
     z = np.load(os.path.join(HERE, "golden", "hashed", "c4_4096lv_p1_nt64_uhash.npz"), allow_pickle=False)
     cfg = CONFIGS["C4"]
     lt = cfg.levels()
     algo = native.MIOC_ALGO_SEPARABLE
-    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=int(variant == "persistent"))
+    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=int(variant != "steps"), pair=int(variant == "pair"))
     df, uo = z["df"], z["u_old"]
     B = int(z["B"][0])
     ctx.bellman(df, uo, B, float(z["dt"][0]))
     assert ctx.last_algo() == algo
+    ctx.synchronize()
+    assert ctx.kernel_stats(0)[2] == {"pair": "k_sdt_pair", "persistent": "k_sdt_run", "steps": "k_sdt_step"}[variant]
     nt = df.shape[1]
     bad = [i for i in range(nt - 1) if not np.array_equal(_hash(ctx.argmin_table(i)), z["u_hash"][i])]
     assert not bad, f"{variant}: U differs from the oracle at steps {bad[:10]}"
@@ -60,9 +65,9 @@ def test_c4_nt64_fixture(variant):
     ctx.close()
 
 
-@pytest.mark.parametrize("persist", [1, 0], ids=["persistent", "steps"])
+@pytest.mark.parametrize("variant", ["pair", "persistent", "steps"])
 @pytest.mark.parametrize("mode", ["zero", "integer", "steep"])
-def test_c4_tie_heavy_vs_oracle(oracle_c, mode, persist):
+def test_c4_tie_heavy_vs_oracle(oracle_c, mode, variant):
     """4096 levels, B = 256: every target of a zero-gradient row ties (the listed-target buffer overflows and the
     scan sweeps every rank); integer gradients tie often; 'steep' puts rows outside the transform's binade."""
     cfg = CONFIGS["C4"]
@@ -79,7 +84,7 @@ def test_c4_tie_heavy_vs_oracle(oracle_c, mode, persist):
         df = df * 1e3  # value spread ~1e12 beta: outside the transform's binade (2^36 units)
     beta = 1e-13 if mode == "steep" else cfg.beta
     phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_ONE, beta, cfg.dt)
-    ctx = _ctx(lt, beta, native.MIOC_ALGO_SEPARABLE, persist)
+    ctx = _ctx(lt, beta, native.MIOC_ALGO_SEPARABLE, int(variant != "steps"), int(variant == "pair"))
     ctx.bellman(df, uo, cfg.B, cfg.dt)
     diag = ctx.diagnostics()
     for i in range(n - 1):
@@ -136,15 +141,16 @@ def test_c4_chunked_rows_vs_oracle(oracle_c):
     ctx.close()
 
 
-def test_c4_nt64_fixture_wait_timeout_redoes_dp():
-    """The headline kernel's timeout path: with a spin limit of one poll, the persistent k_sdt_run gives up at its
-    first dependency wait that is not already satisfied, every workgroup leaves, and the host redoes the DP with
-    per-step launches (check_run, counted in diagnostics [6]) before anything reads the tables -- so every step's U
-    hash, u and Φ* still equal the oracle fixture."""
+@pytest.mark.parametrize("pair", [1, 0], ids=["pair", "persistent"])
+def test_c4_nt64_fixture_wait_timeout_redoes_dp(pair):
+    """The headline kernels' timeout path: with a spin limit of one poll, the persistent k_sdt_pair / k_sdt_run gives
+    up at its first dependency wait that is not already satisfied, every workgroup leaves, and the host redoes the DP
+    with per-step launches (check_run, counted in diagnostics [6]) before anything reads the tables -- so every
+    step's U hash, u and Φ* still equal the oracle fixture."""
     z = np.load(os.path.join(HERE, "golden", "hashed", "c4_4096lv_p1_nt64_uhash.npz"), allow_pickle=False)
     lt = CONFIGS["C4"].levels()
     algo = native.MIOC_ALGO_SEPARABLE
-    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=1)
+    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=1, pair=pair)
     ctx.set_option(native.MIOC_OPT_SPIN_LIMIT, 1)
     df, uo = z["df"], z["u_old"]
     ctx.bellman(df, uo, int(z["B"][0]), float(z["dt"][0]))

@@ -237,6 +237,59 @@ def test_backtrack_budgets_device_vs_single():
         ctx.close()
 
 
+@pytest.mark.parametrize("algo", ["separable", "pyramid", "pinf"])
+def test_backtrack_budgets_device_start_kernels(algo):
+    """The per-restart budget check of the other start kernels (k_stage_argmin0 for the staging-layout DPs,
+    k_pinf_start for the p=Inf collapse): a budget outside [0, B] gives that subproblem MIOC_ESTATE and a NaN u row,
+    the others equal a separate backtrack at their budget (multi-trust.jl:108-110 per restart)."""
+    import torch
+    rng = np.random.default_rng({"separable": 31, "pyramid": 32, "pinf": 33}[algo])
+    if algo == "pinf":
+        cfg = CONFIGS["C2"]
+        lt = cfg.levels()
+        K, nt, B, beta, dt, pk = 5, 96, 40, cfg.beta, cfg.dt, P_INF
+        subs = [make_inputs(cfg, k=k, nt=nt)[1:] for k in range(K)]
+        aid = native.MIOC_ALGO_PINF
+    else:
+        lv = Levels.product([list(range(8))] * 3)
+        lt = LevelTable(lv.nu, [tuple(t) for t in lv.tuples])
+        K, nt, B, beta, dt, pk = 5, 24, 20, 1e-3, 2.0 ** -10, P_ONE
+        subs = []
+        for _ in range(K):
+            df = rng.standard_normal((3, nt))
+            uo = np.array([lv.nuval[rng.integers(lv.L)] for _ in range(nt)], dtype=np.float64).T.copy()
+            subs.append((df, uo))
+        aid = native.MIOC_ALGO_SEPARABLE if algo == "separable" else native.MIOC_ALGO_PYRAMID
+    budgets = [B, -1, B + 1, 5, 0]
+    ddf = torch.tensor(np.ascontiguousarray(np.stack([d.T for d, _ in subs])), dtype=torch.float64, device="cuda")
+    duo = torch.tensor(np.ascontiguousarray(np.stack([u.T for _, u in subs])), dtype=torch.float64, device="cuda")
+    ctx = _ctx(lt, pk, beta, aid)
+    torch.cuda.synchronize()
+    ctx.bellman_batch_tensors(ddf, duo, B, dt)
+    assert ctx.last_algo() == aid
+    du = torch.empty_like(ddf)
+    dphi = torch.empty(K, dtype=torch.float64, device="cuda")
+    dst = torch.empty(K, dtype=torch.int32, device="cuda")
+    ctx.backtrack_batch_budgets_tensors(torch.tensor(budgets, dtype=torch.int32, device="cuda"), du, dphi, dst)
+    ctx.synchronize()
+    ub, st = du.cpu().numpy(), dst.cpu().numpy()
+    for k, Bp in enumerate(budgets):
+        if not 0 <= Bp <= B:
+            assert st[k] == native.MIOC_ESTATE and np.all(np.isnan(ub[k])), (algo, k, Bp)
+            continue
+        single = _ctx(lt, pk, beta, aid)
+        single.bellman(*subs[k], B, dt)
+        try:
+            u, ps, _ = single.backtrack(Bp)
+        except native.MiocNativeError:  # no finite value within this budget: the batch row says so too
+            assert st[k] != 0, (algo, k, Bp)
+            single.close()
+            continue
+        assert st[k] == 0 and np.array_equal(ub[k].T, u) and dphi[k].item() == ps, (algo, k, Bp)
+        single.close()
+    ctx.close()
+
+
 def _path_objective(lt, df, u, dt, beta, p_kind):
     """Φ* recomputed along a control in the reference's rounding order (HelpFunctions.jl:52-71)."""
     M, n = u.shape

@@ -153,3 +153,38 @@ def test_segmented_walk_state_dependent_rows_vs_oracle(oracle_c):
         assert np.array_equal(u, ou) and ps == ops, f"walk={walk}"
         assert ctx.diagnostics()[9] == 1
         ctx.close()
+
+
+def _c4_pinf_fixture():
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "hashed", "c4_4096lv_pinf_nt200.npz")
+    return np.load(path, allow_pickle=False)
+
+
+@pytest.mark.parametrize("walk", [1, -1], ids=["segmented_walk", "serial_walk"])
+@pytest.mark.parametrize("spin", [0, 1], ids=["run", "timeout_redo"])
+def test_c4_pinf_nt200_fixture(walk, spin):
+    """C4 at p = Inf (4096 levels, B = 256) over 199 recursion steps against the C oracle's fixture
+    (tests/golden/make_c4_pinf_fixture.py): the row-segment recursion k_pinf_recur_mc across more than three of its
+    64-step hand-off chunks and a wrap of its 128-slot ring, then u and Φ* at five budgets.  spin = 1: a spin limit of
+    one poll abandons the segmented launch at its first unmet wait, and the host redoes the DP in one workgroup
+    (check_run, diagnostics [6]) before anything reads the tables -- the same u and Φ*."""
+    z = _c4_pinf_fixture()
+    lt = CONFIGS["C4"].levels()
+    ctx = _ctx(lt, float(z["beta"][0]), walk)
+    ctx.set_option(native.MIOC_OPT_TIMING, 1)
+    if spin:
+        ctx.set_option(native.MIOC_OPT_SPIN_LIMIT, 1)
+    ctx.bellman(z["df"], z["u_old"], int(z["B"][0]), float(z["dt"][0]))
+    ctx.synchronize()
+    assert ctx.kernel_stats(0)[2] == "k_pinf_recur_mc"  # the row-segment kernel took this DP
+    for q, Bp in enumerate(z["budgets"]):
+        u, ps, _ = ctx.backtrack(int(Bp))
+        assert np.array_equal(u, z["u"][q]), f"B'={Bp}"
+        assert ps == z["phi_star"][q], f"B'={Bp}: {ps!r} vs {z['phi_star'][q]!r}"
+    diag = ctx.diagnostics()
+    if spin:
+        assert diag[6] >= 1, diag  # the segmented launch was abandoned and redone
+    else:
+        assert diag[6] == 0, diag
+    ctx.close()
