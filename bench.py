@@ -74,6 +74,9 @@ def parse(argv=None):
                          "command: adds counter-backed VALU figures to each line's roofline_valu")
     ap.add_argument("--pinf-batch-config", default="C2",
                     help="the p=Inf batch line's config (the reference's main() runs C1-C3 at p=Inf; 'none' to skip)")
+    ap.add_argument("--single-configs", default="C2,C3",
+                    help="one-subproblem lines (BASELINE configs 2 and 3, the reference's main() presets "
+                         "multi-trust.jl:185-190) with their roofline and CPU baseline ('none' to skip)")
     ap.add_argument("--heat-restarts", type=int, default=4096,
                     help="PDE heat gradient line (SURVEY §8 f4): restarts per rank per step (0 to skip)")
     ap.add_argument("--heat-n", type=int, default=17, help="heat line: P1 grid side (N = n^2 dofs)")
@@ -327,10 +330,10 @@ def roofline_of(res):
         ub = 1 if L <= 256 else 2
         bytes_per_launch = K * (B + 1) * L * (8 + 8 + ub)
         ops = 2.0 * K * ncand_step  # one v_add_f64 + one v_min_f64 per candidate
-    elif name in ("k_sdt_step", "k_sdt_run"):
+    elif name in ("k_sdt_step", "k_sdt_run", "k_sdt_pair"):
         # the same algorithmic traffic as the reference DP step: front in + front out + compact U, per step;
-        # k_sdt_run is one persistent launch over all nt - 1 steps
-        steps = (nt - 1) if name == "k_sdt_run" else 1
+        # k_sdt_run / k_sdt_pair are one persistent launch over all nt - 1 steps
+        steps = (nt - 1) if name != "k_sdt_step" else 1
         bytes_per_launch = steps * K * (B + 1) * L * (8 + 8 + 2)
         # per pass and 8-point line: 14 merges (7 forward, 7 backward), each add + min + sub + cmp (4 FP64 ops) and the
         # near-tie count's v_addc
@@ -636,6 +639,31 @@ def heat_cpu_baseline(hp):
                       f"host: {model}, {aff} CPUs in the affinity mask"}
 
 
+def summary(out):
+    """A compact view of every line (value, ms per step, roofline fraction, CPU baseline), the JSON line's last key."""
+    def brief(d):
+        r = {"value": d.get("value"), "unit": d.get("unit"), "ms_per_step": d.get("ms_per_step")}
+        if isinstance(d.get("roofline"), dict):
+            r["frac"] = d["roofline"].get("frac")
+            r["bound"] = d["roofline"].get("bound")
+            r["kernel"] = d["roofline"].get("kernel")
+        if isinstance(d.get("cpu_baseline"), dict):
+            r["cpu_value"] = d["cpu_baseline"].get("value")
+        if "projected_8gpu_speedup" in d:
+            r["projected_8gpu_speedup"] = d["projected_8gpu_speedup"]
+        return r
+    sm = {"C4": brief(out)}
+    for key, name in (("variant_p_inf", "C4_p_inf"), ("batch", "batch"), ("batch_strong", "batch_strong"),
+                      ("batch_shard8", "batch_shard8"), ("batch_p2", "batch_p2"), ("batch_p_inf", "batch_p_inf"),
+                      ("batch_heat", "heat")):
+        if key in out:
+            sm[name] = brief(out[key])
+    for key in out:
+        if key.startswith("single_"):
+            sm[key] = brief(out[key])
+    return sm
+
+
 def workload(res):
     lv = res["levels"]
     counts = "x".join(str(len(v)) for v in lv.nu)
@@ -705,6 +733,8 @@ def main():
         if args.solver == "native" and len(r2.get("diag", [])) > 9:  # mioc_diagnostics[9]
             variant["walk"] = "serial" if r2["diag"][9] < 0 else "segmented"
             variant["walk_serial_fallbacks"] = max(0, int(r2["diag"][9]))
+        if rank == 0 and world == 1 and not args.no_cpu_baseline and args.solver == "native":
+            variant["cpu_baseline"] = cpu_baseline(args.config, "inf", args.cpu_steps)
     def batch_line(cfg_name, total=None, p_over=None):
         r3 = run(args, cfg_name, args.batch_size, p_over, None, rank, world, device, dist, torch,
                  max(args.steps, 3), args.warmup, total=total)
@@ -757,6 +787,16 @@ def main():
                             "integration/MIOC.jl): the reference's heat configuration (multi-trust.jl:193-195)")
     if args.pinf_batch_config not in ("", "none") and args.nt is None:
         batch_pinf = batch_line(args.pinf_batch_config)
+    singles = {}
+    if args.single_configs not in ("", "none") and args.nt is None:
+        # one subproblem per GPU per step of the reference's own main() presets (doubletank, vanderpol at p = Inf)
+        for cname in args.single_configs.split(","):
+            saved = args.batch_size
+            args.batch_size = 1
+            try:
+                singles[cname] = batch_line(cname)
+            finally:
+                args.batch_size = saved
     if rank == 0:
         value = res["G"] * args.steps / res["elapsed"]
         out = {
@@ -799,8 +839,11 @@ def main():
             out["batch_p_inf"] = batch_pinf
         if heat:
             out["batch_heat"] = heat
+        for cname, line in singles.items():
+            out[f"single_{cname}"] = line
         if not args.no_cpu_baseline and world == 1 and args.nt is None and args.solver == "native":
             out["cpu_baseline"] = cpu_baseline(args.config, args.p, args.cpu_steps)
+        out["summary"] = summary(out)  # last key: every sub-line in the tail of the output
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -313,11 +313,13 @@ __device__ __forceinline__ void s2_scan(const uint16_t *list, int nl, const doub
 
 #if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
 // timeline (diagnostic build): per workgroup and for 32 of its items from the middle of the run, s_memrealtime
-// (100 MHz) at 8 points of an item
+// (100 MHz) at 8 points of an item; kept in LDS during the launch (a global store would join the vector-memory queue
+// the item's counted waits rely on) and copied out at the end
 __device__ unsigned long long g_sdt2_tl[1024][32][8];
+__shared__ unsigned long long s2_tl_lds[32][8];
 #define S2_TL(k)                                                                                                \
   do {                                                                                                          \
-    if (threadIdx.x == 0 && tl_on) tl[k] = __builtin_amdgcn_s_memrealtime();                                  \
+    if (threadIdx.x == 0 && tl_on) s2_tl_lds[item - tl_item0][k] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
 #else
 #define S2_TL(k) \
@@ -370,7 +372,6 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
   const int lb[M] = {G.base[0], G.base[1], G.base[2], G.base[3]};
   const double beta = Lv.beta, inv = Lv.inv_beta;
 #if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
-  unsigned long long tl[8];
   const int tl_item0 = (nt / 2 - par) / 2;  // items from the middle of the run
   bool tl_on = false;
 #endif
@@ -671,9 +672,13 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     s2_dfuo_dma(dfk, uok, pstep(i - 2), nt, sds);
     S2_TL(4);
     // ---- the transform -------------------------------------------------------------------------------------------
-    double o[16];  // the last pass's values at this lane's lines (targets (tid + 256·ln) | x << 9)
     auto pos3 = [&](int e) { return sd_swz((sd_tid() + S2_T * (e >> 3)) | ((e & 7) << 9)); };
+    // an opaque zero: the targets' T1 terms a_3·ν_3 are recomputed per target (two VALU) instead of being hoisted into
+    // registers that would be spilled
+    int zop = 0;
+    asm volatile("" : "+v"(zop));
     if (transform) {
+      double o[16];
       auto pass = [&](int m) {
         int pos[16];
 #pragma unroll
@@ -711,13 +716,8 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       sd_wave_sync();
       pass(2);
       sd_bar();  // (2) the last pass runs along x3: every wave's values
-      pass(3);
     }
     // (direct / sparse rows: no barrier here, they read Ψ by rank only after barrier (3))
-    S2Ent eOn, eAnn;  // the orders of steps i-2 (the next item's outputs) and i-3 (A of the item after it): loaded
-                      // here, a while before the loop's back edge moves them into place (no wait there)
-    s2_ent_issue(eOn, pk + (size_t)pstep(i - 2) * S2_PACK, sk + (size_t)pstep(i - 2) * (S2_NW * S2_SEAMS));
-    s2_ent_issue(eAnn, pk + (size_t)pstep(i - 3) * S2_PACK, sk + (size_t)pstep(i - 3) * (S2_NW * S2_SEAMS));
     S2_TL(5);
     // ---- targets: R(l, j*) for a certified winner, the others listed for the exact scan ---------------------------
     // (outputs at the swizzled positions the last pass read: each lane writes only its own)
@@ -729,21 +729,29 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       reinterpret_cast<ulonglong2 *>(uu)[2 * tid + 1] = make_ulonglong2(~0ull, ~0ull);
     } else if (transform) {
 #pragma unroll
-      for (int ln = 0; ln < 2; ++ln) {  // a line at a time: the eight winners' Ψ reads issue together
+      for (int ln = 0; ln < 2; ++ln) {
+        // the last pass (along x3) on this line, then its eight winners (their Ψ reads issue together)
+        double o[8];
+#pragma unroll
+        for (int x = 0; x < 8; ++x) o[x] = dtv[pos3(8 * ln + x)];
+#pragma unroll
+        for (int x = 1; x < 8; ++x) o[x] = sd_merge(o[x], o[x - 1] + 1.0, tol);
+#pragma unroll
+        for (int x = 6; x >= 0; --x) o[x] = sd_merge(o[x], o[x + 1] + 1.0, tol);
         int jx[8];
         double pv[8];
 #pragma unroll
-        for (int x = 0; x < 8; ++x) jx[x] = (__double2loint(o[8 * ln + x]) >> SD_CB) & ((1 << SD_RB) - 1);
+        for (int x = 0; x < 8; ++x) jx[x] = (__double2loint(o[x]) >> SD_CB) & ((1 << SD_RB) - 1);
 #pragma unroll
         for (int x = 0; x < 8; ++x) pv[x] = psi[jx[x]];
 #pragma unroll
         for (int x = 0; x < 8; ++x) {
           const int e = 8 * ln + x, r = (tid + S2_T * ln) | (x << 9), j = jx[x];
-          const bool fin = (valid >> e & 1) && o[e] < INFINITY;
-          const bool flg = (__double2loint(o[e]) & SD_CNT) != 0;
+          const bool fin = (valid >> e & 1) && o[x] < INFINITY;
+          const bool flg = (__double2loint(o[x]) & SD_CNT) != 0;
           // d(l, j*) exactly: an unflagged finite o is V_j* + d with V_j* the stamp of Ψ_j*
-          const double dd = o[e] - stamp(pv[x], j);
-          const double t1 = pre[ln] + a[M - 1] * (double)(lb[M - 1] + x);
+          const double dd = o[x] - stamp(pv[x], j);
+          const double t1 = pre[ln] + a[M - 1] * (double)(lb[M - 1] + x + zop);
           const double val = (t1 + beta * dd) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
           listed |= (unsigned)(fin && flg) << e;
           uu[r] = (uint16_t)(fin && !flg ? j : 0xFFFF);
@@ -761,7 +769,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
           if (direct) {
             listed |= valid & (1u << e);
           } else if (valid >> e & 1) {  // sparse: the reference loop over the finite sources, ties to the lower rank
-            const double t1 = pre[ln] + a[M - 1] * (double)(lb[M - 1] + x);
+            const double t1 = pre[ln] + a[M - 1] * (double)(lb[M - 1] + x + zop);
             double bv = INFINITY;
             int bj = 0xFFFF;
             for (int q = 0; q < nf; ++q) {
@@ -790,8 +798,12 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
           ++e;
         }
     }
-    // this wave's stores of the previous item have landed (everything older than go()'s loads; they have had the
-    // whole item)
+    S2Ent eOn, eAnn;  // the orders of steps i-2 (the next item's outputs) and i-3 (A of the item after it): loaded
+                      // here, a while before the loop's back edge moves them into place (no wait there)
+    s2_ent_issue(eOn, pk + (size_t)pstep(i - 2) * S2_PACK, sk + (size_t)pstep(i - 2) * (S2_NW * S2_SEAMS));
+    s2_ent_issue(eAnn, pk + (size_t)pstep(i - 3) * S2_PACK, sk + (size_t)pstep(i - 3) * (S2_NW * S2_SEAMS));
+    // this wave's stores of the previous item have landed (everything older than go()'s loads and these orders; they
+    // have had the whole item)
     asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
     static_assert(S2_NGO == 25, "the late drain's count");
     sd_bar();  // (3) ... every wave's: the previous item is done; the list is complete
@@ -841,10 +853,6 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       Ur[1] = ub;
     }
     S2_TL(7);
-#if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
-    if (tid == 0 && tl_on && blockIdx.x < 1024)
-      for (int q = 0; q < 8; ++q) g_sdt2_tl[blockIdx.x][item - tl_item0][q] = tl[q];
-#endif
     prev_i = i;
   }
   // the last item: its stores drained, then published (the other workgroups of the rows above read step i_last)
@@ -855,6 +863,11 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       __hip_atomic_store(done + 2 * cp + par, tok(prev_i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
     if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
+#if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
+    if (blockIdx.x < 1024)
+      for (int j = 0; j < 32; ++j)
+        for (int q = 0; q < 8; ++q) g_sdt2_tl[blockIdx.x][j][q] = s2_tl_lds[j][q];
+#endif
   }
 }
 
