@@ -70,9 +70,9 @@ extern "C" {
 #define MIOC_OPT_SPIN_LIMIT 5 /* separable transform, persistent launch: polls a dependency wait may take
                                  before the launch is abandoned and the DP redone with per-step launches
                                  (default 2^24; a tiny value forces that fallback, for tests) */
-#define MIOC_OPT_SDT_BUFFERS 6 /* persistent separable transform: staging buffers (4..192, default 128; more
-                                  buffers let rows run further apart, which hides the row hand-off; halved
-                                  while a subproblem's staging region would exceed 4 GiB) */
+#define MIOC_OPT_SDT_BUFFERS 6 /* persistent separable transform: staging buffers (4..256, default 256; more
+                                  buffers let rows run further apart, which hides the row hand-off; cut to
+                                  the most that keep a subproblem's staging region under 4 GiB) */
 #define MIOC_OPT_FSEP_SEGMENTS 7 /* fused separable DP: row segments per subproblem, each on its own workgroup
                                     (0, default: chosen from the batch size -- more than one only when the
                                     batch alone cannot fill the GPU; 1..8: forced; -1: the one-lane-per-row

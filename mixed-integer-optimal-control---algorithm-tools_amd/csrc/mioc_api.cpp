@@ -104,7 +104,7 @@ void free_all(mioc_ctx *ctx) {
                   ctx->pinf.kabs, ctx->pinf.ftab, ctx->pinf.fseg, ctx->pinf.fneed,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
                   ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm, ctx->d_same2, ctx->d_strad,
-                  ctx->d_pack,  ctx->d_pseam,
+                  ctx->d_pack,  ctx->d_pseam,  ctx->d_phead,
                   ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own, ctx->d_ode_state};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -302,8 +302,12 @@ int run_bellman(mioc_ctx *ctx) {
     // persistent layout: per subproblem NB staging buffers of (B+1)·L, then row 0 of every step (nt·L), one region
     // addressed by one buffer resource (< 4 GiB); per-step layout: two buffers of K blocks of (B+1)·L
     int nbuf = persist ? ctx->opt_nb : 2;
-    // one buffer resource addresses a subproblem's whole region (32-bit offsets): fewer buffers where it would not fit
-    while (persist && nbuf > 4 && ((size_t)nbuf * s_stride + nt * L) * sizeof(double) >= (1ull << 32)) nbuf /= 2;
+    // one buffer resource addresses a subproblem's whole region (32-bit offsets): as many buffers as fit under 4 GiB
+    if (persist) {
+      const size_t cap = (1ull << 32) / sizeof(double);
+      const size_t fit = cap > nt * L ? (cap - nt * L - 1) / s_stride : 0;
+      if ((size_t)nbuf > fit) nbuf = (int)std::max<size_t>(fit, 4);
+    }
     const size_t kstride = persist ? (size_t)nbuf * s_stride + nt * L : s_stride;
     if (persist && kstride * sizeof(double) >= (1ull << 32)) persist = false;  // (then also kstride = s_stride)
     const size_t ks = persist ? kstride : s_stride;
@@ -330,6 +334,8 @@ int run_bellman(mioc_ctx *ctx) {
     if (!rc && seams) rc = grow(ctx, &ctx->d_strad, &ctx->strad_cap, K * nt * 8 * 32 * sizeof(uint16_t), "seam lists");
     if (!rc && pair) rc = grow(ctx, &ctx->d_pack, &ctx->pack_cap, K * nt * (L / 2) * sizeof(uint32_t), "packed orders");
     if (!rc && pair) rc = grow(ctx, &ctx->d_pseam, &ctx->pseam_cap, K * nt * 128 * sizeof(uint32_t), "packed seams");
+    if (!rc && pair)
+      rc = grow(ctx, &ctx->d_phead, &ctx->phead_cap, K * (size_t)(ctx->B + 1) * nt * 4 * sizeof(double), "row head parts");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
     double *term = persist ? ctx->d_stage + ((nt - 1) % nbuf) * s_stride : st[(nt - 1) & 1];
@@ -342,6 +348,9 @@ int run_bellman(mioc_ctx *ctx) {
                                    (size_t)nbuf * s_stride, (uint16_t *)ctx->d_U, uu_stride_k));
       if (pair) HIP_TRY(ctx, launch_sdt_pack(ctx->stream, P, ctx->d_perm, ctx->d_pack, ctx->d_pseam, ctx->d_counters));
       HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, runflag_bytes, ctx->stream));
+      // head values not yet written: all-ones (a NaN no DP value takes)
+      if (pair)
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_phead, 0xFF, K * (size_t)(ctx->B + 1) * nt * 4 * sizeof(double), ctx->stream));
       ctx->last_sdt_kernel = pair ? "k_sdt_pair" : "k_sdt_run";
       ev_begin(ctx, 0, ctx->last_sdt_kernel);
       // (the grid is nwg <= CUs x resident workgroups per CU by construction above; a wait that never ends anyway --
@@ -349,7 +358,7 @@ int run_bellman(mioc_ctx *ctx) {
       if (pair)
         HIP_TRY(ctx, launch_sdt_pair(ctx->stream, P, Lv, ctx->pyr, ctx->d_pack, ctx->d_pseam, ctx->d_stage, ks, nbuf,
                                      (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags,
-                                     ctx->spin_limit));
+                                     ctx->d_phead, ctx->spin_limit));
       else
         HIP_TRY(ctx, launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_same2, ctx->d_strad, ctx->d_stage,
                                     ks, nbuf, (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags, nwg,
@@ -700,7 +709,7 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
     return MIOC_OK;
   }
   if (option == MIOC_OPT_SDT_BUFFERS) {
-    if (value < 4 || value > kSdtMaxBuffers) return fail(ctx, MIOC_EINVAL, "staging buffers must be in [4, 192]");
+    if (value < 4 || value > kSdtMaxBuffers) return fail(ctx, MIOC_EINVAL, "staging buffers must be in [4, 256]");
     ctx->opt_nb = (int)value;
     return MIOC_OK;
   }

@@ -121,8 +121,8 @@ size_t pyr_lds_bytes(const PyrGeom &G);
 bool sdt_supported(const PyrGeom &G);
 bool sdt_seam_lists(const PyrGeom &G);  // the persistent driver loads straddling pair elements by seam lists (k_pyr_order)
 size_t sdt_lds_bytes(const PyrGeom &G);
-constexpr int kSdtMaxBuffers = 192;  // persistent separable transform: staging buffers S_i, step i in buffer i % NB
-constexpr int kSdtDefaultBuffers = 128;  // (C4: 128 x 8.4 MB + the 2.1 GB row-0 array, under the 4 GiB buffer range)
+constexpr int kSdtMaxBuffers = 256;  // persistent separable transform: staging buffers S_i, step i in buffer i % NB
+constexpr int kSdtDefaultBuffers = 256;  // at most (C4: 255 x 8.4 MB + the 2.1 GB row-0 array fit the 4 GiB buffer range)
 hipError_t launch_sdt_step(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int i,
                            const uint32_t *perm, const double *Sin, double *Sout, uint16_t *UU, size_t s_stride,
                            size_t uu_stride_k, int32_t *counters);
@@ -148,7 +148,7 @@ hipError_t launch_sdt_pack(hipStream_t s, const ProblemDev &P, const uint32_t *p
                            int32_t *counters);
 hipError_t launch_sdt_pair(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
                            const uint32_t *pack, const uint32_t *seams, double *S, size_t kstride, int NB, uint16_t *UU,
-                           size_t uu_stride_k, int32_t *counters, int32_t *flags, unsigned spin_limit);
+                           size_t uu_stride_k, int32_t *counters, int32_t *flags, double *heads, unsigned spin_limit);
 hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
                                 const double *S0, size_t s_stride, int Bu, Start *start);
 hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,
@@ -323,6 +323,8 @@ struct mioc_ctx {
   size_t pack_cap = 0;
   uint32_t *d_pseam = nullptr;     // [K][nt][4][32] seam words (k_sdt_pair)
   size_t pseam_cap = 0;
+  double *d_phead = nullptr;       // [K][B+1][nt][4] head-value parts handed between a row's two workgroups
+  size_t phead_cap = 0;
   int opt_sdt_pair = 1;            // 8^4 persistent separable DP: two workgroups per row (MIOC_OPT_SDT_PAIR)
   const char *last_sdt_kernel = "";  // the persistent separable kernel of the last DP (k_sdt_pair / k_sdt_run)
   size_t perm_cap = 0;

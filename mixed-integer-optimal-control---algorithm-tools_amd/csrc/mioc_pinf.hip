@@ -33,6 +33,9 @@ namespace mioc {
 #ifndef PINF_RECUR_MC_LANES
 #define PINF_RECUR_MC_LANES 8  // k_pinf_recur_mc: lanes per budget row (8: 8 rows per segment; 16: 4 rows, 8 % slower at C4; 4: 16 rows, 11 % slower with the one-step loop; 2: 32)
 #endif
+#ifndef PINF_MC_SPLIT
+#define PINF_MC_SPLIT 1  // k_pinf_recur_mc, 8 lanes per row: classes >= 8 (rows below the segment) off the step chain
+#endif
 #ifndef PINF_RECUR_XR
 #define PINF_RECUR_XR 1     // C4's B = 256: eight waves and the extra row split by classes (k_pinf_recur_xr)
 #endif
@@ -722,12 +725,72 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
       __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(rv), (unsigned)__double2hiint(rv)},
                                             Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
     };
-    // two steps per trip, the class-value registers alternating (no copies between steps)
-    double ka[CB], kb[CB];
-    kload(ka, hi);
-    for (int i = hi; i >= lo; i -= 2) {
-      step(i, ka, kb);
-      if (i - 1 >= lo) step(i - 1, kb, ka);
+    if constexpr (PINF_MC_SPLIT && LPR == 8) {
+      // The chain split in two.  Row c = 8q + r reads R_{i+1}[c - b]: a class b < 8 may read one of the segment's
+      // own rows, which the previous step wrote (the step-to-step chain); a class b >= 8 reads only rows below the
+      // segment, staged for the whole chunk, so their minimum P_i is computed one step ahead, off the chain.  On the
+      // chain, lane h of a row group takes classes 2(h&3) and 2(h&3)+1 (lanes h and h+4 the same two): two DPP
+      // steps and the min with P_i, where the one-part form above has three DPP steps after the class sums.  min is
+      // exact, so the grouping changes no bit.
+      constexpr int CO = (BWP - 8) / 8;  // off-chain classes per lane: 8 + CO·h .. 8 + CO·h + CO - 1
+      const int b0 = 2 * (h & 3);
+      // class values of step i (reads below the chunk's first step land in the LDS in front of Kc, unused)
+      auto kl = [&](double (&kc)[2], double (&kf)[CO], int i) {
+        const double *kr = Kc + (i - lo) * BWP;
+        const double2 y = *reinterpret_cast<const double2 *>(kr + b0);
+        kc[0] = y.x;
+        kc[1] = y.y;
+#pragma unroll
+        for (int t = 0; t < CO; ++t) kf[t] = kr[8 + CO * h + t];
+      };
+      // the off-chain part from the window R_{i+1}[c - 8 - CO·h - (CO-1) .. c - 8 - CO·h] (wf) and K_i (kf)
+      auto offc = [&](const double (&kf)[CO], const double (&wf)[CO]) {
+        double p = kf[0] + wf[CO - 1];
+#pragma unroll
+        for (int t = 1; t < CO; ++t) p = pvmin(p, kf[t] + wf[CO - 1 - t]);
+        p = pvmin(p, pv_dpp<0xB1>(p));
+        p = pvmin(p, pv_dpp<0x4E>(p));
+        return pvmin(p, pv_dpp<0x141>(p));
+      };
+      auto wload = [&](double (&wf)[CO], int i) {  // R_{i+1} below the segment, for step i's off-chain part
+        const double *Af = slot(i + 1) + u - 8 - CO * h - (CO - 1);
+#pragma unroll
+        for (int t = 0; t < CO; ++t) wf[t] = Af[t];
+      };
+      // one step: the chain's reads of step i issued first, then the off-chain reads and class values of step i-1
+      // (at the chunk's last step they read rows and values the chunk does not use), then P_i from the registers
+      // the previous step loaded -- its VALU work fills the wait for the chain's reads -- then the chain
+      auto st = [&](int i, const double (&kc)[2], const double (&kf)[CO], const double (&wf)[CO], double (&kcn)[2],
+                    double (&kfn)[CO], double (&wfn)[CO]) {
+        asm volatile("" ::: "memory");
+        const double *Ain = slot(i + 1) + u - b0 - 1;  // R_{i+1}[c - b0 - 1], R_{i+1}[c - b0]
+        const double w0 = Ain[0], w1 = Ain[1];
+        wload(wfn, i - 1);
+        kl(kcn, kfn, i - 1);
+        const double P = offc(kf, wf);
+        double rv = pvmin(kc[0] + w1, kc[1] + w0);
+        rv = pvmin(rv, pv_dpp<0xB1>(rv));
+        rv = pvmin(rv, pv_dpp<0x4E>(rv));
+        rv = pvmin(rv, P);
+        slot(i)[u] = rv;
+        __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(rv), (unsigned)__double2hiint(rv)},
+                                              Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
+      };
+      double kca[2], kcb[2], kfa[CO], kfb[CO], wa[CO], wb[CO];
+      kl(kca, kfa, hi);
+      wload(wa, hi);
+      for (int i = hi; i >= lo; i -= 2) {
+        st(i, kca, kfa, wa, kcb, kfb, wb);
+        if (i - 1 >= lo) st(i - 1, kcb, kfb, wb, kca, kfa, wa);
+      }
+    } else {
+      // two steps per trip, the class-value registers alternating (no copies between steps)
+      double ka[CB], kb[CB];
+      kload(ka, hi);
+      for (int i = hi; i >= lo; i -= 2) {
+        step(i, ka, kb);
+        if (i - 1 >= lo) step(i - 1, kb, ka);
+      }
     }
     // this chunk's rows have landed: publish its last step for the segments above
     vm_drain();

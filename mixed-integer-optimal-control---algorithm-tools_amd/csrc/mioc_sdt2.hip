@@ -55,8 +55,7 @@ namespace {
 constexpr int S2_L = 4096, S2_T = 256, S2_NW = 4, S2_Q = 8;  // levels, threads, waves, position pairs per lane
 constexpr int S2_SEAMS = 32;                                   // seam words per wave (<= 28 seams in a sphere order)
 constexpr int S2_PACK = S2_L / 2;                              // pair words per step
-constexpr int S2_NGO = 25;  // vector-memory instructions a wave issues from go() to the late drain (its counted wait)
-constexpr int S2_NST = 10;  // ... and as an item's stores (the counted wait at the next item's start)
+constexpr int S2_NST = 10;  // vector-memory instructions of an item's stores (the counted wait at the next item's start)
 
 // LDS (dynamic): Ψ by rank | transform values (swizzled; the outputs after the last pass) | U row | scan list |
 // per wave df(:, i..i+1), u_old(:, i..i+2)
@@ -66,7 +65,7 @@ constexpr size_t S2_PSI = 0, S2_DTV = S2_PSI + S2_L * 8, S2_UU = S2_DTV + S2_L *
 struct S2Shared {
   double redv[SD_COOP * S2_NW];
   int redj[SD_COOP * S2_NW];
-  double rmn[S2_NW], rmx[S2_NW], pmin[S2_NW];
+  double rmn[S2_NW], rmx[S2_NW], pmin[S2_NW];  // pmin: this item's head value (*) over each wave's values
   int rnv[S2_NW];
   int nlist;
   int stop;  // a dependency wait timed out: the launch is abandoned
@@ -74,7 +73,6 @@ struct S2Shared {
   int spj[SD_SPARSE];
   double spv[SD_SPARSE];
   int cnt[2];     // targets sent to the exact scan (near ties, direct rows); flushed to the counters [0], [1]
-  double l0keep;  // Φ_i[c', h(i)] of this workgroup's last item (the head term of the next chain step)
 };
 
 // pair word: rank_a | rank_b << 12 | b̃_a << 24 | (b̃_b != b̃_a) << 29; seam word: o | b̃ << 10 | rank << 16 for the
@@ -330,16 +328,18 @@ __shared__ unsigned long long s2_tl_lds[32][8];
 }  // namespace
 
 // The persistent DP, two workgroups per budget row (see the file header).  Grid: 2·K·B workgroups of 256 threads,
-// two resident per CU (the host checks); flags: done [K][B+1][2], loaded [K][B+1][2], then the error word (zeroed).
+// two resident per CU (the host checks); flags: done [K][B+1][2], loaded [K][B+1][2], then the error word (zeroed);
+// heads [K][B+1][nt][4]: item (c', i)'s four waves' parts of the head minimum (*), all-ones (a NaN) until written.
 __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv, PyrGeom G,
                                                      const uint32_t *__restrict__ pack_all,
                                                      const uint32_t *__restrict__ seam_all, double *S_all,
                                                      size_t kstride, int NB, uint16_t *__restrict__ UU_all,
                                                      size_t uu_stride_k, int32_t *__restrict__ counters,
-                                                     int32_t *flags, unsigned spin_limit,
+                                                     int32_t *flags, double *heads, unsigned spin_limit,
                                                      const double *__restrict__ df_all,
                                                      const double *__restrict__ uo_all) {
   constexpr int M = 4, L = S2_L, Smax = 7 * M;
+  constexpr unsigned OOB = 0xFFFFFFF0u;
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ S2Shared sh;
   double *psi = reinterpret_cast<double *>(sds + S2_PSI);
@@ -359,6 +359,11 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
   const int tid = threadIdx.x, lane = tid & 63;
   int32_t *done = flags + (size_t)k * R * 2, *loaded = flags + ((size_t)P.K + k) * R * 2;
   int32_t *err = flags + (size_t)P.K * R * 4;
+  // the flag words and this row's head values through buffer resources: every wave issues the same stores, with
+  // out-of-range offsets in all lanes but one (a fixed vector-memory sequence per wave, for the counted waits)
+  const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(flags, 0, (int)(((size_t)P.K * R * 4 + 1) * 4), 0x00020000);
+  double *hk = heads + ((size_t)k * R + cp) * nt * 4;  // item (cp, s)'s wave parts at hk[4s .. 4s+3]
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(hk, 0, nt * 32, 0x00020000);
   const unsigned rowb = (unsigned)L * 8u, bufb = (unsigned)R * rowb, r0b = (unsigned)NB * bufb;
   double *reg = S_all + (size_t)k * kstride;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(r0b + (unsigned)nt * rowb), 0x00020000);
@@ -378,12 +383,63 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
   if (tid == 0) {
     sh.stop = 0;
     sh.cnt[0] = sh.cnt[1] = 0;
-    sh.l0keep = INFINITY;  // Φ_{nt-1}[c', h(nt-1)] = +Inf for c' >= 1 (the terminal row is finite at budget b̃ only)
   }
+  // a wave-uniform wait for one flag word per lane (lanes with nothing to wait for point at row 0's words, never
+  // written, with need 0); false (and the launch abandoned) past the spin limit
+  auto spin = [&](const int32_t *fp, int need, int &val) {
+    unsigned spins = 0;
+    while (!__all(val >= need)) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
+        if (lane == 0) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sh.stop = 1;  // read after the next barrier: the launch is abandoned
+        }
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+  };
+  // The words item ii's go() checks: lanes 0..27 rows cp - s of step ii-1 (RAW, the values of the item after it) and
+  // rows cp + s of step ii+NB-1 (WAR: the readers of the step that buffer ii % NB held before item ii's stores)
+  struct Deps {
+    int32_t *fp1, *fp2;
+    int need1, need2;
+  };
+  auto deps = [&](int ii, int ln) {
+    Deps d{done, done, 0, 0};  // row 0's words: never written, needed 0
+    const int s = ln + 1;
+    if (ln < Smax) {
+      const int rd = cp - s, ru = cp + s, sw = ii + NB - 1;
+      if (ii - 2 >= 0 && rd >= 1) {
+        d.fp1 = done + 2 * rd + parof(ii - 1);
+        d.need1 = tok(ii - 1);
+      }
+      if (ru <= B && sw <= nt - 2) {
+        d.fp2 = loaded + 2 * ru + parof(sw);
+        d.need2 = tok(sw);
+      }
+    }
+    return d;
+  };
+  // What item ii reads before its first wait: the partner's head parts of step ii+1 (lanes 0..3; all-ones until that
+  // item has stored them) and its go() words -- issued one item ahead, before the stores, so that no wait on them
+  // waits for the stores
+  auto tail_loads = [&](int ii, int ln, double &pp, int &v1, int &v2) {
+    const Deps d = deps(ii, ln);
+    const unsigned long long *hp_src =
+        reinterpret_cast<const unsigned long long *>(hk + 4 * min(max(ii + 1, 0), nt - 1) + (ln & 3));
+    pp = __longlong_as_double((long long)__hip_atomic_load(hp_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    v1 = __hip_atomic_load(d.fp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v2 = __hip_atomic_load(d.fp2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  double pp;       // the partner's head parts (lanes 0..3)
+  int val1, val2;  // the go() words of the next item
+  double Hprev = INFINITY;  // Φ_{i+2}[cp, h(i+2)]: the previous item's head value (+Inf: the terminal row at cp >= 1)
   // ---- prologue: the first item's sphere orders and values; the next item's A orders ----------------------------
-  S2Ent eA, eP, eO, eAn;  // orders of steps i+1 (values A), i+2 (values P), i (outputs), i-1 (the next item's A)
+  S2Ent eA, eO, eAn;  // orders of steps i+1 (values A), i (outputs), i-1 (the next item's A)
   s2_ent_issue(eA, pk + (size_t)pstep(i0 + 1) * S2_PACK, sk + (size_t)pstep(i0 + 1) * (S2_NW * S2_SEAMS));
-  s2_ent_issue(eP, pk + (size_t)pstep(i0 + 2) * S2_PACK, sk + (size_t)pstep(i0 + 2) * (S2_NW * S2_SEAMS));
   s2_ent_issue(eO, pk + (size_t)i0 * S2_PACK, sk + (size_t)i0 * (S2_NW * S2_SEAMS));
   s2_ent_issue(eAn, pk + (size_t)pstep(i0 - 1) * S2_PACK, sk + (size_t)pstep(i0 - 1) * (S2_NW * S2_SEAMS));
   s2_dfuo_dma(dfk, uok, i0, nt, sds);
@@ -396,24 +452,14 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       fp = done + 2 * r + parof(nt - 2);
       need = tok(nt - 2);
     }
-    unsigned spins = 0;
-    while (!__all(__hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need)) {
-      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
-        if (lane == 0) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          sh.stop = 1;
-        }
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
+    int val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    spin(fp, need, val);
   }
+  tail_loads(i0, lane, pp, val1, val2);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the orders are in
   sd_bar();
-  S2Raw rA, rP;
+  S2Raw rA;
   s2_issue(rA, rs, eA, cp, boffs(i0 + 1), r0b + (unsigned)(i0 + 1) * rowb, rowb, sh.stop == 0);
-  // the P values (step i0 + 2) exist only below the terminal step
-  s2_issue(rP, rs, eP, cp, boffs(pstep(i0 + 2)), r0b + (unsigned)pstep(i0 + 2) * rowb, rowb, i0 + 2 <= nt - 1);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   sd_bar();
   bool stop = sh.stop != 0;
@@ -429,10 +475,11 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     // hoisted out of the loop into registers held across every item
     const int tid = sd_tid(), lane = tid & 63, w = tid >> 6;
     const bool has_next = i - 2 >= 0;
-    // everything but the previous item's ten stores has landed: this item's values, orders and df / u_old
+    // everything but the previous item's ten stores has landed: this item's values, orders, df / u_old, the partner's
+    // head parts and the go() words
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     static_assert(S2_NST == 10, "the item start's count");
-    // ---- the step's scalars (this wave's LDS copy): df(:, i), df(:, i+1), u_old(:, i .. i+2) --------------------
+    // ---- the step's scalars (this wave's LDS copy): df(:, i .. i+1), u_old(:, i .. i+2) -----------------------------
     // (the same in every lane: read into scalars)
     auto sread = [&](int e) {
       const double x = dfuo[e];
@@ -448,44 +495,80 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       u1[m] = sread(3 * M + m);
       u2[m] = sread(4 * M + m);
     }
-    const int h1 = s2_rank(u1, lb), h2 = s2_rank(u2, lb);
-    const bool sameP = h1 == h2;  // d(h(i+1), j) = b̃_j(i+2) (the sphere index of step i+2) for every j
-    // T1(h(i+1), i+1), left to right (HelpFunctions.jl:52-57): the level values of h(i+1) are u_old(:, i+1)
-    double T1P = 0.0;
+    const int h0 = s2_rank(u0, lb), h1 = s2_rank(u1, lb);
+    const bool sameH = h0 == h1;  // d(h(i), j) = b̃_j(i+1) (the sphere index of step i+1) for every j
+    // T1(h(i), i), left to right (HelpFunctions.jl:52-57): the level values of h(i) are u_old(:, i)
+    double T1H = 0.0;
 #pragma unroll
-    for (int m = 0; m < M; ++m) T1P = T1P + an[m] * u1[m];
-    int d12 = 0;
+    for (int m = 0; m < M; ++m) T1H = T1H + a[m] * u0[m];
+    int d01 = 0;
 #pragma unroll
-    for (int m = 0; m < M; ++m) d12 += abs((int)u1[m] - (int)u2[m]);
-    const unsigned hb1 = sd_bytes((unsigned)h1);
-    // ---- the chain (*): Φ_{i+1}[c', h(i+1)] over the P values, the head term after the barrier -------------------
-    double pm = INFINITY;
-    {
-      double v[2 * S2_Q], xs;
-      s2_take(v, xs, rP);
-      auto cand = [&](double x, unsigned d) { return (T1P + beta * (double)d) + x; };  // HelpFunctions.jl:67,71
-      if (sameP) {
-#pragma unroll
-        for (int q = 0; q < S2_Q; ++q) {
-          const unsigned d = (unsigned)s2_bt(eP.w[q]);
-          pm = sd_min(pm, sd_min(cand(v[2 * q], d), cand(v[2 * q + 1], d)));
+    for (int m = 0; m < M; ++m) d01 += abs((int)u0[m] - (int)u1[m]);
+    const unsigned hb0 = sd_bytes((unsigned)h0);
+    // ---- the value at this item's head position, Φ_{i+1}[c', h(i+1)] = min(the partner's parts over the values of its
+    // item (c', i+1), the term j = h(i+2): fl(fl(T1(h(i+1), i+1) + β·d(h(i+1), h(i+2))) + Φ_{i+2}[c', h(i+2)])); +Inf at
+    // the terminal step (Φ_{nt-1} is finite at budget b̃ only) -------------------------------------------------------
+    double l0v = INFINITY;
+    if (i < nt - 2) {
+      {  // the parts were loaded one item ahead; a part still all-ones (not yet stored) is polled here
+        // (the first test outside the loop: its operand is the tail load, which the item start's count covers)
+        bool okp = !__any(lane < 4 && __double_as_longlong(pp) == -1ll);
+        unsigned spins = 0;
+        while (!okp) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
+            if (lane == 0) {
+              __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              sh.stop = 1;
+            }
+            pp = INFINITY;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          pp = __longlong_as_double((long long)__hip_atomic_load(
+              reinterpret_cast<const unsigned long long *>(hk + 4 * (i + 1) + (lane & 3)), __ATOMIC_RELAXED,
+              __HIP_MEMORY_SCOPE_AGENT));
+          okp = !__any(lane < 4 && __double_as_longlong(pp) == -1ll);
         }
-        pm = sd_min(pm, cand(xs, (eP.seam >> 10) & 31u));
-      } else {
-#pragma unroll
-        for (int q = 0; q < S2_Q; ++q) {
-          pm = sd_min(pm, sd_min(cand(v[2 * q], sd_l1(sd_bytes((unsigned)s2_ra(eP.w[q])), hb1)),
-                                 cand(v[2 * q + 1], sd_l1(sd_bytes((unsigned)s2_rb(eP.w[q])), hb1))));
-        }
-        pm = sd_min(pm, cand(xs, sd_l1(sd_bytes(eP.seam >> 16), hb1)));
       }
-      pm = s2_wave_min(pm);
+      double T1P = 0.0;  // T1(h(i+1), i+1), left to right (HelpFunctions.jl:52-57)
+#pragma unroll
+      for (int m = 0; m < M; ++m) T1P = T1P + an[m] * u1[m];
+      int d12 = 0;
+#pragma unroll
+      for (int m = 0; m < M; ++m) d12 += abs((int)u1[m] - (int)u2[m]);
+      l0v = (T1P + beta * (double)d12) + Hprev;  // HelpFunctions.jl:67,71
+#pragma unroll
+      for (int q = 0; q < 4; ++q) l0v = sd_min(l0v, sd_rdl(pp, q));
     }
     // ---- this item's values A: Ψ by rank, raw into the transform buffer, the row's statistics -------------------
     double v[2 * S2_Q], xs;
     s2_take(v, xs, rA);
     const int srank = (int)(eA.seam >> 16);
     const bool shas = lane < 32 && eA.seam != 0xFFFFFFFFu;
+    // ---- this item's part of its own head value Φ_i[c', h(i)] (b̃ = 0, row c'), the chain (*): the minimum over the
+    // values of this wave, stored at once for the partner's next item (one lane per wave; every wave issues the store)
+    double hp = INFINITY;
+    {
+      auto cand = [&](double x, unsigned d) { return (T1H + beta * (double)d) + x; };  // HelpFunctions.jl:67,71
+      if (sameH) {
+#pragma unroll
+        for (int q = 0; q < S2_Q; ++q) {
+          const unsigned d = (unsigned)s2_bt(eA.w[q]);
+          hp = sd_min(hp, sd_min(cand(v[2 * q], d), cand(v[2 * q + 1], d)));
+        }
+        hp = sd_min(hp, cand(xs, (eA.seam >> 10) & 31u));
+      } else {
+#pragma unroll
+        for (int q = 0; q < S2_Q; ++q) {
+          hp = sd_min(hp, sd_min(cand(v[2 * q], sd_l1(sd_bytes((unsigned)s2_ra(eA.w[q])), hb0)),
+                                 cand(v[2 * q + 1], sd_l1(sd_bytes((unsigned)s2_rb(eA.w[q])), hb0))));
+        }
+        hp = sd_min(hp, cand(xs, sd_l1(sd_bytes(eA.seam >> 16), hb0)));
+      }
+      hp = s2_wave_min(hp);
+      __builtin_amdgcn_raw_buffer_store_b64((sd_u32x2){(unsigned)__double2loint(hp), (unsigned)__double2hiint(hp)},
+                                            hrs, lane == 0 ? (unsigned)(4 * i + w) * 8u : OOB, 0, 16);
+    }
     // this lane's targets: the lines q = tid and tid + 256 of the last pass, ranks q | x << 9
     int uo[M];
 #pragma unroll
@@ -544,44 +627,30 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       sh.rmn[w] = pmn;
       sh.rmx[w] = pmx;
       sh.rnv[w] = nv;
-      sh.pmin[w] = pm;
+      sh.pmin[w] = hp;
     }
     S2_TL(1);
     sd_bar();  // (1) every wave has consumed its values (in LDS now): `loaded`; the statistics are in
-    // ---- publish `loaded`, issue this wave's dependency polls (checked in go()) ------------------------------------
-    if (tid == 0) __hip_atomic_store(loaded + 2 * cp + par, tok(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int32_t *fp1 = done, *fp2 = done;  // row 0's words: never written, needed 0
-    int need1 = 0, need2 = 0;
+    // ---- this item's head value (the next item's head term) and `loaded` (one lane; every wave issues the store) ------
     {
-      // lanes 0..27: rows cp - s of steps i-1 (RAW, the next item's A) / cp + s of step i+NB-1 (WAR);
-      // lanes 32..59: rows cp - s of step i (RAW, the next item's P) / cp + s of step i+NB-2 (WAR)
-      const int s = (lane & 31) + 1, hi = lane >> 5;
-      if ((lane & 31) < Smax) {
-        const int rd = cp - s, ru = cp + s, sr = hi ? i : i - 1, sw = i + NB - 1 - hi;
-        if (has_next && rd >= 1) {
-          fp1 = done + 2 * rd + parof(sr);
-          need1 = tok(sr);
-        }
-        if (ru <= B && sw <= nt - 2) {
-          fp2 = loaded + 2 * ru + parof(sw);
-          need2 = tok(sw);
-        }
-      }
+      double hm = (T1H + beta * (double)d01) + l0v;  // the term j = h(i+1) of (*)
+#pragma unroll
+      for (int q = 0; q < S2_NW; ++q) hm = sd_min(hm, sh.pmin[q]);
+      Hprev = hm;
+      __builtin_amdgcn_raw_buffer_store_b32((unsigned)tok(i), frs,
+                                            tid == S2_T - 64 ? (unsigned)((size_t)(loaded + 2 * cp + par) - (size_t)flags)
+                                                             : OOB,
+                                            0, 16);
     }
-    int val1 = __hip_atomic_load(fp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int val2 = __hip_atomic_load(fp2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // ---- the row's statistics, the chain value and the A head h(i+1) ---------------------------------------------
-    double pmn2 = INFINITY, pmx2 = -INFINITY, l0v = INFINITY;
+    // ---- the row's statistics, the A head h(i+1) -------------------------------------------------------------------
+    double pmn2 = INFINITY, pmx2 = -INFINITY;
     nv = 0;
 #pragma unroll
     for (int q = 0; q < S2_NW; ++q) {
       pmn2 = sd_min(pmn2, sh.rmn[q]);
       pmx2 = sd_max(pmx2, sh.rmx[q]);
-      l0v = sd_min(l0v, sh.pmin[q]);
       nv += sh.rnv[q];
     }
-    l0v = sd_min(l0v, (T1P + beta * (double)d12) + sh.l0keep);  // the head term j = h(i+2) of (*)
-    // l0v = Φ_{i+1}[c', h(i+1)]: the value at this item's head position (b̃ = 0, row c')
     int nf = (nv >> 16) + (l0v < INFINITY ? 1 : 0);
     nv &= 0xFFFF;
     pmn2 = sd_min(pmn2, l0v);
@@ -646,9 +715,12 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     }
     const bool transform = !direct && !empty && !sparse;
     S2_TL(2);
-    // ---- go(): this wave's polls matched -> the next item's loads (A: step i-1, P: step i), the orders of the
-    // items after it, df / u_old; exactly S2_NGO vector-memory instructions ----------------------------------------
+    // ---- go(): this wave's polls matched (RAW: the rows below have published step i-1; WAR: the rows above have
+    // loaded the step this item's stores overwrite) -> the next item's loads (values A of step i-1, its df / u_old) --
     {
+      const Deps dp = deps(i, lane);
+      int32_t *const fp1 = dp.fp1, *const fp2 = dp.fp2;
+      const int need1 = dp.need1, need2 = dp.need2;
       bool ready = __all(val1 >= need1 && val2 >= need2);
       unsigned spins = 0;
       while (!ready) {
@@ -667,9 +739,8 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       S2_TL(3);
       const int ni = i - 2;
       s2_issue(rA, rs, eAn, cp, boffs(pstep(ni + 1)), r0b + (unsigned)pstep(ni + 1) * rowb, rowb, has_next);
-      s2_issue(rP, rs, eO, cp, boffs(i), r0b + (unsigned)i * rowb, rowb, has_next);
+      s2_dfuo_dma(dfk, uok, pstep(ni), nt, sds);
     }
-    s2_dfuo_dma(dfk, uok, pstep(i - 2), nt, sds);
     S2_TL(4);
     // ---- the transform -------------------------------------------------------------------------------------------
     auto pos3 = [&](int e) { return sd_swz((sd_tid() + S2_T * (e >> 3)) | ((e & 7) << 9)); };
@@ -715,9 +786,15 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       pass(1);
       sd_wave_sync();
       pass(2);
-      sd_bar();  // (2) the last pass runs along x3: every wave's values
     }
-    // (direct / sparse rows: no barrier here, they read Ψ by rank only after barrier (3))
+    // the previous item's stores have landed (all but this item's head part, `loaded` and go()'s ten instructions)
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    sd_bar();  // (2) the last pass runs along x3: every wave's values; the previous item is complete
+    __builtin_amdgcn_raw_buffer_store_b32((unsigned)tok(prev_i), frs,
+                                          tid == S2_T - 64 && prev_i >= 0
+                                              ? (unsigned)((size_t)(done + 2 * cp + par) - (size_t)flags)
+                                              : OOB,
+                                          0, 16);
     S2_TL(5);
     // ---- targets: R(l, j*) for a certified winner, the others listed for the exact scan ---------------------------
     // (outputs at the swizzled positions the last pass read: each lane writes only its own)
@@ -798,18 +875,12 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
           ++e;
         }
     }
+    S2_TL(6);
     S2Ent eOn, eAnn;  // the orders of steps i-2 (the next item's outputs) and i-3 (A of the item after it): loaded
                       // here, a while before the loop's back edge moves them into place (no wait there)
     s2_ent_issue(eOn, pk + (size_t)pstep(i - 2) * S2_PACK, sk + (size_t)pstep(i - 2) * (S2_NW * S2_SEAMS));
     s2_ent_issue(eAnn, pk + (size_t)pstep(i - 3) * S2_PACK, sk + (size_t)pstep(i - 3) * (S2_NW * S2_SEAMS));
-    // this wave's stores of the previous item have landed (everything older than go()'s loads and these orders; they
-    // have had the whole item)
-    asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
-    static_assert(S2_NGO == 25, "the late drain's count");
-    sd_bar();  // (3) ... every wave's: the previous item is done; the list is complete
-    if (tid == 0 && prev_i >= 0)
-      __hip_atomic_store(done + 2 * cp + par, tok(prev_i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    S2_TL(6);
+    sd_bar();  // (3) the list is complete
     const int nl = sh.nlist;
     if (nl) {
       if (nl <= SD_COOP)
@@ -821,24 +892,22 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       sd_bar();
       if (tid == 0) sh.cnt[direct ? 1 : 0] += nl;
     }
-    // ---- row c' of S_i in the sphere order of u_old(i), the U row; the chain's next head term ---------------------
+    // ---- row c' of S_i in the sphere order of u_old(i), the U row ---------------------------------------------------
     unsigned long long so[2 * S2_Q];
 #pragma unroll
     for (int q = 0; q < S2_Q; ++q) {
       so[2 * q] = __double_as_longlong(dtv[sd_swz(s2_ra(eO.w[q]))]);
       so[2 * q + 1] = __double_as_longlong(dtv[sd_swz(s2_rb(eO.w[q]))]);
     }
-    // position 0 of the order of step i is h(i) (b̃ = 0): this item's output there is the next item's head term
-    if (tid == 0) sh.l0keep = __longlong_as_double(so[0]);
     const ulonglong2 ua = reinterpret_cast<const ulonglong2 *>(uu)[2 * tid];
     const ulonglong2 ub = reinterpret_cast<const ulonglong2 *>(uu)[2 * tid + 1];
-    // the next item's orders: A = this item's eAn, P = this item's outputs' order, then the two loaded above
+    // the next item's orders: A = this item's eAn, outputs = the one loaded above, then A of the item after it
     eA = eAn;
-    eP = eO;
     eO = eOn;
     eAn = eAnn;
     sd_bar();  // (4) every wave has read the outputs: the next item may overwrite the buffers
     stop = sh.stop != 0;
+    tail_loads(i - 2, lane, pp, val1, val2);  // before the stores (the next item's first waits do not wait for them)
     {
       const __amdgpu_buffer_rsrc_t rso = sd_rsrc(reg + (size_t)(i % NB) * R * L + (size_t)cp * L, L * 8);
 #pragma unroll
@@ -893,13 +962,14 @@ hipError_t launch_sdt_pack(hipStream_t s, const ProblemDev &P, const uint32_t *p
 
 hipError_t launch_sdt_pair(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
                            const uint32_t *pack, const uint32_t *seams, double *S, size_t kstride, int NB, uint16_t *UU,
-                           size_t uu_stride_k, int32_t *counters, int32_t *flags, unsigned spin_limit) {
+                           size_t uu_stride_k, int32_t *counters, int32_t *flags, double *heads, unsigned spin_limit) {
   // every workgroup must be resident (the caller checked 2·K·B <= CUs x resident workgroups per CU); an ordinary
   // launch (mioc_sdt.hip, launch_sdt_run: a cooperative launch crashed the profiler at exit)
   const double *df = P.df, *uo = P.uold;
   void *args[] = {(void *)&P,     (void *)&Lv,         (void *)&G,     (void *)&pack,       (void *)&seams,
                   (void *)&S,     (void *)&kstride,    (void *)&NB,    (void *)&UU,         (void *)&uu_stride_k,
-                  (void *)&counters, (void *)&flags,   (void *)&spin_limit, (void *)&df,   (void *)&uo};
+                  (void *)&counters, (void *)&flags,   (void *)&heads, (void *)&spin_limit, (void *)&df,
+                  (void *)&uo};
   return hipLaunchKernel((const void *)k_sdt_pair, dim3(2 * P.K * P.B), dim3(S2_T), args, S2_LDS, s);
 }
 

@@ -1,8 +1,8 @@
 """Timeline of k_sdt_pair (the two-workgroups-per-row persistent separable DP, mioc_sdt2.hip) from the diagnostic
 build libmioc_stamps_tl.so (`make stamps_tl`): per workgroup and for 32 of its items from the middle of the run,
-s_memrealtime (100 MHz) at 8 points of an item: 0 start, 1 statistics written (before barrier 1), 2 go() entered
-(after the sparse path), 3 polls matched, 4 next loads + orders issued, 5 transform done, 6 after the late drain's
-barrier (3), 7 stores issued.  Prints the phase medians, the item period per workgroup and the skew between rows.
+s_memrealtime (100 MHz) at 8 points of an item: 0 start, 1 statistics written (before the head poll and barrier 1),
+2 go() entered (head value published, after the sparse path), 3 polls matched, 4 the next loads issued, 5 transform
+done, 6 winners done, 7 stores issued.  Prints the phase medians, the item period per workgroup and the skew between rows.
 Usage: python scripts/probe_sdt2_timeline.py [nt]"""
 import ctypes
 import os
@@ -29,6 +29,8 @@ def main():
         ctx.set_cost(1, cfg.beta)
         ctx.set_option(native.MIOC_OPT_TIMING, 1)
         ctx.set_option(native.MIOC_OPT_SDT_PAIR, 1)
+        if int(os.environ.get("SDT_NB", "0")):  # staging buffers (MIOC_OPT_SDT_BUFFERS)
+            ctx.set_option(native.MIOC_OPT_SDT_BUFFERS, int(os.environ["SDT_NB"]))
         ctx.bellman(df, uo, cfg.B, cfg.dt)
         ctx.synchronize()
         ms, _, name = ctx.kernel_stats(0)
@@ -41,9 +43,12 @@ def main():
     f.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     assert f(buf.ctypes.data, 1024) == 0
     t = buf[:NB].astype(np.float64) * 0.01  # us (100 MHz)
+    out = os.environ.get("TL_SAVE")  # the raw stamps for offline analysis (blocks x items x points, us)
+    if out:
+        np.save(out, t)
     d = np.diff(t, axis=2)
-    names = ["start -> stats written", "-> go()", "poll wait", "issue loads + orders", "transform",
-             "winners + late drain + barrier", "scans + gather + stores"]
+    names = ["start -> stats written", "head poll + drain + barrier 1", "poll wait", "issue", "transform",
+             "winners", "orders + scans + gather + stores"]
     for q, nm in enumerate(names):
         x = d[:, :, q].ravel()
         print(f"{nm:34s} median {np.median(x):7.3f}  p10 {np.percentile(x, 10):7.3f}  p90 {np.percentile(x, 90):7.3f} us")
@@ -59,6 +64,12 @@ def main():
     order = np.argsort(row)
     sk = np.diff(st0[order])
     print(f"skew row c vs c-1 (parity 0, same item): median {np.median(sk):.3f} us, total {np.sum(sk):.1f} us")
+    # per row (parity 0): the phases of rows 1, 2, 3, B/2 and B
+    blk = {int(r): int(b) for b, r in enumerate(row)}
+    for r in (1, 2, 3, R // 2, R):
+        b = blk[r]
+        ph = " ".join(f"{np.median(d[b, :, q]):6.2f}" for q in range(7))
+        print(f"row {r:4d}: phases {ph}  period {np.median(np.diff(t[b, :, 0])):6.2f} us")
 
 
 if __name__ == "__main__":
