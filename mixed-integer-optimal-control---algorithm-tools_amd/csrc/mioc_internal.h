@@ -325,7 +325,7 @@ struct mioc_ctx {
   size_t pseam_cap = 0;
   double *d_phead = nullptr;       // [K][B+1][nt][4] head-value parts handed between a row's two workgroups
   size_t phead_cap = 0;
-  int opt_sdt_pair = 1;            // 8^4 persistent separable DP: two workgroups per row (MIOC_OPT_SDT_PAIR)
+  int opt_sdt_pair = 0;            // 8^4 persistent separable DP: two workgroups per row (MIOC_OPT_SDT_PAIR, opt-in)
   const char *last_sdt_kernel = "";  // the persistent separable kernel of the last DP (k_sdt_pair / k_sdt_run)
   size_t perm_cap = 0;
   bool opt_persist = true;         // separable transform: one persistent launch (MIOC_OPT_PERSIST)

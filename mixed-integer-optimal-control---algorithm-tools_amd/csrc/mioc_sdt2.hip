@@ -315,6 +315,12 @@ __device__ __forceinline__ void s2_scan(const uint16_t *list, int nl, const doub
 // the item's counted waits rely on) and copied out at the end
 __device__ unsigned long long g_sdt2_tl[1024][32][8];
 __shared__ unsigned long long s2_tl_lds[32][8];
+__device__ unsigned long long g_sdt2_tlx[1024][32][4];  // extra points: 0 item-start wait done, 1 head parts in, 2 spins
+__shared__ unsigned long long s2_tlx_lds[32][4];
+#define S2_TLX(k, v)                                                            \
+  do {                                                                          \
+    if (threadIdx.x == 0 && tl_on) s2_tlx_lds[item - tl_item0][k] = (v);       \
+  } while (0)
 #define S2_TL(k)                                                                                                \
   do {                                                                                                          \
     if (threadIdx.x == 0 && tl_on) s2_tl_lds[item - tl_item0][k] = __builtin_amdgcn_s_memrealtime();          \
@@ -322,6 +328,9 @@ __shared__ unsigned long long s2_tl_lds[32][8];
 #else
 #define S2_TL(k) \
   do {           \
+  } while (0)
+#define S2_TLX(k, v) \
+  do {               \
   } while (0)
 #endif
 
@@ -352,7 +361,10 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
   const int par = (int)blockIdx.x / NR, rid0 = (int)blockIdx.x - par * NR;
   // rows by XCD (blocks b and b + 8 share one under round-robin dispatch; speed only): consecutive rows -- which read
   // each other -- on one XCD; the two workgroups of a row (b, b + NR) too when NR % 8 == 0
-  const int rid = NR % 8 == 0 ? (rid0 & 7) * (NR >> 3) + (rid0 >> 3) : rid0;
+  // and the second workgroups shifted by half the rows: under that dispatch blocks b and b + NR share a CU, and the two
+  // workgroups of one row, which hand each other the head parts, fall into step and compete for the same SIMDs
+  const int rid1 = NR % 8 == 0 ? (rid0 & 7) * (NR >> 3) + (rid0 >> 3) : rid0;
+  const int rid = par ? (rid1 + NR / 2) % NR : rid1;
   const int k = rid / B, cp = 1 + rid % B;
   const int i0 = nt - 2 - par;  // this workgroup's first step; then i0 - 2, i0 - 4, ...
   if (i0 < 0) return;
@@ -423,19 +435,15 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     }
     return d;
   };
-  // What item ii reads before its first wait: the partner's head parts of step ii+1 (lanes 0..3; all-ones until that
-  // item has stored them) and its go() words -- issued one item ahead, before the stores, so that no wait on them
-  // waits for the stores
-  auto tail_loads = [&](int ii, int ln, double &pp, int &v1, int &v2) {
-    const Deps d = deps(ii, ln);
-    const unsigned long long *hp_src =
+  // The partner's head parts of step ii+1 (lanes 0..3; all-ones until that item has stored them), which item ii reads
+  // before its first wait: loaded one item ahead, before the stores, so that the wait on them does not wait for the
+  // stores
+  auto parts_load = [&](int ii, int ln) {
+    const unsigned long long *src =
         reinterpret_cast<const unsigned long long *>(hk + 4 * min(max(ii + 1, 0), nt - 1) + (ln & 3));
-    pp = __longlong_as_double((long long)__hip_atomic_load(hp_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    v1 = __hip_atomic_load(d.fp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    v2 = __hip_atomic_load(d.fp2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __longlong_as_double((long long)__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   };
-  double pp;       // the partner's head parts (lanes 0..3)
-  int val1, val2;  // the go() words of the next item
+  double pp;  // the partner's head parts (lanes 0..3)
   double Hprev = INFINITY;  // Φ_{i+2}[cp, h(i+2)]: the previous item's head value (+Inf: the terminal row at cp >= 1)
   // ---- prologue: the first item's sphere orders and values; the next item's A orders ----------------------------
   S2Ent eA, eO, eAn;  // orders of steps i+1 (values A), i (outputs), i-1 (the next item's A)
@@ -455,7 +463,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     int val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     spin(fp, need, val);
   }
-  tail_loads(i0, lane, pp, val1, val2);
+  pp = parts_load(i0, lane);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the orders are in
   sd_bar();
   S2Raw rA;
@@ -479,6 +487,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     // head parts and the go() words
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     static_assert(S2_NST == 10, "the item start's count");
+    S2_TLX(0, __builtin_amdgcn_s_memrealtime());
     // ---- the step's scalars (this wave's LDS copy): df(:, i .. i+1), u_old(:, i .. i+2) -----------------------------
     // (the same in every lane: read into scalars)
     auto sread = [&](int e) {
@@ -505,41 +514,6 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
 #pragma unroll
     for (int m = 0; m < M; ++m) d01 += abs((int)u0[m] - (int)u1[m]);
     const unsigned hb0 = sd_bytes((unsigned)h0);
-    // ---- the value at this item's head position, Φ_{i+1}[c', h(i+1)] = min(the partner's parts over the values of its
-    // item (c', i+1), the term j = h(i+2): fl(fl(T1(h(i+1), i+1) + β·d(h(i+1), h(i+2))) + Φ_{i+2}[c', h(i+2)])); +Inf at
-    // the terminal step (Φ_{nt-1} is finite at budget b̃ only) -------------------------------------------------------
-    double l0v = INFINITY;
-    if (i < nt - 2) {
-      {  // the parts were loaded one item ahead; a part still all-ones (not yet stored) is polled here
-        // (the first test outside the loop: its operand is the tail load, which the item start's count covers)
-        bool okp = !__any(lane < 4 && __double_as_longlong(pp) == -1ll);
-        unsigned spins = 0;
-        while (!okp) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
-            if (lane == 0) {
-              __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              sh.stop = 1;
-            }
-            pp = INFINITY;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          pp = __longlong_as_double((long long)__hip_atomic_load(
-              reinterpret_cast<const unsigned long long *>(hk + 4 * (i + 1) + (lane & 3)), __ATOMIC_RELAXED,
-              __HIP_MEMORY_SCOPE_AGENT));
-          okp = !__any(lane < 4 && __double_as_longlong(pp) == -1ll);
-        }
-      }
-      double T1P = 0.0;  // T1(h(i+1), i+1), left to right (HelpFunctions.jl:52-57)
-#pragma unroll
-      for (int m = 0; m < M; ++m) T1P = T1P + an[m] * u1[m];
-      int d12 = 0;
-#pragma unroll
-      for (int m = 0; m < M; ++m) d12 += abs((int)u1[m] - (int)u2[m]);
-      l0v = (T1P + beta * (double)d12) + Hprev;  // HelpFunctions.jl:67,71
-#pragma unroll
-      for (int q = 0; q < 4; ++q) l0v = sd_min(l0v, sd_rdl(pp, q));
-    }
     // ---- this item's values A: Ψ by rank, raw into the transform buffer, the row's statistics -------------------
     double v[2 * S2_Q], xs;
     s2_take(v, xs, rA);
@@ -569,6 +543,43 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       __builtin_amdgcn_raw_buffer_store_b64((sd_u32x2){(unsigned)__double2loint(hp), (unsigned)__double2hiint(hp)},
                                             hrs, lane == 0 ? (unsigned)(4 * i + w) * 8u : OOB, 0, 16);
     }
+    // ---- the value at this item's head position, Φ_{i+1}[c', h(i+1)] = min(the partner's parts over the values of its
+    // item (c', i+1), the term j = h(i+2): fl(fl(T1(h(i+1), i+1) + β·d(h(i+1), h(i+2))) + Φ_{i+2}[c', h(i+2)])); +Inf at
+    // the terminal step (Φ_{nt-1} is finite at budget b̃ only) -------------------------------------------------------
+    double l0v = INFINITY;
+    if (i < nt - 2) {
+      {  // the parts were loaded one item ahead; a part still all-ones (not yet stored) is polled here
+        // (the first test outside the loop: its operand is the tail load, which the item start's count covers)
+        bool okp = !__any(lane < 4 && __double_as_longlong(pp) == -1ll);
+        unsigned spins = 0;
+        while (!okp) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
+            if (lane == 0) {
+              __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              sh.stop = 1;
+            }
+            pp = INFINITY;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          pp = __longlong_as_double((long long)__hip_atomic_load(
+              reinterpret_cast<const unsigned long long *>(hk + 4 * (i + 1) + (lane & 3)), __ATOMIC_RELAXED,
+              __HIP_MEMORY_SCOPE_AGENT));
+          okp = !__any(lane < 4 && __double_as_longlong(pp) == -1ll);
+        }
+        S2_TLX(2, spins);
+      }
+      double T1P = 0.0;  // T1(h(i+1), i+1), left to right (HelpFunctions.jl:52-57)
+#pragma unroll
+      for (int m = 0; m < M; ++m) T1P = T1P + an[m] * u1[m];
+      int d12 = 0;
+#pragma unroll
+      for (int m = 0; m < M; ++m) d12 += abs((int)u1[m] - (int)u2[m]);
+      l0v = (T1P + beta * (double)d12) + Hprev;  // HelpFunctions.jl:67,71
+#pragma unroll
+      for (int q = 0; q < 4; ++q) l0v = sd_min(l0v, sd_rdl(pp, q));
+    }
+    S2_TLX(1, __builtin_amdgcn_s_memrealtime());
     // this lane's targets: the lines q = tid and tid + 256 of the last pass, ranks q | x << 9
     int uo[M];
 #pragma unroll
@@ -630,16 +641,30 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       sh.pmin[w] = hp;
     }
     S2_TL(1);
-    sd_bar();  // (1) every wave has consumed its values (in LDS now): `loaded`; the statistics are in
+    // every wave's stores of the previous item have landed (all but this item's head part, younger)
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    sd_bar();  // (1) every wave has consumed its values (in LDS now): `loaded`; the statistics are in; the previous
+               // item is complete: `done`
     // ---- this item's head value (the next item's head term) and `loaded` (one lane; every wave issues the store) ------
     {
       double hm = (T1H + beta * (double)d01) + l0v;  // the term j = h(i+1) of (*)
 #pragma unroll
       for (int q = 0; q < S2_NW; ++q) hm = sd_min(hm, sh.pmin[q]);
       Hprev = hm;
+    }
+    // go()'s words, checked after the winners
+    const Deps dp = deps(i, lane);
+    int val1 = __hip_atomic_load(dp.fp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int val2 = __hip_atomic_load(dp.fp2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    {
       __builtin_amdgcn_raw_buffer_store_b32((unsigned)tok(i), frs,
                                             tid == S2_T - 64 ? (unsigned)((size_t)(loaded + 2 * cp + par) - (size_t)flags)
                                                              : OOB,
+                                            0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32((unsigned)tok(prev_i), frs,
+                                            tid == S2_T - 64 && prev_i >= 0
+                                                ? (unsigned)((size_t)(done + 2 * cp + par) - (size_t)flags)
+                                                : OOB,
                                             0, 16);
     }
     // ---- the row's statistics, the A head h(i+1) -------------------------------------------------------------------
@@ -715,33 +740,6 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     }
     const bool transform = !direct && !empty && !sparse;
     S2_TL(2);
-    // ---- go(): this wave's polls matched (RAW: the rows below have published step i-1; WAR: the rows above have
-    // loaded the step this item's stores overwrite) -> the next item's loads (values A of step i-1, its df / u_old) --
-    {
-      const Deps dp = deps(i, lane);
-      int32_t *const fp1 = dp.fp1, *const fp2 = dp.fp2;
-      const int need1 = dp.need1, need2 = dp.need2;
-      bool ready = __all(val1 >= need1 && val2 >= need2);
-      unsigned spins = 0;
-      while (!ready) {
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
-          if (lane == 0) {
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sh.stop = 1;  // read after the next barrier: the launch is abandoned
-          }
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        val1 = __hip_atomic_load(fp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        val2 = __hip_atomic_load(fp2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ready = __all(val1 >= need1 && val2 >= need2);
-      }
-      S2_TL(3);
-      const int ni = i - 2;
-      s2_issue(rA, rs, eAn, cp, boffs(pstep(ni + 1)), r0b + (unsigned)pstep(ni + 1) * rowb, rowb, has_next);
-      s2_dfuo_dma(dfk, uok, pstep(ni), nt, sds);
-    }
-    S2_TL(4);
     // ---- the transform -------------------------------------------------------------------------------------------
     auto pos3 = [&](int e) { return sd_swz((sd_tid() + S2_T * (e >> 3)) | ((e & 7) << 9)); };
     // an opaque zero: the targets' T1 terms a_3·ν_3 are recomputed per target (two VALU) instead of being hoisted into
@@ -787,15 +785,8 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       sd_wave_sync();
       pass(2);
     }
-    // the previous item's stores have landed (all but this item's head part, `loaded` and go()'s ten instructions)
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    sd_bar();  // (2) the last pass runs along x3: every wave's values; the previous item is complete
-    __builtin_amdgcn_raw_buffer_store_b32((unsigned)tok(prev_i), frs,
-                                          tid == S2_T - 64 && prev_i >= 0
-                                              ? (unsigned)((size_t)(done + 2 * cp + par) - (size_t)flags)
-                                              : OOB,
-                                          0, 16);
-    S2_TL(5);
+    if (transform) sd_bar();  // (2) the last pass runs along x3: every wave's values
+    S2_TL(3);
     // ---- targets: R(l, j*) for a certified winner, the others listed for the exact scan ---------------------------
     // (outputs at the swizzled positions the last pass read: each lane writes only its own)
     unsigned listed = 0;
@@ -875,6 +866,42 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
           ++e;
         }
     }
+    S2_TL(4);
+#if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
+    unsigned long long tl_bits = 0;
+#endif
+    // ---- go(): this wave's polls matched (RAW: the rows below have published step i-1; WAR: the rows above have
+    // loaded the step this item's stores overwrite) -> the next item's loads (values A of step i-1, its df / u_old) --
+    {
+      int32_t *const fp1 = dp.fp1, *const fp2 = dp.fp2;
+      const int need1 = dp.need1, need2 = dp.need2;
+      bool ready = __all(val1 >= need1 && val2 >= need2);
+#if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
+      // the first test's outcome in the stamp's top bits: 62 RAW unmet, 61 WAR unmet
+      tl_bits = (__all(val1 >= need1) ? 0ull : 1ull << 62) | (__all(val2 >= need2) ? 0ull : 1ull << 61);
+#endif
+      unsigned spins = 0;
+      while (!ready) {
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
+          if (lane == 0) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh.stop = 1;  // read after the next barrier: the launch is abandoned
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        val1 = __hip_atomic_load(fp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        val2 = __hip_atomic_load(fp2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ready = __all(val1 >= need1 && val2 >= need2);
+      }
+      const int ni = i - 2;
+      s2_issue(rA, rs, eAn, cp, boffs(pstep(ni + 1)), r0b + (unsigned)pstep(ni + 1) * rowb, rowb, has_next);
+      s2_dfuo_dma(dfk, uok, pstep(ni), nt, sds);
+    }
+    S2_TL(5);
+#if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
+    if (threadIdx.x == 0 && tl_on) s2_tl_lds[item - tl_item0][5] |= tl_bits;
+#endif
     S2_TL(6);
     S2Ent eOn, eAnn;  // the orders of steps i-2 (the next item's outputs) and i-3 (A of the item after it): loaded
                       // here, a while before the loop's back edge moves them into place (no wait there)
@@ -907,7 +934,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     eAn = eAnn;
     sd_bar();  // (4) every wave has read the outputs: the next item may overwrite the buffers
     stop = sh.stop != 0;
-    tail_loads(i - 2, lane, pp, val1, val2);  // before the stores (the next item's first waits do not wait for them)
+    pp = parts_load(i - 2, lane);  // before the stores (the next item's first wait does not wait for them)
     {
       const __amdgpu_buffer_rsrc_t rso = sd_rsrc(reg + (size_t)(i % NB) * R * L + (size_t)cp * L, L * 8);
 #pragma unroll
@@ -936,6 +963,9 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     if (blockIdx.x < 1024)
       for (int j = 0; j < 32; ++j)
         for (int q = 0; q < 8; ++q) g_sdt2_tl[blockIdx.x][j][q] = s2_tl_lds[j][q];
+    if (blockIdx.x < 1024)
+      for (int j = 0; j < 32; ++j)
+        for (int q = 0; q < 4; ++q) g_sdt2_tlx[blockIdx.x][j][q] = s2_tlx_lds[j][q];
 #endif
   }
 }
@@ -974,6 +1004,12 @@ hipError_t launch_sdt_pair(hipStream_t s, const ProblemDev &P, const LevelsDev &
 }
 
 #if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
+extern "C" int32_t mioc_debug_sdt2_timeline_x(unsigned long long *out, int64_t nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sdt2_tlx), (size_t)nblocks * 32 * 4 * sizeof(unsigned long long)) ==
+                 hipSuccess
+             ? 0
+             : -4;
+}
 extern "C" int32_t mioc_debug_sdt2_timeline(unsigned long long *out, int64_t nblocks) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sdt2_tl), (size_t)nblocks * 32 * 8 * sizeof(unsigned long long)) ==
                  hipSuccess

@@ -1,8 +1,8 @@
 """Timeline of k_sdt_pair (the two-workgroups-per-row persistent separable DP, mioc_sdt2.hip) from the diagnostic
 build libmioc_stamps_tl.so (`make stamps_tl`): per workgroup and for 32 of its items from the middle of the run,
-s_memrealtime (100 MHz) at 8 points of an item: 0 start, 1 statistics written (before the head poll and barrier 1),
-2 go() entered (head value published, after the sparse path), 3 polls matched, 4 the next loads issued, 5 transform
-done, 6 winners done, 7 stores issued.  Prints the phase medians, the item period per workgroup and the skew between rows.
+s_memrealtime (100 MHz) at 8 points of an item: 0 start, 1 statistics written (before the drain and barrier 1 that
+publish the previous item), 2 before the transform, 3 after the transform, 4 winners done (go() entered), 5 go()'s
+polls matched and the next loads issued, 6 (= 5), 7 stores issued.  Prints the phase medians, the item period per workgroup and the skew between rows.
 Usage: python scripts/probe_sdt2_timeline.py [nt]"""
 import ctypes
 import os
@@ -42,13 +42,23 @@ def main():
     f.restype = ctypes.c_int32
     f.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     assert f(buf.ctypes.data, 1024) == 0
+    raw_unmet = (buf[:NB, :, 5] >> np.uint64(62)) & np.uint64(1)
+    war_unmet = (buf[:NB, :, 5] >> np.uint64(61)) & np.uint64(1)
+    buf[:NB, :, 5] &= np.uint64((1 << 61) - 1)
+    print(f"go() first test unmet: RAW {raw_unmet.mean():.3f}, WAR {war_unmet.mean():.3f} of the items")
     t = buf[:NB].astype(np.float64) * 0.01  # us (100 MHz)
+    bx = np.zeros((1024, 32, 4), dtype=np.uint64)
+    fx = lib.mioc_debug_sdt2_timeline_x
+    fx.restype = ctypes.c_int32
+    fx.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    assert fx(bx.ctypes.data, 1024) == 0
     out = os.environ.get("TL_SAVE")  # the raw stamps for offline analysis (blocks x items x points, us)
     if out:
         np.save(out, t)
+        np.save(out.replace(".npy", "_x.npy"), bx[:NB])
     d = np.diff(t, axis=2)
-    names = ["start -> stats written", "head poll + drain + barrier 1", "poll wait", "issue", "transform",
-             "winners", "orders + scans + gather + stores"]
+    names = ["start -> stats written", "drain + barrier 1 + head value", "transform", "winners", "poll wait + issue",
+             "-", "orders + scans + gather + stores"]
     for q, nm in enumerate(names):
         x = d[:, :, q].ravel()
         print(f"{nm:34s} median {np.median(x):7.3f}  p10 {np.percentile(x, 10):7.3f}  p90 {np.percentile(x, 90):7.3f} us")
@@ -69,7 +79,8 @@ def main():
     for r in (1, 2, 3, R // 2, R):
         b = blk[r]
         ph = " ".join(f"{np.median(d[b, :, q]):6.2f}" for q in range(7))
-        print(f"row {r:4d}: phases {ph}  period {np.median(np.diff(t[b, :, 0])):6.2f} us")
+        print(f"row {r:4d}: phases {ph}  period {np.median(np.diff(t[b, :, 0])):6.2f} us  "
+              f"unmet RAW {raw_unmet[b].mean():.2f} WAR {war_unmet[b].mean():.2f}")
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
-"""GPU parity of the C4 (BASELINE roofline) shape on the code the bench times: k_sdt_pair (the persistent separable
-transform with two workgroups per budget row, 8^4 = 4096 levels, B = 256, p = 1) -- and the one-workgroup-per-row
-k_sdt_run<4> and the per-step k_sdt_step -- against the CPU oracle, never against another device algorithm.
+"""GPU parity of the C4 (BASELINE roofline) shape on the code the bench times: k_sdt_run<4> (the persistent separable
+transform, one workgroup per budget row, 8^4 = 4096 levels, B = 256, p = 1) -- and the opt-in two-workgroups-per-row
+k_sdt_pair and the per-step k_sdt_step -- against the CPU oracle, never against another device algorithm.
 
   * a committed oracle fixture at the full L = 4096, B = 256 with nt = 64 (63 recursion steps: every rotation of
     the four staging buffers and row B's two-step lag, many times): sha256 of every step's argmin table U in the
@@ -42,8 +42,8 @@ def _hash(t):
 @pytest.mark.parametrize("variant", ["pair", "persistent", "steps"])
 def test_c4_nt64_fixture(variant):
     """The separable transform writes U exactly like the reference: the rank where the reference writes it, and
-    nothing (-1) elsewhere, so every step's table hashes to the oracle's.  pair: k_sdt_pair (the bench's kernel),
-    persistent: k_sdt_run, steps: one k_sdt_step launch per step."""
+    nothing (-1) elsewhere, so every step's table hashes to the oracle's.  persistent: k_sdt_run (the bench's kernel),
+    pair: k_sdt_pair (MIOC_OPT_SDT_PAIR), steps: one k_sdt_step launch per step."""
     z = np.load(os.path.join(HERE, "golden", "hashed", "c4_4096lv_p1_nt64_uhash.npz"), allow_pickle=False)
     cfg = CONFIGS["C4"]
     lt = cfg.levels()
