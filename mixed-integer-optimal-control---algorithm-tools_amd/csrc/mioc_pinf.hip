@@ -36,6 +36,9 @@ namespace mioc {
 #ifndef PINF_MC_SPLIT
 #define PINF_MC_SPLIT 1  // k_pinf_recur_mc, 8 lanes per row: classes >= 8 (rows below the segment) off the step chain
 #endif
+#ifndef PINF_MC_HELPERS
+#define PINF_MC_HELPERS 1  // k_pinf_recur_mcw: the off-chain minima of a chunk by three helper waves (A/B builds: 0)
+#endif
 #ifndef PINF_RECUR_XR
 #define PINF_RECUR_XR 1     // C4's B = 256: eight waves and the extra row split by classes (k_pinf_recur_xr)
 #endif
@@ -450,13 +453,23 @@ __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P
           r1 = pvmin(r1, pv_dpp<0x4E>(r1));
         }
         double *Aout = A + (size_t)(i & 1) * AW;
-        if (G == 1 || h == 0) {
+#if defined(PINF_EXP_STORE16)
+        if constexpr (G == 1) {  // the row pair as one 16-byte store (c0 even, RP even: aligned)
           Aout[c0 + BWP - 1] = r0;
-          R[(size_t)i * RP + c0] = c0 <= B ? r0 : INFINITY;
-        }
-        if (G == 1 || h == 1) {
           Aout[c0 + BWP] = r1;
-          R[(size_t)i * RP + c0 + 1] = c0 + 1 <= B ? r1 : INFINITY;
+          *reinterpret_cast<double2 *>(R + (size_t)i * RP + c0) =
+              make_double2(c0 <= B ? r0 : INFINITY, c0 + 1 <= B ? r1 : INFINITY);
+        } else
+#endif
+        {
+          if (G == 1 || h == 0) {
+            Aout[c0 + BWP - 1] = r0;
+            R[(size_t)i * RP + c0] = c0 <= B ? r0 : INFINITY;
+          }
+          if (G == 1 || h == 1) {
+            Aout[c0 + BWP] = r1;
+            R[(size_t)i * RP + c0 + 1] = c0 + 1 <= B ? r1 : INFINITY;
+          }
         }
       }
       PI_T(t2);
@@ -769,12 +782,16 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
         kl(kcn, kfn, i - 1);
         const double P = offc(kf, wf);
         double rv = pvmin(kc[0] + w1, kc[1] + w0);
+#if !defined(PINF_EXP_NODPP)
         rv = pvmin(rv, pv_dpp<0xB1>(rv));
         rv = pvmin(rv, pv_dpp<0x4E>(rv));
+#endif
         rv = pvmin(rv, P);
         slot(i)[u] = rv;
+#if !defined(PINF_EXP_NOSTORE)
         __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(rv), (unsigned)__double2hiint(rv)},
                                               Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
+#endif
       };
       double kca[2], kcb[2], kfa[CO], kfb[CO], wa[CO], wb[CO];
       kl(kca, kfa, hi);
@@ -795,6 +812,162 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
     // this chunk's rows have landed: publish its last step for the segments above
     vm_drain();
     if (lane == 0) __hip_atomic_store(done + q, nt - 1 - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hi = nhi;
+    lo = nlo;
+  }
+}
+
+// k_pinf_recur_mc with helper waves (8 lanes per row, 8-row segments, classes 16 or 32): the chain of a step only
+// involves the classes b < 8 -- rows of the segment itself, which the previous step wrote; every class b >= 8 reads a
+// row below the segment, staged for the whole chunk before the chunk starts.  So the off-chain minima
+//   P_i[c] = min_{8 <= b < BWP} fl(Kmin_i[b] + R_{i+1}[c - b])
+// of a whole chunk are computed ahead, by three helper waves, while wave 0 runs the previous chunk's chain; they also
+// wait for the segments below, copy the chunk's rows below (LDS-DMA, sc1) and its class rows.  Wave 0's step is then
+// the on-chain part only (lane h of a row group: classes 2(h&3), 2(h&3)+1, two DPP steps) and one min with P_i from
+// the LDS.  min is exact, so R is bit-identical to k_pinf_recur's.  A workgroup barrier per chunk; a failed wait (spin
+// limit) stops every wave after it.
+template <int BWP>
+__global__ __launch_bounds__(256) void k_pinf_recur_mcw(ProblemDev P, PinfDev D, int nseg, int32_t *flags,
+                                                       unsigned spin_limit) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  __shared__ int s_stop, s_hsync;
+  constexpr int RPS = 8, AS = 32 + RPS, CH = PINF_MC_CHUNK, NS = 2 * CH;
+  static_assert(BWP == 16 || BWP == 32, "k_pinf_recur_mcw: classes 16 or 32");
+  const int RP = P.RP, B = P.B, nt = P.nt, K = P.K;
+  const int k = (int)blockIdx.x / nseg, q = (int)blockIdx.x - k * nseg;
+  const int tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63;
+  double *A = sm, *Kbuf = sm + (size_t)NS * AS, *Pbuf = Kbuf + (size_t)2 * CH * BWP;  // Pbuf: [2][CH][RPS]
+  const double *kmin = D.kmin + (size_t)k * nt * BWP;
+  double *R = D.R + (size_t)k * nt * RP;
+  int32_t *done = flags + (size_t)k * nseg, *err = flags + (size_t)K * nseg;
+  const __amdgpu_buffer_rsrc_t Rr = __builtin_amdgcn_make_buffer_rsrc(R, 0, (int)((size_t)nt * RP * 8), 0x00020000);
+  auto slot = [&](int s) { return A + (size_t)(s % NS) * AS; };
+  // terminal row R_{n-1}[c'] = Kmin_{n-1}[c'] (c' < BWP), the rows below included (a function of kmin: no hand-off)
+  for (int e = tid; e < NS * AS; e += 256) A[e] = INFINITY;
+  if (tid == 0) {
+    s_stop = 0;
+    s_hsync = 0;
+  }
+  lds_barrier();
+  for (int e = tid; e < AS; e += 256) {
+    const int cc = RPS * q - 32 + e;
+    slot(nt - 1)[e] = cc >= 0 && cc < BWP ? kmin[(size_t)(nt - 1) * BWP + cc] : INFINITY;
+  }
+  if (tid < RPS) {
+    const int c = RPS * q + tid;
+    R[(size_t)(nt - 1) * RP + c] = c <= B && c < BWP ? kmin[(size_t)(nt - 1) * BWP + c] : INFINITY;
+  }
+  lds_barrier();
+  if (nt < 2) return;
+  // ---- the helpers (waves 1..3, ht = 0..191): chunk [clo, chi] into buffer b ----------------------------------------
+  int hgen = 0;  // helper-only syncs so far
+  auto hsync = [&]() {  // the three helper waves (an LDS counter: wave 0 does not take part)
+    ++hgen;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(&s_hsync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(&s_hsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 3 * hgen)
+      __builtin_amdgcn_s_sleep(1);
+  };
+  auto prepare = [&](int clo, int chi, int b) {
+    const int ht = tid - 64;
+    glds_copy_asm(kmin + (size_t)clo * BWP, Kbuf + (size_t)b * CH * BWP, (chi - clo + 1) * BWP * 8, ht, 192);
+    const int s1 = min(chi + 1, nt - 2);  // the rows below of steps clo+1 .. chi+1 (step nt-1's are the terminal's)
+    bool ok = true;
+    if (q > 0 && clo + 1 <= s1) {
+      // the segments within 32 rows below (q-1 .. q-4) have published step clo+1 (token nt-2-clo)
+      const int need = nt - 1 - (clo + 1);
+      for (int d = 1; d * RPS <= 32 && q - d >= 0 && ok; ++d) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(done + q - d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) s_stop = 1;
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      if (ok) {  // lane l of a helper wave moves rows RPS·q-32+2l, +1 of one step (16 bytes, LDS-DMA, sc1)
+        const int row = RPS * q - 32 + 2 * lane;
+        for (int s = clo + 1 + (w - 1); s <= s1; s += 3) {
+          if (lane < 16 && row >= 0) {
+            const void *g = pi_uniform(R + (size_t)s * RP);
+            const unsigned m0 =
+                __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)slot(s)));
+            const unsigned voff = 8u * (unsigned)row;
+            unsigned keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 sc1\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(voff), "s"(g), "s"(m0)
+                         : "memory");
+          }
+        }
+      }
+    }
+    vm_drain();  // this wave's copies are in the LDS
+    hsync();     // ... and every helper wave's
+    // P_i[c] for every step of the chunk and row of the segment: (step, row) pairs over the 192 helper lanes
+    const double *Kc = Kbuf + (size_t)b * CH * BWP;
+    double *Pc = Pbuf + (size_t)b * CH * RPS;
+    for (int e = ht; e < (chi - clo + 1) * RPS; e += 192) {
+      const int ii = e / RPS, r = e - ii * RPS, i = clo + ii;
+      const double *kr = Kc + (size_t)ii * BWP;
+      const double *Ab = slot(i + 1) + r + 32;  // R_{i+1}[c - b] = Ab[-b]
+      double m[4];
+#pragma unroll
+      for (int bb = 8; bb < BWP; ++bb) {
+        const double cand = kr[bb] + Ab[-bb];
+        m[bb & 3] = bb < 12 ? cand : pvmin(m[bb & 3], cand);
+      }
+      Pc[e] = pvmin(pvmin(m[0], m[1]), pvmin(m[2], m[3]));
+    }
+  };
+  int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
+  if (w > 0) prepare(lo, hi, 0);
+  lds_barrier();
+  bool stop = s_stop != 0;
+  // ---- wave 0's lanes: row r = lane / 8 of the segment, h = lane % 8; classes 2(h&3), 2(h&3)+1 ---------------------
+  const int r = lane >> 3, h = lane & 7, c = RPS * q + r, u = r + 32, b0 = 2 * (h & 3);
+  for (int qq = 0; hi >= 0 && !stop; ++qq) {
+    const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
+    if (w == 0) {
+      const double *Kc = Kbuf + (size_t)(qq & 1) * CH * BWP;
+      const double *Pc = Pbuf + (size_t)(qq & 1) * CH * RPS;
+      // step i's on-chain class values and P (read one step ahead: not on the chain)
+      auto ld = [&](double (&kc)[2], double &pv, int i) {
+        const double2 y = *reinterpret_cast<const double2 *>(Kc + (size_t)(i - lo) * BWP + b0);
+        kc[0] = y.x;
+        kc[1] = y.y;
+        pv = Pc[(i - lo) * RPS + r];
+      };
+      auto st = [&](int i, const double (&kc)[2], double pv, double (&kcn)[2], double &pvn) {
+        asm volatile("" ::: "memory");
+        const double *Ain = slot(i + 1) + u - b0 - 1;  // R_{i+1}[c - b0 - 1], R_{i+1}[c - b0]
+        const double w0 = Ain[0], w1 = Ain[1];
+        if (i > lo) ld(kcn, pvn, i - 1);
+        double rv = pvmin(kc[0] + w1, kc[1] + w0);
+        rv = pvmin(rv, pv_dpp<0xB1>(rv));
+        rv = pvmin(rv, pv_dpp<0x4E>(rv));
+        rv = pvmin(rv, pv);
+        slot(i)[u] = rv;
+        __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(rv), (unsigned)__double2hiint(rv)},
+                                              Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
+      };
+      double ka[2], kb[2], pa, pb;
+      ld(ka, pa, hi);
+      for (int i = hi; i >= lo; i -= 2) {
+        st(i, ka, pa, kb, pb);
+        if (i - 1 >= lo) st(i - 1, kb, pb, ka, pa);
+      }
+      // this chunk's rows have landed: publish its last step for the segments above
+      vm_drain();
+      if (lane == 0) __hip_atomic_store(done + q, nt - 1 - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (nhi >= 0) {
+      prepare(nlo, nhi, (qq + 1) & 1);
+    }
+    lds_barrier();
+    stop = s_stop != 0;
     hi = nhi;
     lo = nlo;
   }
@@ -838,15 +1011,24 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
     if (PINF_RECUR_MC && flags && segmented && D.BWP >= 2 * LPR && D.BWP <= 32 && nseg >= 3 && P.K * nseg <= ncu &&
         RPS * nseg <= P.RP && (size_t)P.nt * P.RP * 8 < (1ull << 31)) {
       constexpr int CH = PINF_MC_CHUNK;
-      const size_t lds = (size_t)(2 * CH * (32 + RPS) + 2 * CH * D.BWP) * sizeof(double);
-      const bool ok = D.BWP == 8    ? launch_pinf_mc<8, LPR>(s, P, D, nseg, flags, spin_limit, lds)
-                      : D.BWP == 16 ? launch_pinf_mc<16, LPR>(s, P, D, nseg, flags, spin_limit, lds)
-                                    : launch_pinf_mc<32, LPR>(s, P, D, nseg, flags, spin_limit, lds);
+      const bool helpers = PINF_MC_HELPERS && LPR == 8 && (D.BWP == 16 || D.BWP == 32);
+      const size_t lds = (size_t)(2 * CH * (32 + RPS) + 2 * CH * D.BWP + (helpers ? 2 * CH * RPS : 0)) * sizeof(double);
+      bool ok = true;
+      if (helpers) {
+        if (D.BWP == 16)
+          hipLaunchKernelGGL((k_pinf_recur_mcw<16>), dim3(P.K * nseg), dim3(256), lds, s, P, D, nseg, flags, spin_limit);
+        else
+          hipLaunchKernelGGL((k_pinf_recur_mcw<32>), dim3(P.K * nseg), dim3(256), lds, s, P, D, nseg, flags, spin_limit);
+      } else {
+        ok = D.BWP == 8    ? launch_pinf_mc<8, LPR>(s, P, D, nseg, flags, spin_limit, lds)
+             : D.BWP == 16 ? launch_pinf_mc<16, LPR>(s, P, D, nseg, flags, spin_limit, lds)
+                           : launch_pinf_mc<32, LPR>(s, P, D, nseg, flags, spin_limit, lds);
+      }
       if (ok) {
         // rows above B (the top segment's finite values, and the rows no segment computes): +Inf, after the launch
         if (P.B + 1 < P.RP) hipLaunchKernelGGL(k_pinf_rfill, dim3(64, P.K), dim3(256), 0, s, P, D, P.B + 1);
         *segmented = true;
-        if (variant) *variant = "k_pinf_recur_mc";
+        if (variant) *variant = helpers ? "k_pinf_recur_mcw" : "k_pinf_recur_mc";
         return hipGetLastError();
       }
     }

@@ -179,7 +179,7 @@ def test_c4_pinf_nt200_fixture(walk, spin):
     ctx.synchronize()
     # the row-segment kernel took this DP; after an abandoned launch the stats name the one-workgroup redo (C4's
     # B = 256: k_pinf_recur_xr)
-    assert ctx.kernel_stats(0)[2] == ("k_pinf_recur_xr" if spin else "k_pinf_recur_mc")
+    assert ctx.kernel_stats(0)[2] == ("k_pinf_recur_xr" if spin else "k_pinf_recur_mcw")
     for q, Bp in enumerate(z["budgets"]):
         u, ps, _ = ctx.backtrack(int(Bp))
         assert np.array_equal(u, z["u"][q]), f"B'={Bp}"
