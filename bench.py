@@ -301,13 +301,15 @@ def pmc_traffic(kernel, cfg=None, K=None):
         except (OSError, ValueError, KeyError):
             continue
         # entries recorded from a single-config pass are qualified "kernel@CFG"; plain names come from the default
-        # bench passes, where each kernel belongs to one line (C4 headline / its p=Inf variant / the C5 batch)
-        # a batch size qualifier first ("k_fsep2@C5x128": the grid-size split of scripts/pmc_traffic.py --qualify),
-        # then the config, then (C4) a launch variant of the kernel ("k_pinf_recur_xr" for the event "k_pinf_recur")
-        e = (ks.get(f"{kernel}@{cfg}x{K}") if K else None) or ks.get(f"{kernel}@{cfg}") or \
-            (ks.get(kernel) if cfg in (None, "C4", "C5") else None)
-        if not e and cfg in (None, "C4"):
-            e = next((v for n, v in sorted(ks.items()) if n.startswith(kernel + "_") and "@" not in n), None)
+        # bench passes, where each kernel belongs to one line (C4 headline / its p=Inf variant / the C5 batch).
+        # A batch size qualifier first ("k_fsep2@C5x128": the grid-size split of scripts/pmc_traffic.py --qualify);
+        # an unqualified "@CFG" entry is a batch pass's, so a one-subproblem line (K = 1) never takes it.  `kernel` is
+        # the launched variant (kernel_stats names it), so no prefix matching.
+        e = ks.get(f"{kernel}@{cfg}x{K}") if K else None
+        if not e and (not K or K > 1):
+            e = ks.get(f"{kernel}@{cfg}")
+        if not e and cfg in (None, "C4", "C5"):
+            e = ks.get(kernel)
         if e and "hbm_bytes_per_launch" in e:
             found.append((int(re.search(r"round(\d+)_", os.path.basename(f)).group(1)), e["hbm_bytes_per_launch"], f))
     if not found:
