@@ -453,23 +453,13 @@ __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P
           r1 = pvmin(r1, pv_dpp<0x4E>(r1));
         }
         double *Aout = A + (size_t)(i & 1) * AW;
-#if defined(PINF_EXP_STORE16)
-        if constexpr (G == 1) {  // the row pair as one 16-byte store (c0 even, RP even: aligned)
+        if (G == 1 || h == 0) {
           Aout[c0 + BWP - 1] = r0;
+          R[(size_t)i * RP + c0] = c0 <= B ? r0 : INFINITY;
+        }
+        if (G == 1 || h == 1) {
           Aout[c0 + BWP] = r1;
-          *reinterpret_cast<double2 *>(R + (size_t)i * RP + c0) =
-              make_double2(c0 <= B ? r0 : INFINITY, c0 + 1 <= B ? r1 : INFINITY);
-        } else
-#endif
-        {
-          if (G == 1 || h == 0) {
-            Aout[c0 + BWP - 1] = r0;
-            R[(size_t)i * RP + c0] = c0 <= B ? r0 : INFINITY;
-          }
-          if (G == 1 || h == 1) {
-            Aout[c0 + BWP] = r1;
-            R[(size_t)i * RP + c0 + 1] = c0 + 1 <= B ? r1 : INFINITY;
-          }
+          R[(size_t)i * RP + c0 + 1] = c0 + 1 <= B ? r1 : INFINITY;
         }
       }
       PI_T(t2);
@@ -782,16 +772,12 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
         kl(kcn, kfn, i - 1);
         const double P = offc(kf, wf);
         double rv = pvmin(kc[0] + w1, kc[1] + w0);
-#if !defined(PINF_EXP_NODPP)
         rv = pvmin(rv, pv_dpp<0xB1>(rv));
         rv = pvmin(rv, pv_dpp<0x4E>(rv));
-#endif
         rv = pvmin(rv, P);
         slot(i)[u] = rv;
-#if !defined(PINF_EXP_NOSTORE)
         __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(rv), (unsigned)__double2hiint(rv)},
                                               Rr, (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
-#endif
       };
       double kca[2], kcb[2], kfa[CO], kfb[CO], wa[CO], wb[CO];
       kl(kca, kfa, hi);
