@@ -80,8 +80,9 @@ extern "C" {
 #define MIOC_OPT_PINF_WALK 8 /* p=Inf backtrack: 0 (default) the segmented walk -- one subproblem's path spread
                                 over many workgroups -- for batches of at most 64 subproblems with >= 512 steps,
                                 else one serial walk per subproblem; 1: segmented walk forced; -1: serial walk */
-#define MIOC_OPT_SDT_PAIR 9 /* persistent separable transform on 8^4 grids: 1: two workgroups per budget row
-                               (two row items in flight per CU; K·B <= CUs), 0 (default): one workgroup per row */
+#define MIOC_OPT_SDT_PAIR 9 /* persistent separable transform on 8^4 grids: two workgroups per budget row (two row
+                               items in flight per CU; K·B <= CUs) of 256 threads (1) or 512 threads (2); 0
+                               (default): one workgroup per row */
 
 typedef struct mioc_ctx mioc_ctx;
 

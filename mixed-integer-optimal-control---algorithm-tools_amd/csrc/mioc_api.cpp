@@ -283,6 +283,7 @@ int run_bellman(mioc_ctx *ctx) {
     const size_t run_lds = sdt_lds_bytes(ctx->pyr);
     int nwg = 0;
     bool persist = false, pair = false;
+    const int pair_t = ctx->opt_sdt_pair == 2 ? 512 : 256;  // k_sdt_pair's workgroup size
     // (B + 1)·L·8 < 2^31: the persistent kernel addresses a staging block with 32-bit buffer offsets
     // ... and every b̃ within the kernel's dependency window (7 per dimension: u_old on the level grid); a u_old
     // off the grid reaches rows further back than the window waits for, so those problems take per-step launches
@@ -292,7 +293,7 @@ int run_bellman(mioc_ctx *ctx) {
       HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
       // 8^4 grids with every budget row on its own CU: two workgroups per row (k_sdt_pair, mioc_sdt2.hip); else one
       // workgroup per CU over contiguous row chunks (k_sdt_run)
-      pair = ctx->opt_sdt_pair && sdt_pair_supported(ctx->pyr, (int)K, ctx->B, ncu, sdt_pair_blocks_per_cu());
+      pair = ctx->opt_sdt_pair && sdt_pair_supported(ctx->pyr, (int)K, ctx->B, ncu, sdt_pair_blocks_per_cu(pair_t));
       const int bpc = std::min(sdt_run_blocks_per_cu(ctx->pyr, run_lds), 1);  // one row workgroup per CU
       const size_t slots = (size_t)ncu * (size_t)std::max(bpc, 0);
       const size_t per_k = std::min<size_t>((size_t)ctx->B, K ? slots / K : 0);  // workgroups per subproblem
@@ -333,9 +334,12 @@ int run_bellman(mioc_ctx *ctx) {
     const bool seams = persist && !pair && sdt_seam_lists(ctx->pyr);
     if (!rc && seams) rc = grow(ctx, &ctx->d_strad, &ctx->strad_cap, K * nt * 8 * 32 * sizeof(uint16_t), "seam lists");
     if (!rc && pair) rc = grow(ctx, &ctx->d_pack, &ctx->pack_cap, K * nt * (L / 2) * sizeof(uint32_t), "packed orders");
-    if (!rc && pair) rc = grow(ctx, &ctx->d_pseam, &ctx->pseam_cap, K * nt * 128 * sizeof(uint32_t), "packed seams");
     if (!rc && pair)
-      rc = grow(ctx, &ctx->d_phead, &ctx->phead_cap, K * (size_t)(ctx->B + 1) * nt * 4 * sizeof(double), "row head parts");
+      rc = grow(ctx, &ctx->d_pseam, &ctx->pseam_cap, K * nt * sdt_pair_seam_words(pair_t) * sizeof(uint32_t),
+                "packed seams");
+    if (!rc && pair)
+      rc = grow(ctx, &ctx->d_phead, &ctx->phead_cap, K * (size_t)(ctx->B + 1) * nt * (pair_t / 64) * sizeof(double),
+                "row head parts");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
     double *term = persist ? ctx->d_stage + ((nt - 1) % nbuf) * s_stride : st[(nt - 1) & 1];
@@ -346,11 +350,13 @@ int run_bellman(mioc_ctx *ctx) {
       // the whole DP as one persistent launch: rows handed between resident workgroups by flags
       HIP_TRY(ctx, launch_sdt_prep(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_chain, ctx->d_stage, ks,
                                    (size_t)nbuf * s_stride, (uint16_t *)ctx->d_U, uu_stride_k));
-      if (pair) HIP_TRY(ctx, launch_sdt_pack(ctx->stream, P, ctx->d_perm, ctx->d_pack, ctx->d_pseam, ctx->d_counters));
+      if (pair)
+        HIP_TRY(ctx, launch_sdt_pack(ctx->stream, P, ctx->d_perm, ctx->d_pack, ctx->d_pseam, ctx->d_counters, pair_t));
       HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, runflag_bytes, ctx->stream));
       // head values not yet written: all-ones (a NaN no DP value takes)
       if (pair)
-        HIP_TRY(ctx, hipMemsetAsync(ctx->d_phead, 0xFF, K * (size_t)(ctx->B + 1) * nt * 4 * sizeof(double), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_phead, 0xFF, K * (size_t)(ctx->B + 1) * nt * (pair_t / 64) * sizeof(double),
+                                    ctx->stream));
       ctx->last_sdt_kernel = pair ? "k_sdt_pair" : "k_sdt_run";
       ev_begin(ctx, 0, ctx->last_sdt_kernel);
       // (the grid is nwg <= CUs x resident workgroups per CU by construction above; a wait that never ends anyway --
@@ -358,7 +364,7 @@ int run_bellman(mioc_ctx *ctx) {
       if (pair)
         HIP_TRY(ctx, launch_sdt_pair(ctx->stream, P, Lv, ctx->pyr, ctx->d_pack, ctx->d_pseam, ctx->d_stage, ks, nbuf,
                                      (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags,
-                                     ctx->d_phead, ctx->spin_limit));
+                                     ctx->d_phead, ctx->spin_limit, pair_t));
       else
         HIP_TRY(ctx, launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_same2, ctx->d_strad, ctx->d_stage,
                                     ks, nbuf, (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags, nwg,
@@ -714,7 +720,8 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
     return MIOC_OK;
   }
   if (option == MIOC_OPT_SDT_PAIR) {
-    ctx->opt_sdt_pair = value != 0;
+    if (value < 0 || value > 2) return fail(ctx, MIOC_EINVAL, "SDT pair option must be 0, 1 or 2");
+    ctx->opt_sdt_pair = (int)value;
     return MIOC_OK;
   }
   if (option == MIOC_OPT_PINF_WALK) {

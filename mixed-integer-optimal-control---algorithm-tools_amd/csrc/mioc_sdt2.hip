@@ -52,21 +52,34 @@
 namespace mioc {
 namespace {
 
-constexpr int S2_L = 4096, S2_T = 256, S2_NW = 4, S2_Q = 8;  // levels, threads, waves, position pairs per lane
-constexpr int S2_SEAMS = 32;                                   // seam words per wave (<= 28 seams in a sphere order)
-constexpr int S2_PACK = S2_L / 2;                              // pair words per step
-constexpr int S2_NST = 10;  // vector-memory instructions of an item's stores (the counted wait at the next item's start)
+constexpr int S2_L = 4096;         // levels
+constexpr int S2_SEAMS = 32;        // seam words per wave (<= 28 seams in a sphere order)
+constexpr int S2_PACK = S2_L / 2;   // pair words per step
 
 // LDS (dynamic): Ψ by rank | transform values (swizzled; the outputs after the last pass) | U row | scan list |
 // per wave df(:, i..i+1), u_old(:, i..i+2)
 constexpr size_t S2_PSI = 0, S2_DTV = S2_PSI + S2_L * 8, S2_UU = S2_DTV + S2_L * 8, S2_LIST = S2_UU + S2_L * 2,
-                 S2_DFUO = S2_LIST + SD_LCAP * 2, S2_DFUO_WAVE = 256, S2_LDS = S2_DFUO + S2_NW * S2_DFUO_WAVE;
+                 S2_DFUO = S2_LIST + SD_LCAP * 2, S2_DFUO_WAVE = 256;
 
+// the workgroup shape: T = 256 threads (16 values per lane, two last-pass lines, 4 waves: two workgroups per CU at
+// 256 VGPRs) or 512 (8 values per lane, one line, 8 waves: two workgroups per CU -- four waves per SIMD -- at 128)
+template <int T>
+struct S2C {
+  static constexpr int NW = T / 64;                // waves
+  static constexpr int Q = S2_L / 2 / T;           // position pairs per lane
+  static constexpr int LN = S2_L / 8 / T;          // last-pass lines per lane
+  static constexpr int UB = S2_L * 2 / T / 16;     // 16-byte stores per lane of the U row
+  static constexpr int NST = Q + UB;               // an item's stores (the counted wait at the next item's start)
+  static constexpr size_t LDS = S2_DFUO + NW * S2_DFUO_WAVE;
+  static_assert(Q % 4 == 0 && LN >= 1 && UB >= 1, "k_sdt_pair shape");
+};
+
+template <int NW>
 struct S2Shared {
-  double redv[SD_COOP * S2_NW];
-  int redj[SD_COOP * S2_NW];
-  double rmn[S2_NW], rmx[S2_NW], pmin[S2_NW];  // pmin: this item's head value (*) over each wave's values
-  int rnv[S2_NW];
+  double redv[SD_COOP * NW];
+  int redj[SD_COOP * NW];
+  double rmn[NW], rmx[NW], pmin[NW];  // pmin: this item's head value (*) over each wave's values
+  int rnv[NW];
   int nlist;
   int stop;  // a dependency wait timed out: the launch is abandoned
   int nsp;   // sparse rows: the finite sources (rank, Ψ)
@@ -81,25 +94,28 @@ __device__ __forceinline__ int s2_ra(uint32_t w) { return (int)(w & 0xFFFu); }
 __device__ __forceinline__ int s2_rb(uint32_t w) { return (int)((w >> 12) & 0xFFFu); }
 __device__ __forceinline__ int s2_bt(uint32_t w) { return (int)((w >> 24) & 31u); }
 __device__ __forceinline__ bool s2_strad(uint32_t w) { return (w >> 29) & 1u; }
-// the position of in-wave offset o of wave w: o = 128q + 2l + h <-> position 2(64w + l + 256q) + h
-__device__ __forceinline__ int s2_seam_pos(int w, int o) { return 512 * (o >> 7) + 128 * w + (o & 127); }
+// the position of in-wave offset o of wave w: o = 128q + 2l + h <-> position 2(64w + l + T·q) + h
+template <int T>
+__device__ __forceinline__ int s2_seam_pos(int w, int o) { return 2 * T * (o >> 7) + 128 * w + (o & 127); }
 
-// One step's sphere order (perm: rank | b̃ << 16 by position, k_pyr_order) packed for k_sdt_pair: thread t's eight pair
-// words contiguous (two 16-byte loads), and per wave the second elements of the pairs that straddle a seam.
-__global__ __launch_bounds__(256) void k_sdt2_pack(const uint32_t *__restrict__ perm_all, int nt,
+// One step's sphere order (perm: rank | b̃ << 16 by position, k_pyr_order) packed for k_sdt_pair: thread t's Q pair
+// words contiguous (16-byte loads), and per wave the second elements of the pairs that straddle a seam.
+template <int T>
+__global__ __launch_bounds__(T) void k_sdt2_pack(const uint32_t *__restrict__ perm_all, int nt,
                                                    uint32_t *__restrict__ pack_all, uint32_t *__restrict__ seam_all,
                                                    int32_t *__restrict__ counters) {
   const int i = (int)blockIdx.x, k = (int)blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  constexpr int NW = S2C<T>::NW, Q = S2C<T>::Q;
   const uint32_t *perm = perm_all + ((size_t)k * nt + i) * S2_L;
-  __shared__ int cnt[S2_NW];
-  __shared__ uint32_t sl[S2_NW * S2_SEAMS];
-  if (t < S2_NW) cnt[t] = 0;
-  for (int e = t; e < S2_NW * S2_SEAMS; e += S2_T) sl[e] = 0xFFFFFFFFu;
+  __shared__ int cnt[NW];
+  __shared__ uint32_t sl[NW * S2_SEAMS];
+  if (t < NW) cnt[t] = 0;
+  for (int e = t; e < NW * S2_SEAMS; e += T) sl[e] = 0xFFFFFFFFu;
   __syncthreads();
-  uint32_t wd[S2_Q];
+  uint32_t wd[Q];
 #pragma unroll
-  for (int q = 0; q < S2_Q; ++q) {
-    const int u = t + S2_T * q;
+  for (int q = 0; q < Q; ++q) {
+    const int u = t + T * q;
     const uint32_t ea = perm[2 * u], eb = perm[2 * u + 1];
     const uint32_t ba = min(ea >> 16, 31u), bb = min(eb >> 16, 31u);
     const bool st = ba != bb;
@@ -112,65 +128,75 @@ __global__ __launch_bounds__(256) void k_sdt2_pack(const uint32_t *__restrict__ 
         atomicAdd(&counters[3], 1);  // the list cannot hold this seam: a loud internal-consistency failure
     }
   }
-  uint4 *dst = reinterpret_cast<uint4 *>(pack_all + ((size_t)k * nt + i) * S2_PACK + (size_t)t * S2_Q);
-  dst[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-  dst[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+  uint4 *dst = reinterpret_cast<uint4 *>(pack_all + ((size_t)k * nt + i) * S2_PACK + (size_t)t * Q);
+#pragma unroll
+  for (int q4 = 0; q4 < Q / 4; ++q4) dst[q4] = make_uint4(wd[4 * q4], wd[4 * q4 + 1], wd[4 * q4 + 2], wd[4 * q4 + 3]);
   __syncthreads();
-  if (t < S2_NW * S2_SEAMS) seam_all[((size_t)k * nt + i) * (S2_NW * S2_SEAMS) + t] = sl[t];
+  for (int e = t; e < NW * S2_SEAMS; e += T) seam_all[((size_t)k * nt + i) * (NW * S2_SEAMS) + e] = sl[e];
 }
 
 // this lane's pair words and seam word of one step (registers)
+template <int Q>
 struct S2Ent {
-  uint32_t w[S2_Q];
+  uint32_t w[Q];
   uint32_t seam;
 };
 // the loads of one step's values at this lane's positions (registers, in flight across an item)
+template <int Q>
 struct S2Raw {
-  sd_u32x4 a[S2_Q];
+  sd_u32x4 a[Q];
   sd_u32x2 sv;
   unsigned mask;  // per pair q: bit 2q the first element has no value here (row below 0, or the head), 2q+1 the second
   int srow;       // the seam element's source row (< 0: none / below row 0)
 };
 
-__device__ __forceinline__ void s2_ent_issue(S2Ent &e, const uint32_t *pack, const uint32_t *seam) {
+template <int Q>
+__device__ __forceinline__ void s2_ent_issue(S2Ent<Q> &e, const uint32_t *pack, const uint32_t *seam) {
   const int t = threadIdx.x;
-  const uint4 *src = reinterpret_cast<const uint4 *>(pack + (size_t)t * S2_Q);
-  const uint4 x = src[0], y = src[1];
-  e.w[0] = x.x, e.w[1] = x.y, e.w[2] = x.z, e.w[3] = x.w;
-  e.w[4] = y.x, e.w[5] = y.y, e.w[6] = y.z, e.w[7] = y.w;
+  const uint4 *src = reinterpret_cast<const uint4 *>(pack + (size_t)t * Q);
+#pragma unroll
+  for (int q4 = 0; q4 < Q / 4; ++q4) {
+    const uint4 x = src[q4];
+    e.w[4 * q4] = x.x, e.w[4 * q4 + 1] = x.y, e.w[4 * q4 + 2] = x.z, e.w[4 * q4 + 3] = x.w;
+  }
   e.seam = seam[(t >> 6) * S2_SEAMS + (t & 31)];  // lanes 32..63 repeat lanes 0..31 (masked in s2_issue)
 }
 
 // The loads of one step's values for source row cp: position pair q from row cp - b̃_a (one 16-byte `sc1` load), the
 // straddling second elements by the wave's seam list (one 8-byte load per lane); out-of-range offsets (dropped by the
 // hardware) for rows below 0, for the head (b̃ = 0: the caller supplies it) and when `live` is false.  Always
-// exactly S2_Q + 1 vector-memory instructions.
-__device__ __forceinline__ void s2_issue(S2Raw &r, __amdgpu_buffer_rsrc_t rs, const S2Ent &e, int cp, unsigned boff,
-                                         unsigned r0, unsigned rowb, bool live) {
+// exactly Q + 1 vector-memory instructions.
+template <int T, int Q>
+__device__ __forceinline__ void s2_issue(S2Raw<Q> &r, __amdgpu_buffer_rsrc_t rs, const S2Ent<Q> &e, int cp,
+                                         unsigned boff, unsigned r0, unsigned rowb, bool live) {
   constexpr unsigned OOB = 0xFFFFFFF0u;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   unsigned mask = 0;
 #pragma unroll
-  for (int q = 0; q < S2_Q; ++q) {
-    const int p2 = 2 * (t + S2_T * q);
+  for (int q = 0; q < Q; ++q) {
+    const int p2 = 2 * (t + T * q);
     const int ra = cp - s2_bt(e.w[q]);
     const bool bad = !live || ra < 0 || ra == cp;  // (ra == cp: the head, position 0 -- its pair always straddles)
-    const unsigned oa = bad ? OOB : ra >= 1 ? boff + (unsigned)ra * rowb + (unsigned)p2 * 8u : r0 + (unsigned)p2 * 8u;
+    unsigned oa = bad ? OOB : ra >= 1 ? boff + (unsigned)ra * rowb + (unsigned)p2 * 8u : r0 + (unsigned)p2 * 8u;
+    // (the offset as an opaque value: otherwise the select became a branch with a load on each side, which the
+    // compiler's wait counts then treat as possibly not issued -- later waits on older loads became waits on these)
+    asm volatile("" : "+v"(oa));
     r.a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, oa, 0, 16);
     mask |= ((unsigned)bad | (unsigned)(bad || s2_strad(e.w[q])) << 1) << (2 * q);
   }
   const uint32_t sw = lane < 32 ? e.seam : 0xFFFFFFFFu;
   const int srow = sw == 0xFFFFFFFFu || !live ? -1 : cp - (int)((sw >> 10) & 31u);
-  const int P = s2_seam_pos(w, (int)(sw & 1023u));
+  const int P = s2_seam_pos<T>(w, (int)(sw & 1023u));
   const unsigned os = srow < 0 ? OOB : srow >= 1 ? boff + (unsigned)srow * rowb + (unsigned)P * 8u : r0 + (unsigned)P * 8u;
   r.sv = __builtin_amdgcn_raw_buffer_load_b64(rs, os, 0, 16);
   r.mask = mask;
   r.srow = srow;
 }
-// the sixteen values (+Inf where this lane has none) and the seam element (+Inf if none)
-__device__ __forceinline__ void s2_take(double (&v)[2 * S2_Q], double &xs, const S2Raw &r) {
+// the 2Q values (+Inf where this lane has none) and the seam element (+Inf if none)
+template <int Q>
+__device__ __forceinline__ void s2_take(double (&v)[2 * Q], double &xs, const S2Raw<Q> &r) {
 #pragma unroll
-  for (int q = 0; q < S2_Q; ++q) {
+  for (int q = 0; q < Q; ++q) {
     const unsigned m = r.mask >> (2 * q);
     v[2 * q] = (m & 1) ? INFINITY : __hiloint2double((int)r.a[q].y, (int)r.a[q].x);
     v[2 * q + 1] = (m & 2) ? INFINITY : __hiloint2double((int)r.a[q].w, (int)r.a[q].z);
@@ -183,7 +209,9 @@ __device__ __forceinline__ void s2_take(double (&v)[2 * S2_Q], double &xs, const
 // vector-memory instruction per wave.  s <= nt - 2; u_old(:, nt) does not exist: those lanes read u_old(:, nt - 1)
 // (the caller never uses u_old(:, s+2) at s = nt - 2)
 __device__ __forceinline__ void s2_dfuo_dma(const double *dfk, const double *uok, int s, int nt, unsigned char *sds) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // (the lane's offsets from an opaque thread index, recomputed per call: held across the loop they were spilled, and
+  // the reload's vmcnt(0) waited for the values A issued just before)
+  const int t = sd_tid(), wave = t >> 6, lane = t & 63;
   if (lane < 40) {
     const int e = min(4 * 2 * s + (lane - 16), 4 * 2 * nt - 1);  // dword index into u_old(:, :) (8 dwords per step)
     const char *g = lane < 16 ? (const char *)(dfk + (size_t)s * 4) + 4 * lane : (const char *)uok + 4 * (size_t)e;
@@ -214,12 +242,13 @@ __device__ __forceinline__ int s2_rank(const double *u, const int *lb) {
   return r;
 }
 
-// Exact scan of the listed targets (the reference loop, HelpFunctions.jl:60-77): as sd_scan (mioc_sdt.hip) for 256
+// Exact scan of the listed targets (the reference loop, HelpFunctions.jl:60-77): as sd_scan (mioc_sdt.hip) for T
 // threads; outputs at the swizzled positions
-template <bool COOP>
+template <int T, bool COOP>
 __device__ __forceinline__ void s2_scan(const uint16_t *list, int nl, const double *psi, const double *a,
                                         const int *base, double beta, uint16_t *UU, double *outs, double *redv,
                                         int *redj) {
+  constexpr int NW = T / 64;
   const int tid = sd_tid(), lane = tid & 63, w = tid >> 6;
   auto target = [&](int r, int *xl) {
     double t1 = 0.0;
@@ -253,8 +282,8 @@ __device__ __forceinline__ void s2_scan(const uint16_t *list, int nl, const doub
       double bv = INFINITY;
       int bj = -1;
 #pragma unroll
-      for (int s = 0; s < S2_L / S2_T; ++s) {  // sources tid + 256·s, ascending for this thread
-        const int j = tid + S2_T * s;
+      for (int s = 0; s < S2_L / T; ++s) {  // sources tid + T·s, ascending for this thread
+        const int j = tid + T * s;
         const double val = (t1 + beta * (double)sd_l1(sd_bytes((unsigned)j), pr)) + psi[j];
         if (val < bv) {
           bv = val;
@@ -263,17 +292,17 @@ __device__ __forceinline__ void s2_scan(const uint16_t *list, int nl, const doub
       }
       wave_min(bv, bj);
       if (lane == 0) {
-        redv[e * S2_NW + w] = bv;
-        redj[e * S2_NW + w] = bj;
+        redv[e * NW + w] = bv;
+        redj[e * NW + w] = bj;
       }
     }
     sd_bar();
     if (tid < nl) {
       double bv = INFINITY;
       int bj = -1;
-      for (int q = 0; q < S2_NW; ++q) {
-        const double ov = redv[tid * S2_NW + q];
-        const int oj = redj[tid * S2_NW + q];
+      for (int q = 0; q < NW; ++q) {
+        const double ov = redv[tid * NW + q];
+        const int oj = redj[tid * NW + q];
         if (better(ov, oj, bv, bj)) {
           bv = ov;
           bj = oj;
@@ -284,7 +313,7 @@ __device__ __forceinline__ void s2_scan(const uint16_t *list, int nl, const doub
       outs[sd_swz(r)] = bj >= 0 ? bv : INFINITY;
     }
   } else {
-    for (int e = w; e < nl; e += S2_NW) {
+    for (int e = w; e < nl; e += NW) {
       const int r = list ? (int)list[e] : e;
       if (!list && !__builtin_isnan(outs[sd_swz(r)])) continue;  // overflowed list: every NaN-marked rank
       int xl[4];
@@ -339,7 +368,8 @@ __shared__ unsigned long long s2_tlx_lds[32][4];
 // The persistent DP, two workgroups per budget row (see the file header).  Grid: 2·K·B workgroups of 256 threads,
 // two resident per CU (the host checks); flags: done [K][B+1][2], loaded [K][B+1][2], then the error word (zeroed);
 // heads [K][B+1][nt][4]: item (c', i)'s four waves' parts of the head minimum (*), all-ones (a NaN) until written.
-__global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv, PyrGeom G,
+template <int T>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T == 512 ? 4 : 2))) void k_sdt_pair(ProblemDev P, LevelsDev Lv, PyrGeom G,
                                                      const uint32_t *__restrict__ pack_all,
                                                      const uint32_t *__restrict__ seam_all, double *S_all,
                                                      size_t kstride, int NB, uint16_t *__restrict__ UU_all,
@@ -348,9 +378,11 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
                                                      const double *__restrict__ df_all,
                                                      const double *__restrict__ uo_all) {
   constexpr int M = 4, L = S2_L, Smax = 7 * M;
+  using C = S2C<T>;
+  constexpr int NW = C::NW, Q = C::Q, LN = C::LN, UB = C::UB;
   constexpr unsigned OOB = 0xFFFFFFF0u;
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
-  __shared__ S2Shared sh;
+  __shared__ S2Shared<NW> sh;
   double *psi = reinterpret_cast<double *>(sds + S2_PSI);
   double *dtv = reinterpret_cast<double *>(sds + S2_DTV);
   uint16_t *uu = reinterpret_cast<uint16_t *>(sds + S2_UU);
@@ -374,13 +406,13 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
   // the flag words and this row's head values through buffer resources: every wave issues the same stores, with
   // out-of-range offsets in all lanes but one (a fixed vector-memory sequence per wave, for the counted waits)
   const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(flags, 0, (int)(((size_t)P.K * R * 4 + 1) * 4), 0x00020000);
-  double *hk = heads + ((size_t)k * R + cp) * nt * 4;  // item (cp, s)'s wave parts at hk[4s .. 4s+3]
-  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(hk, 0, nt * 32, 0x00020000);
+  double *hk = heads + ((size_t)k * R + cp) * nt * NW;  // item (cp, s)'s wave parts at hk[NW·s .. NW·s + NW-1]
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(hk, 0, nt * NW * 8, 0x00020000);
   const unsigned rowb = (unsigned)L * 8u, bufb = (unsigned)R * rowb, r0b = (unsigned)NB * bufb;
   double *reg = S_all + (size_t)k * kstride;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(r0b + (unsigned)nt * rowb), 0x00020000);
   const uint32_t *pk = pack_all + (size_t)k * nt * S2_PACK;
-  const uint32_t *sk = seam_all + (size_t)k * nt * (S2_NW * S2_SEAMS);
+  const uint32_t *sk = seam_all + (size_t)k * nt * (NW * S2_SEAMS);
   const double *dfk = df_all + (size_t)k * nt * M, *uok = uo_all + (size_t)k * nt * M;
   auto tok = [&](int s) { return nt - 1 - s; };
   auto parof = [&](int s) { return (nt - 2 - s) & 1; };
@@ -440,16 +472,17 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
   // stores
   auto parts_load = [&](int ii, int ln) {
     const unsigned long long *src =
-        reinterpret_cast<const unsigned long long *>(hk + 4 * min(max(ii + 1, 0), nt - 1) + (ln & 3));
+        reinterpret_cast<const unsigned long long *>(hk + NW * min(max(ii + 1, 0), nt - 1) + (ln & (NW - 1)));
     return __longlong_as_double((long long)__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   };
-  double pp;  // the partner's head parts (lanes 0..3)
+  double pp;  // the partner's head parts (lanes 0 .. NW-1)
   double Hprev = INFINITY;  // Φ_{i+2}[cp, h(i+2)]: the previous item's head value (+Inf: the terminal row at cp >= 1)
   // ---- prologue: the first item's sphere orders and values; the next item's A orders ----------------------------
-  S2Ent eA, eO, eAn;  // orders of steps i+1 (values A), i (outputs), i-1 (the next item's A)
-  s2_ent_issue(eA, pk + (size_t)pstep(i0 + 1) * S2_PACK, sk + (size_t)pstep(i0 + 1) * (S2_NW * S2_SEAMS));
-  s2_ent_issue(eO, pk + (size_t)i0 * S2_PACK, sk + (size_t)i0 * (S2_NW * S2_SEAMS));
-  s2_ent_issue(eAn, pk + (size_t)pstep(i0 - 1) * S2_PACK, sk + (size_t)pstep(i0 - 1) * (S2_NW * S2_SEAMS));
+  // orders of steps i+1 (values A: the previous item's eAn across the back edge), i-1 (the next item's A: loaded at
+  // the item start) and i (outputs: loaded at go(), read at the item's end) -- eO and eAn are not held across the
+  // transform and the scan together (the 512-thread variant's register cap)
+  S2Ent<Q> eA;
+  s2_ent_issue(eA, pk + (size_t)pstep(i0 + 1) * S2_PACK, sk + (size_t)pstep(i0 + 1) * (NW * S2_SEAMS));
   s2_dfuo_dma(dfk, uok, i0, nt, sds);
   // the second workgroup's first item reads step nt-2, which the first workgroups of the rows below produce
   if (par == 1) {
@@ -466,8 +499,8 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
   pp = parts_load(i0, lane);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the orders are in
   sd_bar();
-  S2Raw rA;
-  s2_issue(rA, rs, eA, cp, boffs(i0 + 1), r0b + (unsigned)(i0 + 1) * rowb, rowb, sh.stop == 0);
+  S2Raw<Q> rA;
+  s2_issue<T>(rA, rs, eA, cp, boffs(i0 + 1), r0b + (unsigned)(i0 + 1) * rowb, rowb, sh.stop == 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   sd_bar();
   bool stop = sh.stop != 0;
@@ -485,9 +518,15 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     const bool has_next = i - 2 >= 0;
     // everything but the previous item's ten stores has landed: this item's values, orders, df / u_old, the partner's
     // head parts and the go() words
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    static_assert(S2_NST == 10, "the item start's count");
+    if constexpr (C::NST == 10)
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    static_assert(C::NST == 10 || C::NST == 5, "the item start's count");
     S2_TLX(0, __builtin_amdgcn_s_memrealtime());
+    S2Ent<Q> eAn;  // the order of step i-1 (the values the go() below issues)
+    s2_ent_issue(eAn, pk + (size_t)pstep(i - 1) * S2_PACK, sk + (size_t)pstep(i - 1) * (NW * S2_SEAMS));
+    asm volatile("" ::: "memory");
     // ---- the step's scalars (this wave's LDS copy): df(:, i .. i+1), u_old(:, i .. i+2) -----------------------------
     // (the same in every lane: read into scalars)
     auto sread = [&](int e) {
@@ -515,7 +554,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     for (int m = 0; m < M; ++m) d01 += abs((int)u0[m] - (int)u1[m]);
     const unsigned hb0 = sd_bytes((unsigned)h0);
     // ---- this item's values A: Ψ by rank, raw into the transform buffer, the row's statistics -------------------
-    double v[2 * S2_Q], xs;
+    double v[2 * Q], xs;
     s2_take(v, xs, rA);
     const int srank = (int)(eA.seam >> 16);
     const bool shas = lane < 32 && eA.seam != 0xFFFFFFFFu;
@@ -526,14 +565,14 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       auto cand = [&](double x, unsigned d) { return (T1H + beta * (double)d) + x; };  // HelpFunctions.jl:67,71
       if (sameH) {
 #pragma unroll
-        for (int q = 0; q < S2_Q; ++q) {
+        for (int q = 0; q < Q; ++q) {
           const unsigned d = (unsigned)s2_bt(eA.w[q]);
           hp = sd_min(hp, sd_min(cand(v[2 * q], d), cand(v[2 * q + 1], d)));
         }
         hp = sd_min(hp, cand(xs, (eA.seam >> 10) & 31u));
       } else {
 #pragma unroll
-        for (int q = 0; q < S2_Q; ++q) {
+        for (int q = 0; q < Q; ++q) {
           hp = sd_min(hp, sd_min(cand(v[2 * q], sd_l1(sd_bytes((unsigned)s2_ra(eA.w[q])), hb0)),
                                  cand(v[2 * q + 1], sd_l1(sd_bytes((unsigned)s2_rb(eA.w[q])), hb0))));
         }
@@ -541,7 +580,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       }
       hp = s2_wave_min(hp);
       __builtin_amdgcn_raw_buffer_store_b64((sd_u32x2){(unsigned)__double2loint(hp), (unsigned)__double2hiint(hp)},
-                                            hrs, lane == 0 ? (unsigned)(4 * i + w) * 8u : OOB, 0, 16);
+                                            hrs, lane == 0 ? (unsigned)(NW * i + w) * 8u : OOB, 0, 16);
     }
     // ---- the value at this item's head position, Φ_{i+1}[c', h(i+1)] = min(the partner's parts over the values of its
     // item (c', i+1), the term j = h(i+2): fl(fl(T1(h(i+1), i+1) + β·d(h(i+1), h(i+2))) + Φ_{i+2}[c', h(i+2)])); +Inf at
@@ -550,7 +589,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     if (i < nt - 2) {
       {  // the parts were loaded one item ahead; a part still all-ones (not yet stored) is polled here
         // (the first test outside the loop: its operand is the tail load, which the item start's count covers)
-        bool okp = !__any(lane < 4 && __double_as_longlong(pp) == -1ll);
+        bool okp = !__any(lane < NW && __double_as_longlong(pp) == -1ll);
         unsigned spins = 0;
         while (!okp) {
           if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
@@ -563,9 +602,9 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
           }
           __builtin_amdgcn_s_sleep(1);
           pp = __longlong_as_double((long long)__hip_atomic_load(
-              reinterpret_cast<const unsigned long long *>(hk + 4 * (i + 1) + (lane & 3)), __ATOMIC_RELAXED,
+              reinterpret_cast<const unsigned long long *>(hk + NW * (i + 1) + (lane & (NW - 1))), __ATOMIC_RELAXED,
               __HIP_MEMORY_SCOPE_AGENT));
-          okp = !__any(lane < 4 && __double_as_longlong(pp) == -1ll);
+          okp = !__any(lane < NW && __double_as_longlong(pp) == -1ll);
         }
         S2_TLX(2, spins);
       }
@@ -577,19 +616,19 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       for (int m = 0; m < M; ++m) d12 += abs((int)u1[m] - (int)u2[m]);
       l0v = (T1P + beta * (double)d12) + Hprev;  // HelpFunctions.jl:67,71
 #pragma unroll
-      for (int q = 0; q < 4; ++q) l0v = sd_min(l0v, sd_rdl(pp, q));
+      for (int q = 0; q < NW; ++q) l0v = sd_min(l0v, sd_rdl(pp, q));
     }
     S2_TLX(1, __builtin_amdgcn_s_memrealtime());
     // this lane's targets: the lines q = tid and tid + 256 of the last pass, ranks q | x << 9
     int uo[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) uo[m] = __builtin_amdgcn_readfirstlane((int)u0[m]);
-    double pre[2];
+    double pre[LN];
     unsigned valid = 0;
     int nv = 0;
 #pragma unroll
-    for (int ln = 0; ln < 2; ++ln) {
-      const int q = tid + S2_T * ln;
+    for (int ln = 0; ln < LN; ++ln) {
+      const int q = tid + T * ln;
       double t = 0.0;
       int bp = 0;
 #pragma unroll
@@ -609,7 +648,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     if (tid == 0) sh.nlist = 0;
     double pmn = INFINITY, pmx = -INFINITY;
 #pragma unroll
-    for (int q = 0; q < S2_Q; ++q)
+    for (int q = 0; q < Q; ++q)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const double x = v[2 * q + hh];
@@ -649,7 +688,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     {
       double hm = (T1H + beta * (double)d01) + l0v;  // the term j = h(i+1) of (*)
 #pragma unroll
-      for (int q = 0; q < S2_NW; ++q) hm = sd_min(hm, sh.pmin[q]);
+      for (int q = 0; q < NW; ++q) hm = sd_min(hm, sh.pmin[q]);
       Hprev = hm;
     }
     // go()'s words, checked after the winners
@@ -658,11 +697,11 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     int val2 = __hip_atomic_load(dp.fp2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     {
       __builtin_amdgcn_raw_buffer_store_b32((unsigned)tok(i), frs,
-                                            tid == S2_T - 64 ? (unsigned)((size_t)(loaded + 2 * cp + par) - (size_t)flags)
+                                            tid == T - 64 ? (unsigned)((size_t)(loaded + 2 * cp + par) - (size_t)flags)
                                                              : OOB,
                                             0, 16);
       __builtin_amdgcn_raw_buffer_store_b32((unsigned)tok(prev_i), frs,
-                                            tid == S2_T - 64 && prev_i >= 0
+                                            tid == T - 64 && prev_i >= 0
                                                 ? (unsigned)((size_t)(done + 2 * cp + par) - (size_t)flags)
                                                 : OOB,
                                             0, 16);
@@ -671,7 +710,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     double pmn2 = INFINITY, pmx2 = -INFINITY;
     nv = 0;
 #pragma unroll
-    for (int q = 0; q < S2_NW; ++q) {
+    for (int q = 0; q < NW; ++q) {
       pmn2 = sd_min(pmn2, sh.rmn[q]);
       pmx2 = sd_max(pmx2, sh.rmx[q]);
       nv += sh.rnv[q];
@@ -718,7 +757,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       if (tid == 0) sh.nsp = 0;
       sd_bar();
 #pragma unroll
-      for (int q = 0; q < S2_Q; ++q)
+      for (int q = 0; q < Q; ++q)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
           if (v[2 * q + hh] < INFINITY) {
@@ -741,27 +780,27 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     const bool transform = !direct && !empty && !sparse;
     S2_TL(2);
     // ---- the transform -------------------------------------------------------------------------------------------
-    auto pos3 = [&](int e) { return sd_swz((sd_tid() + S2_T * (e >> 3)) | ((e & 7) << 9)); };
+    auto pos3 = [&](int e) { return sd_swz((sd_tid() + T * (e >> 3)) | ((e & 7) << 9)); };
     // an opaque zero: the targets' T1 terms a_3·ν_3 are recomputed per target (two VALU) instead of being hoisted into
     // registers that would be spilled
     int zop = 0;
     asm volatile("" : "+v"(zop));
     if (transform) {
-      double o[16];
+      double o[8 * LN];
       auto pass = [&](int m) {
-        int pos[16];
+        int pos[8 * LN];
 #pragma unroll
-        for (int ln = 0; ln < 2; ++ln)
+        for (int ln = 0; ln < LN; ++ln)
 #pragma unroll
           for (int x = 0; x < 8; ++x) {
-            pos[8 * ln + x] = sd_swz(sd_rank(tid + S2_T * ln, m, x));
+            pos[8 * ln + x] = sd_swz(sd_rank(tid + T * ln, m, x));
             o[8 * ln + x] = dtv[pos[8 * ln + x]];
           }
         if (m == 0) {  // the raw Ψ of ranks 8q + x: stamp them here
 #pragma unroll
-          for (int ln = 0; ln < 2; ++ln)
+          for (int ln = 0; ln < LN; ++ln)
 #pragma unroll
-            for (int x = 0; x < 8; ++x) o[8 * ln + x] = stamp_inf(o[8 * ln + x], sd_rank(tid + S2_T * ln, 0, x));
+            for (int x = 0; x < 8; ++x) o[8 * ln + x] = stamp_inf(o[8 * ln + x], sd_rank(tid + T * ln, 0, x));
         }
         // forward then backward sweep of both lines, interleaved (two independent chains)
 #pragma unroll
@@ -776,7 +815,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
         }
         if (m + 1 < M) {
 #pragma unroll
-          for (int x = 0; x < 16; ++x) dtv[pos[x]] = o[x];
+          for (int x = 0; x < 8 * LN; ++x) dtv[pos[x]] = o[x];
         }
       };
       pass(0);
@@ -792,12 +831,12 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     unsigned listed = 0;
     if (empty) {
 #pragma unroll
-      for (int x = 0; x < 16; ++x) dtv[pos3(x)] = INFINITY;
-      reinterpret_cast<ulonglong2 *>(uu)[2 * tid] = make_ulonglong2(~0ull, ~0ull);
-      reinterpret_cast<ulonglong2 *>(uu)[2 * tid + 1] = make_ulonglong2(~0ull, ~0ull);
+      for (int x = 0; x < 8 * LN; ++x) dtv[pos3(x)] = INFINITY;
+#pragma unroll
+      for (int ub = 0; ub < UB; ++ub) reinterpret_cast<ulonglong2 *>(uu)[UB * tid + ub] = make_ulonglong2(~0ull, ~0ull);
     } else if (transform) {
 #pragma unroll
-      for (int ln = 0; ln < 2; ++ln) {
+      for (int ln = 0; ln < LN; ++ln) {
         // the last pass (along x3) on this line, then its eight winners (their Ψ reads issue together)
         double o[8];
 #pragma unroll
@@ -814,7 +853,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
         for (int x = 0; x < 8; ++x) pv[x] = psi[jx[x]];
 #pragma unroll
         for (int x = 0; x < 8; ++x) {
-          const int e = 8 * ln + x, r = (tid + S2_T * ln) | (x << 9), j = jx[x];
+          const int e = 8 * ln + x, r = (tid + T * ln) | (x << 9), j = jx[x];
           const bool fin = (valid >> e & 1) && o[x] < INFINITY;
           const bool flg = (__double2loint(o[x]) & SD_CNT) != 0;
           // d(l, j*) exactly: an unflagged finite o is V_j* + d with V_j* the stamp of Ψ_j*
@@ -828,10 +867,10 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
       }
     } else {
 #pragma unroll
-      for (int ln = 0; ln < 2; ++ln)
+      for (int ln = 0; ln < LN; ++ln)
 #pragma unroll
         for (int x = 0; x < 8; ++x) {
-          const int e = 8 * ln + x, r = (tid + S2_T * ln) | (x << 9);
+          const int e = 8 * ln + x, r = (tid + T * ln) | (x << 9);
           double ov = INFINITY;
           int uj = 0xFFFF;
           if (direct) {
@@ -860,13 +899,18 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     if (listed) {
       int e = atomicAdd(&sh.nlist, __popc(listed));
 #pragma unroll
-      for (int x = 0; x < 16; ++x)
+      for (int x = 0; x < 8 * LN; ++x)
         if (listed >> x & 1) {
-          if (e < SD_LCAP) list[e] = (uint16_t)((tid + S2_T * (x >> 3)) | ((x & 7) << 9));
+          if (e < SD_LCAP) list[e] = (uint16_t)((tid + T * (x >> 3)) | ((x & 7) << 9));
           ++e;
         }
     }
     S2_TL(4);
+    // the order of step i (this item's outputs, read after the scan): issued before the next item's loads, so that the
+    // gather waits for it alone
+    S2Ent<Q> eO;
+    s2_ent_issue(eO, pk + (size_t)i * S2_PACK, sk + (size_t)i * (NW * S2_SEAMS));
+    asm volatile("" ::: "memory");  // (issued here, not sunk below the next item's loads)
 #if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)
     unsigned long long tl_bits = 0;
 #endif
@@ -895,7 +939,7 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
         ready = __all(val1 >= need1 && val2 >= need2);
       }
       const int ni = i - 2;
-      s2_issue(rA, rs, eAn, cp, boffs(pstep(ni + 1)), r0b + (unsigned)pstep(ni + 1) * rowb, rowb, has_next);
+      s2_issue<T>(rA, rs, eAn, cp, boffs(pstep(ni + 1)), r0b + (unsigned)pstep(ni + 1) * rowb, rowb, has_next);
       s2_dfuo_dma(dfk, uok, pstep(ni), nt, sds);
     }
     S2_TL(5);
@@ -903,50 +947,44 @@ __global__ __launch_bounds__(S2_T, 2) void k_sdt_pair(ProblemDev P, LevelsDev Lv
     if (threadIdx.x == 0 && tl_on) s2_tl_lds[item - tl_item0][5] |= tl_bits;
 #endif
     S2_TL(6);
-    S2Ent eOn, eAnn;  // the orders of steps i-2 (the next item's outputs) and i-3 (A of the item after it): loaded
-                      // here, a while before the loop's back edge moves them into place (no wait there)
-    s2_ent_issue(eOn, pk + (size_t)pstep(i - 2) * S2_PACK, sk + (size_t)pstep(i - 2) * (S2_NW * S2_SEAMS));
-    s2_ent_issue(eAnn, pk + (size_t)pstep(i - 3) * S2_PACK, sk + (size_t)pstep(i - 3) * (S2_NW * S2_SEAMS));
     sd_bar();  // (3) the list is complete
     const int nl = sh.nlist;
     if (nl) {
       if (nl <= SD_COOP)
-        s2_scan<true>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
+        s2_scan<T, true>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
       else if (nl <= SD_LCAP)
-        s2_scan<false>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
+        s2_scan<T, false>(list, nl, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);
       else
-        s2_scan<false>(nullptr, L, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);  // every NaN-marked rank
+        s2_scan<T, false>(nullptr, L, psi, a, lb, beta, uu, dtv, sh.redv, sh.redj);  // every NaN-marked rank
       sd_bar();
       if (tid == 0) sh.cnt[direct ? 1 : 0] += nl;
     }
     // ---- row c' of S_i in the sphere order of u_old(i), the U row ---------------------------------------------------
-    unsigned long long so[2 * S2_Q];
+    unsigned long long so[2 * Q];
 #pragma unroll
-    for (int q = 0; q < S2_Q; ++q) {
+    for (int q = 0; q < Q; ++q) {
       so[2 * q] = __double_as_longlong(dtv[sd_swz(s2_ra(eO.w[q]))]);
       so[2 * q + 1] = __double_as_longlong(dtv[sd_swz(s2_rb(eO.w[q]))]);
     }
-    const ulonglong2 ua = reinterpret_cast<const ulonglong2 *>(uu)[2 * tid];
-    const ulonglong2 ub = reinterpret_cast<const ulonglong2 *>(uu)[2 * tid + 1];
-    // the next item's orders: A = this item's eAn, outputs = the one loaded above, then A of the item after it
-    eA = eAn;
-    eO = eOn;
-    eAn = eAnn;
+    // (two named values, not an array: an array of them went to scratch)
+    const ulonglong2 ua = reinterpret_cast<const ulonglong2 *>(uu)[UB * tid];
+    const ulonglong2 ub = UB > 1 ? reinterpret_cast<const ulonglong2 *>(uu)[UB * tid + 1] : ua;
+    eA = eAn;  // the next item's values A
     sd_bar();  // (4) every wave has read the outputs: the next item may overwrite the buffers
     stop = sh.stop != 0;
     pp = parts_load(i - 2, lane);  // before the stores (the next item's first wait does not wait for them)
     {
       const __amdgpu_buffer_rsrc_t rso = sd_rsrc(reg + (size_t)(i % NB) * R * L + (size_t)cp * L, L * 8);
 #pragma unroll
-      for (int q = 0; q < S2_Q; ++q) {
+      for (int q = 0; q < Q; ++q) {
         const sd_u32x4 d = {(unsigned)so[2 * q], (unsigned)(so[2 * q] >> 32), (unsigned)so[2 * q + 1],
                             (unsigned)(so[2 * q + 1] >> 32)};
-        __builtin_amdgcn_raw_buffer_store_b128(d, rso, 2 * (tid + S2_T * q) * 8, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(d, rso, 2 * (tid + T * q) * 8, 0, 16);
       }
       ulonglong2 *Ur = reinterpret_cast<ulonglong2 *>(UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) +
-                                                      (size_t)cp * L) + 2 * tid;
+                                                      (size_t)cp * L) + UB * tid;
       Ur[0] = ua;  // read by later launches only (backtrack)
-      Ur[1] = ub;
+      if constexpr (UB > 1) Ur[1] = ub;
     }
     S2_TL(7);
     prev_i = i;
@@ -977,22 +1015,32 @@ bool sdt_pair_supported(const PyrGeom &G, int K, int B, int ncu, int bpc) {
   return B >= 1 && bpc >= 2 && (size_t)K * (size_t)B <= (size_t)ncu * (size_t)(bpc / 2);
 }
 
-size_t sdt_pair_lds_bytes() { return S2_LDS; }
+size_t sdt_pair_lds_bytes(int threads) { return threads == 512 ? S2C<512>::LDS : S2C<256>::LDS; }
 
-int sdt_pair_blocks_per_cu() {
+int sdt_pair_blocks_per_cu(int threads) {
   int n = 0;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_sdt_pair, S2_T, S2_LDS) == hipSuccess ? n : 0;
+  const hipError_t e =
+      threads == 512
+          ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_sdt_pair<512>, 512, S2C<512>::LDS)
+          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_sdt_pair<256>, 256, S2C<256>::LDS);
+  return e == hipSuccess ? n : 0;
 }
 
+int sdt_pair_seam_words(int threads) { return threads / 64 * S2_SEAMS; }
+
 hipError_t launch_sdt_pack(hipStream_t s, const ProblemDev &P, const uint32_t *perm, uint32_t *pack, uint32_t *seams,
-                           int32_t *counters) {
-  hipLaunchKernelGGL(k_sdt2_pack, dim3(P.nt, P.K), dim3(S2_T), 0, s, perm, P.nt, pack, seams, counters);
+                           int32_t *counters, int threads) {
+  if (threads == 512)
+    hipLaunchKernelGGL(k_sdt2_pack<512>, dim3(P.nt, P.K), dim3(512), 0, s, perm, P.nt, pack, seams, counters);
+  else
+    hipLaunchKernelGGL(k_sdt2_pack<256>, dim3(P.nt, P.K), dim3(256), 0, s, perm, P.nt, pack, seams, counters);
   return hipGetLastError();
 }
 
 hipError_t launch_sdt_pair(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
                            const uint32_t *pack, const uint32_t *seams, double *S, size_t kstride, int NB, uint16_t *UU,
-                           size_t uu_stride_k, int32_t *counters, int32_t *flags, double *heads, unsigned spin_limit) {
+                           size_t uu_stride_k, int32_t *counters, int32_t *flags, double *heads, unsigned spin_limit,
+                           int threads) {
   // every workgroup must be resident (the caller checked 2·K·B <= CUs x resident workgroups per CU); an ordinary
   // launch (mioc_sdt.hip, launch_sdt_run: a cooperative launch crashed the profiler at exit)
   const double *df = P.df, *uo = P.uold;
@@ -1000,7 +1048,9 @@ hipError_t launch_sdt_pair(hipStream_t s, const ProblemDev &P, const LevelsDev &
                   (void *)&S,     (void *)&kstride,    (void *)&NB,    (void *)&UU,         (void *)&uu_stride_k,
                   (void *)&counters, (void *)&flags,   (void *)&heads, (void *)&spin_limit, (void *)&df,
                   (void *)&uo};
-  return hipLaunchKernel((const void *)k_sdt_pair, dim3(2 * P.K * P.B), dim3(S2_T), args, S2_LDS, s);
+  if (threads == 512)
+    return hipLaunchKernel((const void *)k_sdt_pair<512>, dim3(2 * P.K * P.B), dim3(512), args, S2C<512>::LDS, s);
+  return hipLaunchKernel((const void *)k_sdt_pair<256>, dim3(2 * P.K * P.B), dim3(256), args, S2C<256>::LDS, s);
 }
 
 #if defined(MIOC_STAMPS) && defined(MIOC_STAMPS_TL)

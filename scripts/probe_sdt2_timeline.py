@@ -28,7 +28,7 @@ def main():
         ctx.set_levels(lt)
         ctx.set_cost(1, cfg.beta)
         ctx.set_option(native.MIOC_OPT_TIMING, 1)
-        ctx.set_option(native.MIOC_OPT_SDT_PAIR, 1)
+        ctx.set_option(native.MIOC_OPT_SDT_PAIR, int(os.environ.get("SDT_PAIR", "1")))  # 1: 256 threads, 2: 512
         if int(os.environ.get("SDT_NB", "0")):  # staging buffers (MIOC_OPT_SDT_BUFFERS)
             ctx.set_option(native.MIOC_OPT_SDT_BUFFERS, int(os.environ["SDT_NB"]))
         ctx.bellman(df, uo, cfg.B, cfg.dt)
@@ -36,7 +36,7 @@ def main():
         ms, _, name = ctx.kernel_stats(0)
         print(f"{name}: {ms:.3f} ms for {nt - 1} steps = {1e3 * ms / (nt - 1):.3f} us/step; diag {ctx.diagnostics()}")
     lib = native.load_library()
-    NB = 2 * cfg.B
+    NB = 2 * cfg.B  # (workgroups)
     buf = np.zeros((1024, 32, 8), dtype=np.uint64)
     f = lib.mioc_debug_sdt2_timeline
     f.restype = ctypes.c_int32

@@ -39,7 +39,7 @@ def _hash(t):
     return np.frombuffer(hashlib.sha256(np.ascontiguousarray(t, dtype=np.int32).tobytes()).digest(), dtype=np.uint8)
 
 
-@pytest.mark.parametrize("variant", ["pair", "persistent", "steps"])
+@pytest.mark.parametrize("variant", ["pair", "pair512", "persistent", "steps"])
 def test_c4_nt64_fixture(variant):
     """The separable transform writes U exactly like the reference: the rank where the reference writes it, and
     nothing (-1) elsewhere, so every step's table hashes to the oracle's.  persistent: k_sdt_run (the bench's kernel),
@@ -48,13 +48,15 @@ def test_c4_nt64_fixture(variant):
     cfg = CONFIGS["C4"]
     lt = cfg.levels()
     algo = native.MIOC_ALGO_SEPARABLE
-    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=int(variant != "steps"), pair=int(variant == "pair"))
+    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=int(variant != "steps"),
+               pair={"pair": 1, "pair512": 2}.get(variant, 0))
     df, uo = z["df"], z["u_old"]
     B = int(z["B"][0])
     ctx.bellman(df, uo, B, float(z["dt"][0]))
     assert ctx.last_algo() == algo
     ctx.synchronize()
-    assert ctx.kernel_stats(0)[2] == {"pair": "k_sdt_pair", "persistent": "k_sdt_run", "steps": "k_sdt_step"}[variant]
+    assert ctx.kernel_stats(0)[2] == {"pair": "k_sdt_pair", "pair512": "k_sdt_pair", "persistent": "k_sdt_run",
+                                      "steps": "k_sdt_step"}[variant]
     nt = df.shape[1]
     bad = [i for i in range(nt - 1) if not np.array_equal(_hash(ctx.argmin_table(i)), z["u_hash"][i])]
     assert not bad, f"{variant}: U differs from the oracle at steps {bad[:10]}"
@@ -65,7 +67,7 @@ def test_c4_nt64_fixture(variant):
     ctx.close()
 
 
-@pytest.mark.parametrize("variant", ["pair", "persistent", "steps"])
+@pytest.mark.parametrize("variant", ["pair", "pair512", "persistent", "steps"])
 @pytest.mark.parametrize("mode", ["zero", "integer", "steep"])
 def test_c4_tie_heavy_vs_oracle(oracle_c, mode, variant):
     """4096 levels, B = 256: every target of a zero-gradient row ties (the listed-target buffer overflows and the
@@ -84,7 +86,7 @@ def test_c4_tie_heavy_vs_oracle(oracle_c, mode, variant):
         df = df * 1e3  # value spread ~1e12 beta: outside the transform's binade (2^36 units)
     beta = 1e-13 if mode == "steep" else cfg.beta
     phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_ONE, beta, cfg.dt)
-    ctx = _ctx(lt, beta, native.MIOC_ALGO_SEPARABLE, int(variant != "steps"), int(variant == "pair"))
+    ctx = _ctx(lt, beta, native.MIOC_ALGO_SEPARABLE, int(variant != "steps"), {"pair": 1, "pair512": 2}.get(variant, 0))
     ctx.bellman(df, uo, cfg.B, cfg.dt)
     diag = ctx.diagnostics()
     for i in range(n - 1):
@@ -141,7 +143,7 @@ def test_c4_chunked_rows_vs_oracle(oracle_c):
     ctx.close()
 
 
-@pytest.mark.parametrize("pair", [1, 0], ids=["pair", "persistent"])
+@pytest.mark.parametrize("pair", [1, 2, 0], ids=["pair", "pair512", "persistent"])
 def test_c4_nt64_fixture_wait_timeout_redoes_dp(pair):
     """The headline kernels' timeout path: with a spin limit of one poll, the persistent k_sdt_pair / k_sdt_run gives
     up at its first dependency wait that is not already satisfied, every workgroup leaves, and the host redoes the DP
