@@ -525,14 +525,30 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     }
     sd_bar();  // every wave has consumed its loads of S_{i+1} (their values are in LDS)
     h.early();
+    {
+      // every wave's statistics in one batch of LDS reads and one wait (the compiler interleaved them with the
+      // reduction: six dependent LDS round trips), then a tree
+      double mn[NW], mx[NW];
+      int cn[NW];
 #pragma unroll
-    for (int q = 0; q < NW; ++q) {
-      pmn = sd_min(pmn, sh.rmn[q]);
-      pmx = sd_max(pmx, sh.rmx[q]);
+      for (int q = 0; q < NW; ++q) {
+        mn[q] = sh.rmn[q];
+        mx[q] = sh.rmx[q];
+        cn[q] = sh.rnv[q];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int h = NW / 2; h >= 1; h >>= 1)
+#pragma unroll
+        for (int q = 0; q < h; ++q) {
+          mn[q] = sd_min(mn[q], mn[q + h]);
+          mx[q] = sd_max(mx[q], mx[q + h]);
+          cn[q] += cn[q + h];
+        }
+      pmn = mn[0];
+      pmx = mx[0];
+      nv = cn[0];
     }
-    nv = 0;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) nv += sh.rnv[q];
     nf = nv >> 16;
     nv &= 0xFFFF;
     SD_STAMP(1);
