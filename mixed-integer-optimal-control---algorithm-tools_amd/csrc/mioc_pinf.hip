@@ -48,6 +48,12 @@ namespace mioc {
 #ifndef PINF_RECUR_G
 #define PINF_RECUR_G 4      // lanes per row pair when split (2 or 4)
 #endif
+#ifndef PINF_RECUR_WS
+#define PINF_RECUR_WS 1     // few subproblems, classes <= 8: 64-row segments, the chain by DPP wave shifts (k_pinf_recur_ws)
+#endif
+#ifndef PINF_WS_CHUNK
+#define PINF_WS_CHUNK 64    // k_pinf_recur_ws: steps per segment hand-off
+#endif
 
 __device__ __forceinline__ double p_t1(const double *nuv, const double *dfi, int M, double dt) {
   double t = 0.0;
@@ -959,6 +965,133 @@ __global__ __launch_bounds__(256) void k_pinf_recur_mcw(ProblemDev P, PinfDev D,
   }
 }
 
+// Narrow class windows (BW <= 8 classes: the SOS1 shapes C1-C3, where k_pinf_recur's per-step LDS round trip and
+// barrier are the whole step): row segments of 64 rows, one lane per row, one wave per workgroup, on as many CUs.
+// Row c = 64q + l needs R_{i+1}[c - b] for b < CB <= 8 only: inside the segment that is lane l - b's register, reached
+// by b chained DPP `wave_shr:1` moves whose lane 0 is filled from the segment below (rows 64q - b, staged for the step
+// in the LDS); so a step is CB-1 shifts, CB sums and CB-1 minima on registers, and one R store, with no LDS round trip
+// and no barrier on the chain.  The hand-off between segments is k_pinf_recur_mc's (chunks of CH steps: the segment
+// below stores its rows, drains, publishes the chunk's last step; this one polls a chunk ahead and copies the 8 rows
+// below it for the chunk's steps by LDS-DMA).  Same candidates fl(Kmin_i[b] + R_{i+1}[c - b]), and min is exact: R is
+// bit-identical to k_pinf_recur's.  A wait past the spin limit sets the error word (flags[errw]) and the host redoes
+// the DP in one workgroup (check_run).
+template <int CB>
+__device__ __forceinline__ double ws_shr1(double x, double fill) {  // lane l <- lane l-1, lane 0 <- fill
+  return __hiloint2double(__builtin_amdgcn_update_dpp(__double2hiint(fill), __double2hiint(x), 0x138, 0xF, 0xF, false),
+                          __builtin_amdgcn_update_dpp(__double2loint(fill), __double2loint(x), 0x138, 0xF, 0xF, false));
+}
+template <int CB>
+__global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, int nseg, int32_t *flags, int errw,
+                                                      unsigned spin_limit) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  constexpr int CH = PINF_WS_CHUNK, NS = 2 * CH, HB = 8;  // ring of NS step slots of the HB rows below the segment
+  static_assert(CB >= 2 && CB <= HB, "k_pinf_recur_ws: 2 <= classes <= 8");
+  const int RP = P.RP, nt = P.nt, BWP = D.BWP;
+  const int k = (int)blockIdx.x / nseg, q = (int)blockIdx.x - k * nseg;
+  const int lane = (int)threadIdx.x, c = 64 * q + lane;
+  double *H = sm, *Kbuf = sm + (size_t)NS * HB;  // H: [NS][HB] rows 64q-8 .. 64q-1 of step s; Kbuf: [2][CH][BWP]
+  const double *kmin = D.kmin + (size_t)k * nt * BWP;
+  double *R = D.R + (size_t)k * nt * RP;
+  int32_t *done = flags + (size_t)k * nseg, *err = flags + errw;
+  const __amdgpu_buffer_rsrc_t Rr = __builtin_amdgcn_make_buffer_rsrc(R, 0, (int)((size_t)nt * RP * 8), 0x00020000);
+  auto slot = [&](int s) { return H + (size_t)(s % NS) * HB; };
+  // terminal row R_{n-1}[c'] = Kmin_{n-1}[c'] (c' < BWP), the rows below included (a function of kmin: no hand-off)
+  for (int e = lane; e < NS * HB; e += 64) H[e] = INFINITY;
+  if (lane < HB) {
+    const int cc = 64 * q - HB + lane;
+    slot(nt - 1)[lane] = cc >= 0 && cc < BWP ? kmin[(size_t)(nt - 1) * BWP + cc] : INFINITY;
+  }
+  double r = c < BWP ? kmin[(size_t)(nt - 1) * BWP + c] : INFINITY;  // this lane's row of R_{i+1}
+  R[(size_t)(nt - 1) * RP + c] = c <= P.B ? r : INFINITY;
+  if (nt < 2) return;
+  bool stop = false;
+  auto wait_below = [&](int s) {  // segment q-1 has published step s (token nt-1-s); false past the spin limit
+    if (q == 0) return true;
+    const int need = nt - 1 - s;
+    unsigned spins = 0;
+    while (__hip_atomic_load(done + q - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+  };
+  // rows 64q-8 .. 64q-1 of R_s for steps s in [s0, s1] into their ring slots: lanes 0-3, 16 bytes each (LDS-DMA, sc1)
+  auto halo = [&](int s0, int s1) {
+    if (q == 0) return;
+    for (int s = s0; s <= s1; ++s) {
+      if (lane < HB / 2) {
+        const void *g = pi_uniform(R + (size_t)s * RP);
+        const unsigned m0 =
+            __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)slot(s)));
+        const unsigned voff = 8u * (unsigned)(64 * q - HB + 2 * lane);
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 sc1\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(g), "s"(m0)
+                     : "memory");
+      }
+    }
+  };
+  int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
+  glds_copy_asm(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, lane, 64);
+  if (lo + 1 <= nt - 2) {  // the first chunk's rows below (step nt-1's are computed above)
+    stop = !wait_below(lo + 1);
+    halo(lo + 1, nt - 2);
+  }
+  vm_drain();
+  for (int qq = 0; hi >= 0 && !stop; ++qq) {
+    const double *Kc = Kbuf + (size_t)(qq & 1) * CH * BWP;
+    const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
+    if (nhi >= 0) {  // the next chunk: its class rows, and (once the segment below has them) its rows below
+      glds_copy_asm(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((qq + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
+                    lane, 64);
+      if (!wait_below(nlo + 1)) {
+        stop = true;
+        break;
+      }
+      halo(nlo + 1, nhi + 1);
+    }
+    // the step's operands, read a step ahead (broadcast LDS reads, off the chain): class values Kmin_i[0 .. CB-1] and
+    // the fills R_{i+1}[64q - b], b = 1 .. CB-1
+    auto opnd = [&](double (&kv)[CB], double (&hv)[CB], int i) {
+      const double *kr = Kc + (size_t)(i - lo) * BWP;
+      const double *hr = slot(i + 1) + HB - CB;
+#pragma unroll
+      for (int b = 0; b < CB; ++b) {
+        kv[b] = kr[b];
+        hv[b] = hr[b];  // hv[CB-1-b'] = R_{i+1}[64q - 1 - b']
+      }
+    };
+    auto step = [&](int i, const double (&kv)[CB], const double (&hv)[CB], double (&kn)[CB], double (&hn)[CB]) {
+      asm volatile("" ::: "memory");
+      if (i > lo) opnd(kn, hn, i - 1);
+      double sft = r, m = kv[0] + r;
+#pragma unroll
+      for (int b = 1; b < CB; ++b) {
+        sft = ws_shr1<CB>(sft, hv[CB - b]);  // lane l: R_{i+1}[c - b]
+        m = pvmin(m, kv[b] + sft);
+      }
+      r = m;
+      __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(r), (unsigned)__double2hiint(r)}, Rr,
+                                            (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
+    };
+    double ka[CB], ha[CB], kb[CB], hb[CB];
+    opnd(ka, ha, hi);
+    for (int i = hi; i >= lo; i -= 2) {
+      step(i, ka, ha, kb, hb);
+      if (i - 1 >= lo) step(i - 1, kb, hb, ka, ha);
+    }
+    // this chunk's rows have landed: publish its last step for the segment above
+    vm_drain();
+    if (lane == 0) __hip_atomic_store(done + q, nt - 1 - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hi = nhi;
+    lo = nlo;
+  }
+}
+
 // rows c_from .. RP-1 of R (beyond the rows k_pinf_recur_xr / _mc compute, all above B): +Inf for every step
 __global__ void k_pinf_rfill(ProblemDev P, PinfDev D, int c_from) {
   const int k = blockIdx.y, RP = P.RP, nt = P.nt, n = RP - c_from;
@@ -989,6 +1122,31 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
                              unsigned spin_limit, bool *segmented, const char **variant) {
   if (segmented) *segmented = false;
   if (variant) *variant = "k_pinf_recur";
+  // few subproblems, classes <= 8, two or more 64-row segments: k_pinf_recur_ws (its error word where the host reads
+  // k_pinf_recur_mc's: flags[K·pinf_recur_segments])
+  {
+    const int nseg = (P.B + 1 + 63) / 64;
+    if (PINF_RECUR_WS && flags && segmented && D.BW >= 1 && D.BW <= 8 && D.BWP == 8 && nseg >= 2 &&
+        P.K * nseg <= ncu && 64 * nseg <= P.RP && (size_t)P.nt * P.RP * 8 < (1ull << 31)) {
+      const int errw = P.K * pinf_recur_segments(P);
+      const size_t lds = (size_t)(2 * PINF_WS_CHUNK * 8 + 2 * PINF_WS_CHUNK * D.BWP) * sizeof(double);
+      const dim3 grid(P.K * nseg);
+      switch (D.BW < 2 ? 2 : D.BW) {
+        case 2: hipLaunchKernelGGL(k_pinf_recur_ws<2>, grid, dim3(64), lds, s, P, D, nseg, flags, errw, spin_limit); break;
+        case 3: hipLaunchKernelGGL(k_pinf_recur_ws<3>, grid, dim3(64), lds, s, P, D, nseg, flags, errw, spin_limit); break;
+        case 4: hipLaunchKernelGGL(k_pinf_recur_ws<4>, grid, dim3(64), lds, s, P, D, nseg, flags, errw, spin_limit); break;
+        case 5: hipLaunchKernelGGL(k_pinf_recur_ws<5>, grid, dim3(64), lds, s, P, D, nseg, flags, errw, spin_limit); break;
+        case 6: hipLaunchKernelGGL(k_pinf_recur_ws<6>, grid, dim3(64), lds, s, P, D, nseg, flags, errw, spin_limit); break;
+        case 7: hipLaunchKernelGGL(k_pinf_recur_ws<7>, grid, dim3(64), lds, s, P, D, nseg, flags, errw, spin_limit); break;
+        default: hipLaunchKernelGGL(k_pinf_recur_ws<8>, grid, dim3(64), lds, s, P, D, nseg, flags, errw, spin_limit); break;
+      }
+      // rows above B (the top segment's finite values, and the rows no segment computes): +Inf, after the launch
+      if (P.B + 1 < P.RP) hipLaunchKernelGGL(k_pinf_rfill, dim3(64, P.K), dim3(256), 0, s, P, D, P.B + 1);
+      *segmented = true;
+      if (variant) *variant = "k_pinf_recur_ws";
+      return hipGetLastError();
+    }
+  }
   // few subproblems, classes <= 32, tall enough: row segments of 32 on several CUs (k_pinf_recur_mc); the flags
   // (K·nseg + 1 words, zeroed by the caller) carry the hand-off and the error word
   {

@@ -1,6 +1,7 @@
 """C4 at p = Inf (one subproblem, full L and B, nt from argv) across library builds, each in its own process:
 k_pinf_recur time per launch (HIP events), k_pinf_prep's, the whole bellman + backtrack wall time, and a digest of u / Φ* at three
-budgets, which must agree across builds.  Usage: python scripts/probe_pinf_c4.py NT LIB [LIB ...]"""
+budgets, which must agree across builds.  Usage: python scripts/probe_pinf_c4.py NT LIB [LIB ...]
+(PINF_CFG=C1 / C2 / C3: that config instead of C4; NT 0: the config's own nt)"""
 import hashlib, json, math, os, subprocess, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")
@@ -12,7 +13,8 @@ def one(nt, lib):
     import numpy as np
     from mioc import native
     from mioc.synth import CONFIGS, make_inputs
-    cfg = CONFIGS["C4"]
+    cfg = CONFIGS[os.environ.get("PINF_CFG", "C4")]
+    nt = nt or cfg.nt
     lt = cfg.levels()
     _, df, uo = make_inputs(cfg, nt=nt, levels=lt)
     with native.Context(0) as ctx:
