@@ -984,24 +984,20 @@ template <int CB>
 __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, int nseg, int32_t *flags, int errw,
                                                       unsigned spin_limit) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  constexpr int CH = PINF_WS_CHUNK, NS = 2 * CH, HB = 8;  // ring of NS step slots of the HB rows below the segment
-  static_assert(CB >= 2 && CB <= HB, "k_pinf_recur_ws: 2 <= classes <= 8");
+  constexpr int CH = PINF_WS_CHUNK, HB = 8;  // steps per chunk; rows below the segment kept per step
+  static_assert(CB >= 2 && CB <= HB && CH % 16 == 0, "k_pinf_recur_ws shape");
   const int RP = P.RP, nt = P.nt, BWP = D.BWP;
   const int k = (int)blockIdx.x / nseg, q = (int)blockIdx.x - k * nseg;
   const int lane = (int)threadIdx.x, c = 64 * q + lane;
-  double *H = sm, *Kbuf = sm + (size_t)NS * HB;  // H: [NS][HB] rows 64q-8 .. 64q-1 of step s; Kbuf: [2][CH][BWP]
+  // Hbuf: [2][CH][HB] per chunk parity, entry j = rows 64q-8 .. 64q-1 of step lo+1+j (the steps the chunk [lo, hi]
+  // reads); Kbuf: [2][CH][BWP] the chunk's class rows, entry j = step lo+j
+  double *Hbuf = sm, *Kbuf = sm + (size_t)2 * CH * HB;
   const double *kmin = D.kmin + (size_t)k * nt * BWP;
   double *R = D.R + (size_t)k * nt * RP;
   int32_t *done = flags + (size_t)k * nseg, *err = flags + errw;
   const __amdgpu_buffer_rsrc_t Rr = __builtin_amdgcn_make_buffer_rsrc(R, 0, (int)((size_t)nt * RP * 8), 0x00020000);
-  auto slot = [&](int s) { return H + (size_t)(s % NS) * HB; };
-  // terminal row R_{n-1}[c'] = Kmin_{n-1}[c'] (c' < BWP), the rows below included (a function of kmin: no hand-off)
-  for (int e = lane; e < NS * HB; e += 64) H[e] = INFINITY;
-  if (lane < HB) {
-    const int cc = 64 * q - HB + lane;
-    slot(nt - 1)[lane] = cc >= 0 && cc < BWP ? kmin[(size_t)(nt - 1) * BWP + cc] : INFINITY;
-  }
-  double r = c < BWP ? kmin[(size_t)(nt - 1) * BWP + c] : INFINITY;  // this lane's row of R_{i+1}
+  for (int e = lane; e < 2 * CH * HB; e += 64) Hbuf[e] = INFINITY;  // (segment 0: rows below 0 stay +Inf)
+  double r = c < BWP ? kmin[(size_t)(nt - 1) * BWP + c] : INFINITY;  // this lane's row of R_{i+1}: terminal first
   R[(size_t)(nt - 1) * RP + c] = c <= P.B ? r : INFINITY;
   if (nt < 2) return;
   bool stop = false;
@@ -1018,78 +1014,127 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
     }
     return true;
   };
-  // rows 64q-8 .. 64q-1 of R_s for steps s in [s0, s1] into their ring slots: lanes 0-3, 16 bytes each (LDS-DMA, sc1)
-  auto halo = [&](int s0, int s1) {
+  // rows 64q-8 .. 64q-1 of R_s for steps s in [s0, s1] into entries s - s0 of `dst` (LDS-DMA, sc1): lane j of
+  // instruction t moves 16 bytes of step s0 + 16t + j/4, so one instruction covers 16 steps
+  const void *Rg = pi_uniform(R);
+  auto halo = [&](int s0, int s1, double *dst) {
     if (q == 0) return;
-    for (int s = s0; s <= s1; ++s) {
-      if (lane < HB / 2) {
-        const void *g = pi_uniform(R + (size_t)s * RP);
-        const unsigned m0 =
-            __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)slot(s)));
-        const unsigned voff = 8u * (unsigned)(64 * q - HB + 2 * lane);
+    for (int t = 0; s0 + 16 * t <= s1; ++t) {
+      const int s = s0 + 16 * t + (lane >> 2);
+      if (s <= s1) {
+        const unsigned m0 = __builtin_amdgcn_readfirstlane(
+            (unsigned)(uintptr_t)((__attribute__((address_space(3))) char *)(dst + (size_t)16 * HB * t)));
+        const unsigned voff = 8u * (unsigned)((size_t)s * RP + 64 * q - HB + 2 * (lane & 3));
         unsigned keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 sc1\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
-                     : "v"(voff), "s"(g), "s"(m0)
+                     : "v"(voff), "s"(Rg), "s"(m0)
                      : "memory");
       }
     }
   };
   int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
   glds_copy_asm(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, lane, 64);
-  if (lo + 1 <= nt - 2) {  // the first chunk's rows below (step nt-1's are computed above)
+  if (lane < HB) {  // the terminal step's rows below, entry nt-1-(lo+1) (a function of kmin: no hand-off)
+    const int cc = 64 * q - HB + lane;
+    Hbuf[(size_t)(nt - 1 - (lo + 1)) * HB + lane] = cc >= 0 && cc < BWP ? kmin[(size_t)(nt - 1) * BWP + cc] : INFINITY;
+  }
+  if (lo + 1 <= nt - 2) {  // the first chunk's rows below
     stop = !wait_below(lo + 1);
-    halo(lo + 1, nt - 2);
+    halo(lo + 1, nt - 2, Hbuf);
   }
   vm_drain();
+  // The hand-off without a drain stall: chunk [lo, hi]'s stores are published S steps into the next chunk, after a
+  // counted wait that leaves only the S newest stores in flight; the next chunk's DMAs are issued after that publish
+  // and completed at the chunk's end by a counted wait that leaves only the stores issued after them in flight.
+  constexpr int S = 8;
+  int prev_lo = -1;  // the previous chunk (published S steps into this one)
   for (int qq = 0; hi >= 0 && !stop; ++qq) {
-    const double *Kc = Kbuf + (size_t)(qq & 1) * CH * BWP;
-    const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1;
-    if (nhi >= 0) {  // the next chunk: its class rows, and (once the segment below has them) its rows below
-      glds_copy_asm(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((qq + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
-                    lane, 64);
-      if (!wait_below(nlo + 1)) {
-        stop = true;
-        break;
+    const double *Kc = Kbuf + (size_t)(qq & 1) * CH * BWP, *Hc = Hbuf + (size_t)(qq & 1) * CH * HB;
+    const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1, n = hi - lo + 1;
+    // publish the previous chunk, then the next chunk's class rows and (once the segment below has them) its rows below
+    auto mid = [&](bool counted) {
+      if (prev_lo >= 0) {
+        if (counted)
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // S: every store but this chunk's first S
+        else
+          vm_drain();
+        if (lane == 0) __hip_atomic_store(done + q, nt - 1 - prev_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      halo(nlo + 1, nhi + 1);
-    }
-    // the step's operands, read a step ahead (broadcast LDS reads, off the chain): class values Kmin_i[0 .. CB-1] and
-    // the fills R_{i+1}[64q - b], b = 1 .. CB-1
-    auto opnd = [&](double (&kv)[CB], double (&hv)[CB], int i) {
-      const double *kr = Kc + (size_t)(i - lo) * BWP;
-      const double *hr = slot(i + 1) + HB - CB;
-#pragma unroll
-      for (int b = 0; b < CB; ++b) {
-        kv[b] = kr[b];
-        hv[b] = hr[b];  // hv[CB-1-b'] = R_{i+1}[64q - 1 - b']
+      if (nhi >= 0) {  // (the poll first: its wait would otherwise also wait for the DMAs)
+        if (!wait_below(nlo + 1)) {
+          stop = true;
+          return;
+        }
+        glds_copy_asm(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((qq + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
+                      lane, 64);
+        halo(nlo + 1, nhi + 1, Hbuf + (size_t)((qq + 1) & 1) * CH * HB);
       }
     };
-    auto step = [&](int i, const double (&kv)[CB], const double (&hv)[CB], double (&kn)[CB], double (&hn)[CB]) {
+    static_assert(S == 8 && S % 4 == 0 && CH - S <= 63, "k_pinf_recur_ws: the counted waits");
+    // a step's operands (broadcast LDS reads, three steps ahead: off the chain): class values Kmin_i[0 .. CB-1] and the
+    // fills R_{i+1}[64q - b] (hv[CB - b], b = 1 .. CB-1)
+    struct Op {
+      double kv[CB], hv[CB];
+    };
+    auto opnd = [&](Op &o, int i) {
+      const double *kr = Kc + (size_t)(i - lo) * BWP, *hr = Hc + (size_t)(i - lo) * HB + HB - CB;
+#pragma unroll
+      for (int b = 0; b < CB; ++b) {
+        o.kv[b] = kr[b];
+        o.hv[b] = hr[b];
+      }
+    };
+    // step i with its operands `o`; `pre` (the previous step's, consumed) takes step i-3's -- unconditionally (step lo's
+    // again near the chunk's end): a conditional read would leave the compiler's LDS count unknown, and its wait for
+    // this step's operands would then also wait for the reads just issued
+    auto step = [&](int i, const Op &o, Op &pre) {
       asm volatile("" ::: "memory");
-      if (i > lo) opnd(kn, hn, i - 1);
-      double sft = r, m = kv[0] + r;
+      opnd(pre, i - 3 >= lo ? i - 3 : lo);
+      double sft = r, m = o.kv[0] + r;
 #pragma unroll
       for (int b = 1; b < CB; ++b) {
-        sft = ws_shr1<CB>(sft, hv[CB - b]);  // lane l: R_{i+1}[c - b]
-        m = pvmin(m, kv[b] + sft);
+        sft = ws_shr1<CB>(sft, o.hv[CB - b]);  // lane l: R_{i+1}[c - b]
+        m = pvmin(m, o.kv[b] + sft);
       }
       r = m;
       __builtin_amdgcn_raw_buffer_store_b64((pi_u32x2){(unsigned)__double2loint(r), (unsigned)__double2hiint(r)}, Rr,
                                             (unsigned)(((size_t)i * RP + c) * 8), 0, 16);
     };
-    double ka[CB], ha[CB], kb[CB], hb[CB];
-    opnd(ka, ha, hi);
-    for (int i = hi; i >= lo; i -= 2) {
-      step(i, ka, ha, kb, hb);
-      if (i - 1 >= lo) step(i - 1, kb, hb, ka, ha);
+    Op o0, o1, o2, o3;
+    opnd(o0, hi);
+    opnd(o1, hi - 1 >= lo ? hi - 1 : lo);
+    opnd(o2, hi - 2 >= lo ? hi - 2 : lo);
+    bool mid_done = false;
+    for (int i = hi; i >= lo; i -= 4) {
+      step(i, o0, o3);
+      if (i - 1 >= lo) step(i - 1, o1, o0);
+      if (i - 2 >= lo) step(i - 2, o2, o1);
+      if (i - 3 >= lo) step(i - 3, o3, o2);
+      if (n >= S && i - 3 == hi - S + 1) {  // S steps done (a multiple of the trip's four)
+        mid(true);
+        mid_done = true;
+        if (stop) break;
+      }
     }
-    // this chunk's rows have landed: publish its last step for the segment above
-    vm_drain();
-    if (lane == 0) __hip_atomic_store(done + q, nt - 1 - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (stop) break;
+    if (!mid_done) {  // a chunk of at most S steps (the last one, or nt small)
+      mid(false);
+      if (stop) break;
+    }
+    // the next chunk's DMAs have landed (only the stores issued after them may be in flight)
+    if (n == CH)
+      asm volatile("s_waitcnt vmcnt(56)" ::: "memory");  // CH - S
+    else
+      vm_drain();
+    prev_lo = lo;
     hi = nhi;
     lo = nlo;
   }
+  // the last chunk's rows have landed: publish it (segments above wait for it)
+  vm_drain();
+  if (!stop && prev_lo >= 0 && lane == 0)
+    __hip_atomic_store(done + q, nt - 1 - prev_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // rows c_from .. RP-1 of R (beyond the rows k_pinf_recur_xr / _mc compute, all above B): +Inf for every step
@@ -1129,7 +1174,7 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
     if (PINF_RECUR_WS && flags && segmented && D.BW >= 1 && D.BW <= 8 && D.BWP == 8 && nseg >= 2 &&
         P.K * nseg <= ncu && 64 * nseg <= P.RP && (size_t)P.nt * P.RP * 8 < (1ull << 31)) {
       const int errw = P.K * pinf_recur_segments(P);
-      const size_t lds = (size_t)(2 * PINF_WS_CHUNK * 8 + 2 * PINF_WS_CHUNK * D.BWP) * sizeof(double);
+      const size_t lds = (size_t)(2 * PINF_WS_CHUNK * 8 + 2 * PINF_WS_CHUNK * D.BWP) * sizeof(double);  // Hbuf, Kbuf
       const dim3 grid(P.K * nseg);
       switch (D.BW < 2 ? 2 : D.BW) {
         case 2: hipLaunchKernelGGL(k_pinf_recur_ws<2>, grid, dim3(64), lds, s, P, D, nseg, flags, errw, spin_limit); break;
