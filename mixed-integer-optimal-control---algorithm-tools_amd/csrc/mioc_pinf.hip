@@ -984,19 +984,22 @@ template <int CB>
 __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, int nseg, int32_t *flags, int errw,
                                                       unsigned spin_limit) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  constexpr int CH = PINF_WS_CHUNK, HB = 8;  // steps per chunk; rows below the segment kept per step
+  // steps per chunk; rows below the segment kept per step; padding entries in front of a chunk's operands (the reads
+  // three steps ahead run up to three steps past the chunk's last step: junk there, never used)
+  constexpr int CH = PINF_WS_CHUNK, HB = 8, EP = 4, CE = CH + EP;
   static_assert(CB >= 2 && CB <= HB && CH % 16 == 0, "k_pinf_recur_ws shape");
   const int RP = P.RP, nt = P.nt, BWP = D.BWP;
   const int k = (int)blockIdx.x / nseg, q = (int)blockIdx.x - k * nseg;
   const int lane = (int)threadIdx.x, c = 64 * q + lane;
-  // Hbuf: [2][CH][HB] per chunk parity, entry j = rows 64q-8 .. 64q-1 of step lo+1+j (the steps the chunk [lo, hi]
-  // reads); Kbuf: [2][CH][BWP] the chunk's class rows, entry j = step lo+j
-  double *Hbuf = sm, *Kbuf = sm + (size_t)2 * CH * HB;
+  // per chunk parity, entry EP + (i - lo) for step i of the chunk [lo, hi]: Hbuf [2][CE][HB] rows 64q-8 .. 64q-1 of
+  // step i+1; Kbuf [2][CE][BWP] Kmin_i
+  double *Hbuf = sm, *Kbuf = sm + (size_t)2 * CE * HB;
   const double *kmin = D.kmin + (size_t)k * nt * BWP;
   double *R = D.R + (size_t)k * nt * RP;
   int32_t *done = flags + (size_t)k * nseg, *err = flags + errw;
   const __amdgpu_buffer_rsrc_t Rr = __builtin_amdgcn_make_buffer_rsrc(R, 0, (int)((size_t)nt * RP * 8), 0x00020000);
-  for (int e = lane; e < 2 * CH * HB; e += 64) Hbuf[e] = INFINITY;  // (segment 0: rows below 0 stay +Inf)
+  for (int e = lane; e < 2 * CE * HB; e += 64) Hbuf[e] = INFINITY;  // (segment 0: rows below 0 stay +Inf)
+  for (int e = lane; e < 2 * CE * BWP; e += 64) Kbuf[e] = INFINITY;
   double r = c < BWP ? kmin[(size_t)(nt - 1) * BWP + c] : INFINITY;  // this lane's row of R_{i+1}: terminal first
   R[(size_t)(nt - 1) * RP + c] = c <= P.B ? r : INFINITY;
   if (nt < 2) return;
@@ -1033,24 +1036,28 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
       }
     }
   };
-  int hi = nt - 2, lo = hi - CH + 1 < 0 ? 0 : hi - CH + 1;
-  glds_copy_asm(kmin + (size_t)lo * BWP, Kbuf, (hi - lo + 1) * BWP * 8, lane, 64);
-  if (lane < HB) {  // the terminal step's rows below, entry nt-1-(lo+1) (a function of kmin: no hand-off)
+  auto kdst = [&](int par) { return Kbuf + (size_t)par * CE * BWP + EP * BWP; };
+  auto hdst = [&](int par) { return Hbuf + (size_t)par * CE * HB + EP * HB; };
+  // chunks aligned to multiples of CH from step 0: the first (top) one may be short, every later one is full
+  int lo = ((nt - 2) / CH) * CH, hi = nt - 2;
+  glds_copy_asm(kmin + (size_t)lo * BWP, kdst(0), (hi - lo + 1) * BWP * 8, lane, 64);
+  if (lane < HB) {  // the terminal step's rows below, read by step nt-2 (a function of kmin: no hand-off)
     const int cc = 64 * q - HB + lane;
-    Hbuf[(size_t)(nt - 1 - (lo + 1)) * HB + lane] = cc >= 0 && cc < BWP ? kmin[(size_t)(nt - 1) * BWP + cc] : INFINITY;
+    hdst(0)[(size_t)(hi - lo) * HB + lane] = cc >= 0 && cc < BWP ? kmin[(size_t)(nt - 1) * BWP + cc] : INFINITY;
   }
   if (lo + 1 <= nt - 2) {  // the first chunk's rows below
     stop = !wait_below(lo + 1);
-    halo(lo + 1, nt - 2, Hbuf);
+    halo(lo + 1, nt - 2, hdst(0));
   }
   vm_drain();
   // The hand-off without a drain stall: chunk [lo, hi]'s stores are published S steps into the next chunk, after a
   // counted wait that leaves only the S newest stores in flight; the next chunk's DMAs are issued after that publish
   // and completed at the chunk's end by a counted wait that leaves only the stores issued after them in flight.
   constexpr int S = 8;
+  static_assert(S == 8 && CH - S <= 63, "k_pinf_recur_ws: the counted waits");
   int prev_lo = -1;  // the previous chunk (published S steps into this one)
   for (int qq = 0; hi >= 0 && !stop; ++qq) {
-    const double *Kc = Kbuf + (size_t)(qq & 1) * CH * BWP, *Hc = Hbuf + (size_t)(qq & 1) * CH * HB;
+    const double *Kc = Kbuf + (size_t)(qq & 1) * CE * BWP, *Hc = Hbuf + (size_t)(qq & 1) * CE * HB;
     const int nhi = lo - 1, nlo = nhi - CH + 1 < 0 ? 0 : nhi - CH + 1, n = hi - lo + 1;
     // publish the previous chunk, then the next chunk's class rows and (once the segment below has them) its rows below
     auto mid = [&](bool counted) {
@@ -1066,31 +1073,29 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
           stop = true;
           return;
         }
-        glds_copy_asm(kmin + (size_t)nlo * BWP, Kbuf + (size_t)((qq + 1) & 1) * CH * BWP, (nhi - nlo + 1) * BWP * 8,
-                      lane, 64);
-        halo(nlo + 1, nhi + 1, Hbuf + (size_t)((qq + 1) & 1) * CH * HB);
+        glds_copy_asm(kmin + (size_t)nlo * BWP, kdst((qq + 1) & 1), (nhi - nlo + 1) * BWP * 8, lane, 64);
+        halo(nlo + 1, nhi + 1, hdst((qq + 1) & 1));
       }
     };
-    static_assert(S == 8 && S % 4 == 0 && CH - S <= 63, "k_pinf_recur_ws: the counted waits");
     // a step's operands (broadcast LDS reads, three steps ahead: off the chain): class values Kmin_i[0 .. CB-1] and the
-    // fills R_{i+1}[64q - b] (hv[CB - b], b = 1 .. CB-1)
+    // fills R_{i+1}[64q - b] (hv[CB - b], b = 1 .. CB-1); i >= lo - 3 (the padding entries)
     struct Op {
       double kv[CB], hv[CB];
     };
     auto opnd = [&](Op &o, int i) {
-      const double *kr = Kc + (size_t)(i - lo) * BWP, *hr = Hc + (size_t)(i - lo) * HB + HB - CB;
+      const double *kr = Kc + (size_t)(i - lo + EP) * BWP, *hr = Hc + (size_t)(i - lo + EP) * HB + HB - CB;
 #pragma unroll
       for (int b = 0; b < CB; ++b) {
         o.kv[b] = kr[b];
         o.hv[b] = hr[b];
       }
     };
-    // step i with its operands `o`; `pre` (the previous step's, consumed) takes step i-3's -- unconditionally (step lo's
-    // again near the chunk's end): a conditional read would leave the compiler's LDS count unknown, and its wait for
-    // this step's operands would then also wait for the reads just issued
+    // step i with its operands `o`; `pre` (the previous step's, consumed) takes step i-3's -- unconditionally: a
+    // conditional read would leave the compiler's LDS count unknown, and its wait for this step's operands would then
+    // also wait for the reads just issued
     auto step = [&](int i, const Op &o, Op &pre) {
       asm volatile("" ::: "memory");
-      opnd(pre, i - 3 >= lo ? i - 3 : lo);
+      opnd(pre, i - 3);
       double sft = r, m = o.kv[0] + r;
 #pragma unroll
       for (int b = 1; b < CB; ++b) {
@@ -1103,30 +1108,32 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
     };
     Op o0, o1, o2, o3;
     opnd(o0, hi);
-    opnd(o1, hi - 1 >= lo ? hi - 1 : lo);
-    opnd(o2, hi - 2 >= lo ? hi - 2 : lo);
-    bool mid_done = false;
-    for (int i = hi; i >= lo; i -= 4) {
-      step(i, o0, o3);
-      if (i - 1 >= lo) step(i - 1, o1, o0);
-      if (i - 2 >= lo) step(i - 2, o2, o1);
-      if (i - 3 >= lo) step(i - 3, o3, o2);
-      if (n >= S && i - 3 == hi - S + 1) {  // S steps done (a multiple of the trip's four)
-        mid(true);
-        mid_done = true;
-        if (stop) break;
+    opnd(o1, hi - 1);
+    opnd(o2, hi - 2);
+    if (n == CH) {  // a full chunk: groups of four steps, no guards
+      for (int i = hi; i >= lo; i -= 4) {
+        step(i, o0, o3);
+        step(i - 1, o1, o0);
+        step(i - 2, o2, o1);
+        step(i - 3, o3, o2);
+        if (i - 3 == hi - S + 1) {  // S steps done
+          mid(true);
+          if (stop) break;
+        }
       }
-    }
-    if (stop) break;
-    if (!mid_done) {  // a chunk of at most S steps (the last one, or nt small)
+      if (stop) break;
+      asm volatile("s_waitcnt vmcnt(56)" ::: "memory");  // CH - S: the next chunk's DMAs have landed
+    } else {  // the first chunk, short
+      for (int i = hi; i >= lo; i -= 4) {
+        step(i, o0, o3);
+        if (i - 1 >= lo) step(i - 1, o1, o0);
+        if (i - 2 >= lo) step(i - 2, o2, o1);
+        if (i - 3 >= lo) step(i - 3, o3, o2);
+      }
       mid(false);
       if (stop) break;
-    }
-    // the next chunk's DMAs have landed (only the stores issued after them may be in flight)
-    if (n == CH)
-      asm volatile("s_waitcnt vmcnt(56)" ::: "memory");  // CH - S
-    else
       vm_drain();
+    }
     prev_lo = lo;
     hi = nhi;
     lo = nlo;
@@ -1174,7 +1181,7 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
     if (PINF_RECUR_WS && flags && segmented && D.BW >= 1 && D.BW <= 8 && D.BWP == 8 && nseg >= 2 &&
         P.K * nseg <= ncu && 64 * nseg <= P.RP && (size_t)P.nt * P.RP * 8 < (1ull << 31)) {
       const int errw = P.K * pinf_recur_segments(P);
-      const size_t lds = (size_t)(2 * PINF_WS_CHUNK * 8 + 2 * PINF_WS_CHUNK * D.BWP) * sizeof(double);  // Hbuf, Kbuf
+      const size_t lds = (size_t)2 * (PINF_WS_CHUNK + 4) * (8 + D.BWP) * sizeof(double);  // Hbuf, Kbuf
       const dim3 grid(P.K * nseg);
       switch (D.BW < 2 ? 2 : D.BW) {
         case 2: hipLaunchKernelGGL(k_pinf_recur_ws<2>, grid, dim3(64), lds, s, P, D, nseg, flags, errw, spin_limit); break;
