@@ -1054,7 +1054,7 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
   // counted wait that leaves only the S newest stores in flight; the next chunk's DMAs are issued after that publish
   // and completed at the chunk's end by a counted wait that leaves only the stores issued after them in flight.
   constexpr int S = 8;
-  static_assert(S == 8 && CH - S <= 63, "k_pinf_recur_ws: the counted waits");
+  static_assert(S == 8 && (CH == 64 || CH == 32), "k_pinf_recur_ws: the counted waits");
   int prev_lo = -1;  // the previous chunk (published S steps into this one)
   for (int qq = 0; hi >= 0 && !stop; ++qq) {
     const double *Kc = Kbuf + (size_t)(qq & 1) * CE * BWP, *Hc = Hbuf + (size_t)(qq & 1) * CE * HB;
@@ -1122,7 +1122,10 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
         }
       }
       if (stop) break;
-      asm volatile("s_waitcnt vmcnt(56)" ::: "memory");  // CH - S: the next chunk's DMAs have landed
+      if constexpr (CH == 64)
+        asm volatile("s_waitcnt vmcnt(56)" ::: "memory");  // CH - S: the next chunk's DMAs have landed
+      else
+        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
     } else {  // the first chunk, short
       for (int i = hi; i >= lo; i -= 4) {
         step(i, o0, o3);
