@@ -414,6 +414,14 @@ int run_bellman(mioc_ctx *ctx) {
       if (S > 1 && bmax > ctx->pyr.n[0] + ctx->pyr.n[1] - 2) S = 1;
       const bool v2 = S >= 1 && fsep2_plan(ctx->pyr, ctx->B, S, &plan);
       ctx->last_fsep_seg = v2 ? S : 0;
+      if (v2 && S > 1) {
+        // segments with at most one workgroup per CU to go round: reserve more than half a CU's LDS, so that the
+        // dispatcher cannot put two segments on one CU while another CU idles (the segments run as one pipeline,
+        // and a shared CU slows all of them: the 128-restart shard ran 17 - 28 ms from run to run)
+        int ncu = 0;
+        HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        if ((size_t)K * (size_t)S <= (size_t)ncu) plan.lds = std::max<size_t>(plan.lds, 82 * 1024);
+      }
       if (v2) ctx->occupancy = fsep2_blocks_per_cu(ctx->pyr, plan);
       if (v2 && S > 1) {
         const int NB = 8, SM = ctx->pyr.n[0] + ctx->pyr.n[1] - 2;
