@@ -1503,6 +1503,9 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
         winK = readlane_f64(km, winb);
       } else {
         // exact scan of row c' of Φ_j: first rank s with fl(K_l + Φ_j[c', s]) == Φ_i[c, l]
+        // (kf used on this path too: otherwise the compiler sinks its LDS read into the branch above, one more LDS
+        // round trip on the walk's chain every step)
+        asm volatile("" ::"v"(kf));
         ++fallbacks;
         const double *dfj = dfk + (size_t)j * M;
         const double *uoj = uok + (size_t)j * M;
