@@ -332,9 +332,9 @@ def roofline_of(res):
         ub = 1 if L <= 256 else 2
         bytes_per_launch = K * (B + 1) * L * (8 + 8 + ub)
         ops = 2.0 * K * ncand_step  # one v_add_f64 + one v_min_f64 per candidate
-    elif name in ("k_sdt_step", "k_sdt_run", "k_sdt_pair"):
+    elif name in ("k_sdt_step", "k_sdt_run"):
         # the same algorithmic traffic as the reference DP step: front in + front out + compact U, per step;
-        # k_sdt_run / k_sdt_pair are one persistent launch over all nt - 1 steps
+        # k_sdt_run is one persistent launch over all nt - 1 steps
         steps = (nt - 1) if name != "k_sdt_step" else 1
         bytes_per_launch = steps * K * (B + 1) * L * (8 + 8 + 2)
         # per pass and 8-point line: 14 merges (7 forward, 7 backward), each add + min + sub + cmp (4 FP64 ops) and the

@@ -80,9 +80,7 @@ extern "C" {
 #define MIOC_OPT_PINF_WALK 8 /* p=Inf backtrack: 0 (default) the segmented walk -- one subproblem's path spread
                                 over many workgroups -- for batches of at most 64 subproblems with >= 512 steps,
                                 else one serial walk per subproblem; 1: segmented walk forced; -1: serial walk */
-#define MIOC_OPT_SDT_PAIR 9 /* persistent separable transform on 8^4 grids: two workgroups per budget row (two row
-                               items in flight per CU; K·B <= CUs) of 256 threads (1) or 512 threads (2); 0
-                               (default): one workgroup per row */
+/* option 9 (a two-workgroups-per-row separable driver, opt-in and slower) was removed in round 6: MIOC_EINVAL */
 
 typedef struct mioc_ctx mioc_ctx;
 
@@ -291,7 +289,7 @@ int32_t mioc_last_algo(mioc_ctx *ctx);
  * by the exact scan, or for the U-table walks (generic, pyramid) the run-ahead rounds taken (each round
  * settles up to 64 steps), [3] internal consistency failures (must be 0); [4..7] pyramid internals: rows whose
  * value hash overflowed, targets whose value was not found, values flagged as colliding (after a separable-transform
- * DP, [4] instead counts the persistent driver's rows whose predicted stamp scale missed (stamped twice), and [6] counts this context's persistent DPs redone with per-step launches: the grid does not fit, or
+ * DP, [4] instead counts the persistent driver's rows whose write-after-read wait on the rows above was armed (a staging buffer reused while later rows may still read it), and [6] counts this context's persistent DPs redone with per-step launches: the grid does not fit, or
  * a dependency wait timed out -- 0 on a healthy run; after a fused separable DP, the segmented launches redone with
  * one workgroup per subproblem); [7] fused DP: resident workgroups per CU (occupancy query); [8] fused separable DP:
  * row segments per subproblem (0: the one-lane-per-row kernel); [9] p=Inf segmented walk: subproblems whose path

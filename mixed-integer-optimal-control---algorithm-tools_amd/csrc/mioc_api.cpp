@@ -104,7 +104,6 @@ void free_all(mioc_ctx *ctx) {
                   ctx->pinf.kabs, ctx->pinf.ftab, ctx->pinf.fseg, ctx->pinf.fneed,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
                   ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm, ctx->d_same2, ctx->d_strad,
-                  ctx->d_pack,  ctx->d_pseam,  ctx->d_phead,
                   ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own, ctx->d_ode_state};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -282,8 +281,7 @@ int run_bellman(mioc_ctx *ctx) {
     // precomputed (k_sdt_chain, k_sdt_row0), NB staging buffers
     const size_t run_lds = sdt_lds_bytes(ctx->pyr);
     int nwg = 0;
-    bool persist = false, pair = false;
-    const int pair_t = ctx->opt_sdt_pair == 2 ? 512 : 256;  // k_sdt_pair's workgroup size
+    bool persist = false;
     // (B + 1)·L·8 < 2^31: the persistent kernel addresses a staging block with 32-bit buffer offsets
     // ... and every b̃ within the kernel's dependency window (7 per dimension: u_old on the level grid); a u_old
     // off the grid reaches rows further back than the window waits for, so those problems take per-step launches
@@ -291,14 +289,12 @@ int run_bellman(mioc_ctx *ctx) {
         s_stride * sizeof(double) < (1ull << 31) && bmax <= 7 * ctx->pyr.M && !ctx->force_steps) {
       int ncu = 0;
       HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-      // 8^4 grids with every budget row on its own CU: two workgroups per row (k_sdt_pair, mioc_sdt2.hip); else one
-      // workgroup per CU over contiguous row chunks (k_sdt_run)
-      pair = ctx->opt_sdt_pair && sdt_pair_supported(ctx->pyr, (int)K, ctx->B, ncu, sdt_pair_blocks_per_cu(pair_t));
+      // one workgroup per CU over contiguous row chunks (k_sdt_run)
       const int bpc = std::min(sdt_run_blocks_per_cu(ctx->pyr, run_lds), 1);  // one row workgroup per CU
       const size_t slots = (size_t)ncu * (size_t)std::max(bpc, 0);
       const size_t per_k = std::min<size_t>((size_t)ctx->B, K ? slots / K : 0);  // workgroups per subproblem
-      nwg = pair ? (int)(2 * K * (size_t)ctx->B) : (int)(per_k * K);
-      persist = pair || per_k >= 1;
+      nwg = (int)(per_k * K);
+      persist = per_k >= 1;
     }
     // persistent layout: per subproblem NB staging buffers of (B+1)·L, then row 0 of every step (nt·L), one region
     // addressed by one buffer resource (< 4 GiB); per-step layout: two buffers of K blocks of (B+1)·L
@@ -312,8 +308,8 @@ int run_bellman(mioc_ctx *ctx) {
     const size_t kstride = persist ? (size_t)nbuf * s_stride + nt * L : s_stride;
     if (persist && kstride * sizeof(double) >= (1ull << 32)) persist = false;  // (then also kstride = s_stride)
     const size_t ks = persist ? kstride : s_stride;
-    // flags: done and loaded per row (k_sdt_run) or per row and step parity (k_sdt_pair), then the error word
-    const size_t nflag = (pair ? 4 : 2) * K * (size_t)(ctx->B + 1);
+    // flags: done and loaded per row, then the error word
+    const size_t nflag = 2 * K * (size_t)(ctx->B + 1);
     const size_t runflag_bytes = ((nflag + 1) * sizeof(int32_t) + 15) / 16 * 16;
     if (persist) {
       int rcf = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, runflag_bytes, "persistent row flags");
@@ -331,15 +327,8 @@ int run_bellman(mioc_ctx *ctx) {
     if (rc) return rc;
     rc = grow(ctx, &ctx->d_perm, &ctx->perm_cap, K * nt * L * sizeof(uint32_t), "sphere orders");
     if (!rc) rc = grow(ctx, &ctx->d_same2, &ctx->same2_cap, K * nt * sizeof(int32_t), "sphere-order reuse flags");
-    const bool seams = persist && !pair && sdt_seam_lists(ctx->pyr);
+    const bool seams = persist && sdt_seam_lists(ctx->pyr);
     if (!rc && seams) rc = grow(ctx, &ctx->d_strad, &ctx->strad_cap, K * nt * 8 * 32 * sizeof(uint16_t), "seam lists");
-    if (!rc && pair) rc = grow(ctx, &ctx->d_pack, &ctx->pack_cap, K * nt * (L / 2) * sizeof(uint32_t), "packed orders");
-    if (!rc && pair)
-      rc = grow(ctx, &ctx->d_pseam, &ctx->pseam_cap, K * nt * sdt_pair_seam_words(pair_t) * sizeof(uint32_t),
-                "packed seams");
-    if (!rc && pair)
-      rc = grow(ctx, &ctx->d_phead, &ctx->phead_cap, K * (size_t)(ctx->B + 1) * nt * (pair_t / 64) * sizeof(double),
-                "row head parts");
     if (rc) return rc;
     double *st[2] = {ctx->d_stage, ctx->d_stage + K * s_stride};
     double *term = persist ? ctx->d_stage + ((nt - 1) % nbuf) * s_stride : st[(nt - 1) & 1];
@@ -350,25 +339,13 @@ int run_bellman(mioc_ctx *ctx) {
       // the whole DP as one persistent launch: rows handed between resident workgroups by flags
       HIP_TRY(ctx, launch_sdt_prep(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_chain, ctx->d_stage, ks,
                                    (size_t)nbuf * s_stride, (uint16_t *)ctx->d_U, uu_stride_k));
-      if (pair)
-        HIP_TRY(ctx, launch_sdt_pack(ctx->stream, P, ctx->d_perm, ctx->d_pack, ctx->d_pseam, ctx->d_counters, pair_t));
       HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, runflag_bytes, ctx->stream));
-      // head values not yet written: all-ones (a NaN no DP value takes)
-      if (pair)
-        HIP_TRY(ctx, hipMemsetAsync(ctx->d_phead, 0xFF, K * (size_t)(ctx->B + 1) * nt * (pair_t / 64) * sizeof(double),
-                                    ctx->stream));
-      ctx->last_sdt_kernel = pair ? "k_sdt_pair" : "k_sdt_run";
-      ev_begin(ctx, 0, ctx->last_sdt_kernel);
+      ev_begin(ctx, 0, "k_sdt_run");
       // (the grid is nwg <= CUs x resident workgroups per CU by construction above; a wait that never ends anyway --
       // another process holding CUs -- is caught by the spin limit and redone per step by check_run)
-      if (pair)
-        HIP_TRY(ctx, launch_sdt_pair(ctx->stream, P, Lv, ctx->pyr, ctx->d_pack, ctx->d_pseam, ctx->d_stage, ks, nbuf,
-                                     (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags,
-                                     ctx->d_phead, ctx->spin_limit, pair_t));
-      else
-        HIP_TRY(ctx, launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_same2, ctx->d_strad, ctx->d_stage,
-                                    ks, nbuf, (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags, nwg,
-                                    ctx->spin_limit, run_lds));
+      HIP_TRY(ctx, launch_sdt_run(ctx->stream, P, Lv, ctx->pyr, ctx->d_perm, ctx->d_same2, ctx->d_strad, ctx->d_stage,
+                                  ks, nbuf, (uint16_t *)ctx->d_U, uu_stride_k, ctx->d_counters, ctx->d_runflags, nwg,
+                                  ctx->spin_limit, run_lds));
       ev_end(ctx, 0, 1);
       HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + nflag, sizeof(int32_t),
                                   hipMemcpyDeviceToHost, ctx->stream));
@@ -725,11 +702,6 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
   if (option == MIOC_OPT_SDT_BUFFERS) {
     if (value < 4 || value > kSdtMaxBuffers) return fail(ctx, MIOC_EINVAL, "staging buffers must be in [4, 256]");
     ctx->opt_nb = (int)value;
-    return MIOC_OK;
-  }
-  if (option == MIOC_OPT_SDT_PAIR) {
-    if (value < 0 || value > 2) return fail(ctx, MIOC_EINVAL, "SDT pair option must be 0, 1 or 2");
-    ctx->opt_sdt_pair = (int)value;
     return MIOC_OK;
   }
   if (option == MIOC_OPT_PINF_WALK) {

@@ -138,20 +138,6 @@ hipError_t launch_sdt_run(hipStream_t s, const ProblemDev &P, const LevelsDev &L
                           size_t uu_stride_k, int32_t *counters, int32_t *flags, int nwg, unsigned spin_limit,
                           size_t lds);
 int sdt_run_blocks_per_cu(const PyrGeom &G, size_t lds);
-// the two-workgroups-per-row persistent driver (mioc_sdt2.hip, 8^4 grids): the sphere orders packed per position pair
-// ([K][nt][2048] uint32 pair words, [K][nt][4][32] seam words), then the DP; flags [K][B+1][2] done, [K][B+1][2]
-// loaded, err (zeroed by the caller)
-bool sdt_pair_supported(const PyrGeom &G, int K, int B, int ncu, int bpc);
-// threads: 256 (16 values per lane) or 512 (8 per lane, four waves per SIMD)
-size_t sdt_pair_lds_bytes(int threads);
-int sdt_pair_blocks_per_cu(int threads);
-int sdt_pair_seam_words(int threads);  // seam words per step
-hipError_t launch_sdt_pack(hipStream_t s, const ProblemDev &P, const uint32_t *perm, uint32_t *pack, uint32_t *seams,
-                           int32_t *counters, int threads);
-hipError_t launch_sdt_pair(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G,
-                           const uint32_t *pack, const uint32_t *seams, double *S, size_t kstride, int NB, uint16_t *UU,
-                           size_t uu_stride_k, int32_t *counters, int32_t *flags, double *heads, unsigned spin_limit,
-                           int threads);
 hipError_t launch_stage_argmin0(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm,
                                 const double *S0, size_t s_stride, int Bu, Start *start);
 hipError_t launch_stage_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint16_t *UU,
@@ -322,15 +308,6 @@ struct mioc_ctx {
   size_t same2_cap = 0;
   uint16_t *d_strad = nullptr;     // [K][nt][8][32] seam-straddling pairs per wave (k_sdt_run's 8-wave layout)
   size_t strad_cap = 0;
-  uint32_t *d_pack = nullptr;      // [K][nt][2048] packed position pairs (k_sdt_pair)
-  size_t pack_cap = 0;
-  uint32_t *d_pseam = nullptr;     // [K][nt][4][32] seam words (k_sdt_pair)
-  size_t pseam_cap = 0;
-  double *d_phead = nullptr;       // [K][B+1][nt][waves] head-value parts handed between a row's two workgroups
-  size_t phead_cap = 0;
-  int opt_sdt_pair = 0;            // 8^4 persistent separable DP: two workgroups per row (MIOC_OPT_SDT_PAIR, opt-in:
-                                   // 1 = 256 threads each, 2 = 512)
-  const char *last_sdt_kernel = "";  // the persistent separable kernel of the last DP (k_sdt_pair / k_sdt_run)
   size_t perm_cap = 0;
   bool opt_persist = true;         // separable transform: one persistent launch (MIOC_OPT_PERSIST)
   bool force_steps = false;        // redo of a persistent DP whose waits timed out: per-step launches

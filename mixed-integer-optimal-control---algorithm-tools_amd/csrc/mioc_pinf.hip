@@ -1111,17 +1111,20 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
     opnd(o1, hi - 1);
     opnd(o2, hi - 2);
     if (n == CH) {  // a full chunk: groups of four steps, no guards
-      for (int i = hi; i >= lo; i -= 4) {
+      // fully unrolled, so that the vector-memory operations between the counted waits are one straight line of
+      // stores (tests/test_isa_guard.py checks the counts on the compiled code)
+      auto group = [&](int i) {
         step(i, o0, o3);
         step(i - 1, o1, o0);
         step(i - 2, o2, o1);
         step(i - 3, o3, o2);
-        if (i - 3 == hi - S + 1) {  // S steps done
-          mid(true);
-          if (stop) break;
-        }
-      }
+      };
+#pragma unroll
+      for (int g = 0; g < S / 4; ++g) group(hi - 4 * g);
+      mid(true);  // S steps done
       if (stop) break;
+#pragma unroll
+      for (int g = S / 4; g < CH / 4; ++g) group(hi - 4 * g);
       if constexpr (CH == 64)
         asm volatile("s_waitcnt vmcnt(56)" ::: "memory");  // CH - S: the next chunk's DMAs have landed
       else

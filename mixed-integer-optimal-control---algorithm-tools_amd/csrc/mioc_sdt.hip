@@ -290,13 +290,20 @@ struct SdtShared {
   int redj[SD_COOP * NW];
   double rmn[NW], rmx[NW];
   int rnv[NW];
-  int nlist;
+  // by row parity (sdt_body's `par`): targets listed for the exact scan, and whether a near tie was met anywhere in
+  // the row's first (non-counting) transform.  Each row resets the other parity's slots after its first barrier: the
+  // row before has read them before that barrier, the row after writes them after its own first barrier.
+  int nlist[2];
+  int redo[2];
   int stop;  // persistent kernel: a dependency wait timed out
   unsigned long long stamp[16];  // diagnostic build: phase clocks of the current row
   int nsp;   // sparse rows: the finite sources (rank, Ψ)
   int spj[SD_SPARSE];
   double spv[SD_SPARSE];
-  int cnt[2];  // targets sent to the exact scan (near ties, direct rows); flushed to the global counters [0], [1]
+  // targets sent to the exact scan (near ties, direct rows), flushed to the global counters [0], [1]; (persistent
+  // driver) rows whose write-after-read wait on the rows above was armed (staging-buffer reuse), flushed to [4]; rows
+  // whose transform met a near tie and was redone counting them, flushed to [5]
+  int cnt[4];
 };
 
 template <int M>
@@ -377,8 +384,8 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
                                          const uint32_t *pout,
                                          double *Sout, uint16_t *UU, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
                                          unsigned char *sds, Hooks &h, const double *__restrict__ df_all,
-                                         const double *__restrict__ uo_all, unsigned smask = 0, int srank = -1,
-                                         double xs = 0.0) {
+                                         const double *__restrict__ uo_all, int par, unsigned smask = 0,
+                                         int srank = -1, double xs = 0.0) {
   constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
   double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
   double *dtv = psi + L;                                // [L] transform values (swizzled)
@@ -431,7 +438,6 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     nv += __popcll(__ballot(in));
   }
 
-  if (tid == 0) sh.nlist = 0;
   // ---- the binade: values base + (Ψ - ref)/β + d lie in [base, 2·base), grid g = 2^18 ulp ----------------
   // for Ψ in [lo, hi] (ref = lo): every quantity of the certified transform follows from the range alone
   const double inv = Lv.inv_beta;  // fl(1/β), host-computed
@@ -465,12 +471,19 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   // ---- one pass of the transform: forward and backward sweep along the 8 levels of dimension m, unit step 1.0;
   // this thread's line is read from and (but for the last pass) written back to the swizzled LDS values ---------
   double o[8];
-  auto pass = [&](int m) {
+  // the smallest |a - b| over every merge of the row's first transform (per lane): a near tie anywhere (<= tol) sends
+  // the whole row through the counting transform again (below); +Inf - +Inf is NaN, which v_min_f64 ignores
+  double dmin = INFINITY;
+  // COUNT = false: each merge is add, min, and the |a - b| folded into dmin off the value chain (the first transform);
+  // COUNT = true: the certified merge with the near-tie count in the payload (sd_merge), pass 0 reading the raw Ψ by
+  // rank (the redo: dtv holds the first transform's values by then)
+  auto pass = [&](int m, auto count_tag) {
+    constexpr bool COUNT = decltype(count_tag)::value;
     int pos[8];
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
       pos[x] = sd_swz(sd_rank((int)threadIdx.x, m, x));  // tid-only: hoisted out of the row loop
-      o[x] = dtv[pos[x]];
+      o[x] = (COUNT && m == 0) ? psi[sd_rank((int)threadIdx.x, 0, x)] : dtv[pos[x]];
     }
     if (m == 0) {  // the raw Ψ of ranks 8·tid + x (written with Ψ by rank): stamp them here
 #pragma unroll
@@ -479,13 +492,77 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     // in place: after the forward sweep o[x] covers the sources at <= x; a backward merge of o[x] with
     // o[x+1] + 1 compares a source at <= x with itself shifted by >= 2, never within tol, so every
     // flagged tie is between two distinct sources (as in a merge of disjoint sets)
+    auto merge = [&](double a, double b) {
+      if constexpr (COUNT) {
+        return sd_merge(a, b, tol);
+      } else {
+        dmin = sd_min_abs(dmin, a - b);
+        return sd_min(a, b);
+      }
+    };
 #pragma unroll
-    for (int x = 1; x < 8; ++x) o[x] = sd_merge(o[x], o[x - 1] + 1.0, tol);
+    for (int x = 1; x < 8; ++x) o[x] = merge(o[x], o[x - 1] + 1.0);
 #pragma unroll
-    for (int x = 6; x >= 0; --x) o[x] = sd_merge(o[x], o[x + 1] + 1.0, tol);
+    for (int x = 6; x >= 0; --x) o[x] = merge(o[x], o[x + 1] + 1.0);
     if (m + 1 < M) {
 #pragma unroll
       for (int x = 0; x < 8; ++x) dtv[pos[x]] = o[x];
+    }
+  };
+  auto passes = [&](auto count_tag) {
+    // the lines of passes 0 .. M-2 keep the top grid coordinate (rank bits 3(M-1)..), which is the wave index (the
+    // swizzle leaves those bits alone), so a wave reads only what it wrote itself; only the last pass, which runs
+    // along the top coordinate, needs every wave's values
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      pass(m, count_tag);
+      if (m + 2 < M)
+        sd_wave_sync();
+      else if (m + 1 < M)
+        sd_bar();
+      SD_STAMP(3 + m);
+    }
+  };
+  // the certified winners of the transform in o[] (FLAG: the counting transform, near ties listed for the exact scan)
+  auto winners = [&](auto flag_tag) {
+    constexpr bool FLAG = decltype(flag_tag)::value;
+    unsigned listed = 0;
+    int jx[8];
+    double pv[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) jx[x] = (__double2loint(o[x]) >> SD_CB) & ((1 << SD_RB) - 1);  // +Inf: payload 0
+#pragma unroll
+    for (int x = 0; x < 8; ++x) pv[x] = psi[jx[x]];  // branch-free: the eight winners' Ψ reads issue together
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const int r = tid | (x << (3 * (M - 1))), j = jx[x];
+      const bool fin = (valid >> x & 1) && o[x] < INFINITY;
+      const bool flg = FLAG && (__double2loint(o[x]) & SD_CNT) != 0;
+      // d(l, j*) exactly: an unflagged finite o[x] is V_j* + d with V_j* = the stamp of Ψ_j* (the same expression
+      // as the stamping above, payload j*), every term exact in the binade (garbage, unused, otherwise)
+      const double dd = o[x] - stamp(pv[x], j);
+      const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
+      const double val = (t1 + beta * dd) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
+      if constexpr (FLAG) {
+        listed |= (unsigned)(fin && flg) << x;
+        uu[r] = (uint16_t)(fin && !flg ? j : 0xFFFF);  // 0xFFFF: unwritten (Φ = +Inf) or not yet known (listed)
+        outv[r] = fin ? (flg ? __longlong_as_double(0x7FF8000000000000ll) : val) : INFINITY;
+      } else {
+        uu[r] = (uint16_t)(fin ? j : 0xFFFF);  // 0xFFFF: unwritten (Φ = +Inf)
+        outv[r] = fin ? val : INFINITY;
+      }
+    }
+    return listed;
+  };
+  auto list_targets = [&](unsigned listed) {
+    if (listed) {
+      int e = atomicAdd(&sh.nlist[par], __popc(listed));
+#pragma unroll
+      for (int x = 0; x < 8; ++x)
+        if (listed >> x & 1) {
+          if (e < SD_LCAP) list[e] = (uint16_t)(tid | (x << (3 * (M - 1))));
+          ++e;
+        }
     }
   };
   int nf;
@@ -524,6 +601,7 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
       sh.rnv[w] = nv;
     }
     sd_bar();  // every wave has consumed its loads of S_{i+1} (their values are in LDS)
+    if (tid == 0) sh.nlist[par ^ 1] = sh.redo[par ^ 1] = 0;  // the next row's slots
     h.early();
     {
       // every wave's statistics in one batch of LDS reads and one wait (the compiler interleaved them with the
@@ -589,46 +667,15 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   const bool transform = !direct && !empty && !sparse;  // uniform
   // no stamp phase (pass 0 stamps): every wave is past its last read of `pin` (the first barrier)
   h.go();
-  if (transform) {
-    // ---- the M passes: the lines of passes 0 .. M-2 keep the top grid coordinate (rank bits 3(M-1)..), which is the
-    // wave index (the swizzle leaves those bits alone), so a wave reads only what it wrote itself; only the last pass,
-    // which runs along the top coordinate, needs every wave's values
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      pass(m);
-      if (m + 2 < M)
-        sd_wave_sync();
-      else if (m + 1 < M)
-        sd_bar();
-      SD_STAMP(3 + m);
-    }
-  }
+  if (transform) passes(std::false_type{});  // the M passes, near ties folded into dmin
 
   if (!empty) {
-    // ---- targets: R(l, j*) for a certified winner; the others are listed for the exact scan (their
-    // output slot holds NaN until the scan fills it) ----------------------------------------------------
+    // ---- targets: R(l, j*) for a certified winner (no merge of the row's transform came within tol: every winner beats
+    // every other source by more than tol); a row that met a near tie anywhere is redone below, counting them
     unsigned listed = 0;
-    if (!direct && !sparse) {  // branch-free: the eight winners' Ψ reads issue together
-      int jx[8];
-      double pv[8];
-#pragma unroll
-      for (int x = 0; x < 8; ++x) jx[x] = (__double2loint(o[x]) >> SD_CB) & ((1 << SD_RB) - 1);  // +Inf: payload 0
-#pragma unroll
-      for (int x = 0; x < 8; ++x) pv[x] = psi[jx[x]];
-#pragma unroll
-      for (int x = 0; x < 8; ++x) {
-        const int r = tid | (x << (3 * (M - 1))), j = jx[x];
-        const bool fin = (valid >> x & 1) && o[x] < INFINITY;
-        const bool flg = (__double2loint(o[x]) & SD_CNT) != 0;
-        // d(l, j*) exactly: an unflagged finite o[x] is V_j* + d with V_j* = the stamp of Ψ_j* (the same expression
-        // as the stamping above, payload j*), every term exact in the binade (garbage, unused, otherwise)
-        const double dd = o[x] - stamp(pv[x], j);
-        const double t1 = pre + a[M - 1] * (double)(lb[M - 1] + x);
-        const double val = (t1 + beta * dd) + pv[x];  // R(l, j*), HelpFunctions.jl:63-71
-        listed |= (unsigned)(fin && flg) << x;
-        uu[r] = (uint16_t)(fin && !flg ? j : 0xFFFF);  // 0xFFFF: unwritten (Φ = +Inf) or not yet known (listed)
-        outv[r] = fin ? (flg ? __longlong_as_double(0x7FF8000000000000ll) : val) : INFINITY;
-      }
+    if (!direct && !sparse) {
+      winners(std::false_type{});
+      if (__any(dmin <= tol) && lane == 0) sh.redo[par] = 1;
     } else {
 #pragma unroll
       for (int x = 0; x < 8; ++x) {
@@ -662,20 +709,18 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
         outv[r] = (listed >> x & 1) ? __longlong_as_double(0x7FF8000000000000ll) : ov;
       }
     }
-    if (listed) {
-      int e = atomicAdd(&sh.nlist, __popc(listed));
-#pragma unroll
-      for (int x = 0; x < 8; ++x)
-        if (listed >> x & 1) {
-          if (e < SD_LCAP) list[e] = (uint16_t)(tid | (x << (3 * (M - 1))));
-          ++e;
-        }
-    }
+    list_targets(listed);
     h.late_drain();  // this wave's stores of the previous row have landed (late: they have had the whole row)
     sd_bar();
     h.publish();     // ... so have every wave's: the previous row is done
     SD_STAMP(7);
-    const int nl = sh.nlist;
+    if (transform && sh.redo[par]) {  // uniform, rare: a near tie somewhere in the row -- the certified transform
+      passes(std::true_type{});
+      list_targets(winners(std::true_type{}));
+      sd_bar();
+      if (tid == 0) ++sh.cnt[3];
+    }
+    const int nl = sh.nlist[par];
     if (nl) {
       if (nl <= SD_COOP)
         sd_scan<M, true>(list, nl, psi, a, lb, beta, uu, outv, sh.redv, sh.redj);
@@ -1004,7 +1049,10 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
   const int k = (int)blockIdx.y, tid = threadIdx.x;
-  if (tid == 0) sh.cnt[0] = sh.cnt[1] = 0;
+  if (tid == 0) {
+    sh.cnt[0] = sh.cnt[1] = sh.cnt[3] = 0;
+    sh.nlist[0] = sh.redo[0] = 0;
+  }
   // B >= 1: block 0 takes rows 0 and B together, block x the row x (B workgroups, one per CU at B = 256)
   if (blockIdx.x == 0 && P.B >= 1) {
     SdPerm pm;
@@ -1028,10 +1076,11 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
     for (int q = 0; q < 4; ++q) ein[q] = *reinterpret_cast<const uint2 *>(slot + sd_p2<M>(tid, q));
     sdt_body<M, false>(P, Lv, G, k, cp, i, v, ein, slot, slot + L, Sout_all + (size_t)k * s_stride + (size_t)cp * L,
                        UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(P.B + 1) * L) + (size_t)cp * L, sh,
-                       sds, hooks, P.df, P.uold);
+                       sds, hooks, P.df, P.uold, 0);
     if (tid == 0) {
       if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
       if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
+      if (sh.cnt[3]) atomicAdd(&counters[5], sh.cnt[3]);
     }
   }
   SD_FLUSH();
@@ -1313,6 +1362,8 @@ struct SdPipe {
       }
     }
     val = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // diagnostics [4]: this row reuses a staging buffer that a row above may still read (some WAR lane armed above)
+    if (tid == 0 && nt - i - NB > 0 && min(cp + 7 * M, B) >= max(cp + 1, hi)) ++sh->cnt[2];
   }
   // after the row's first barrier (every wave has consumed this row's loads): publish `loaded`; this wave waits until
   // its polls match (re-polling), then issues the next row's loads -- the measured-valid consumer form: the polling
@@ -1344,8 +1395,10 @@ struct SdPipe {
       // the reuse flag of the slot: same2[i-1] = (u_old(i-1) == u_old(i+1)), copied with this step's df / u_old (the
       // slot of step i+1 already holds the order of step ni = i-1 then: the order is a function of u_old alone,
       // k_pyr_order, and by induction every slot holds the order of the last step assigned to it)
-      const int same = *reinterpret_cast<const volatile int32_t *>(sds + sd_dfuo_offset<M>() +
-                                                                   (threadIdx.x >> 6) * sd_dfuo_stride<M>() + 16 * M);
+      // (an LDS load: through the generic pointer it was a flat load, whose vmcnt(0) wait made wave 0 wait for its own
+      // `loaded` flag store above to complete before issuing the next row's loads)
+      const int same = *(const volatile __attribute__((address_space(3))) int32_t *)(
+          sds + sd_dfuo_offset<M>() + (threadIdx.x >> 6) * sd_dfuo_stride<M>() + 16 * M);
       sd_read_next<M>(nx, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N);
       sd_issue_pipe<M>(raw, rs, nx, ncp, (unsigned)((ni + 1) % NB) * bufb, r0b + (unsigned)(ni + 1) * rowb, rowb);
       if (ni != i && !same) {
@@ -1410,7 +1463,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   h.pcp = -1, h.pi = 0;
   if (tid == 0) {
     sh.stop = 0;
-    sh.cnt[0] = sh.cnt[1] = 0;
+    sh.cnt[0] = sh.cnt[1] = sh.cnt[2] = sh.cnt[3] = 0;
+    sh.nlist[0] = sh.nlist[1] = sh.redo[0] = sh.redo[1] = 0;
   }
   // prologue: both sphere orders of the first step, df / u_old, and the first row's loads (the terminal row was
   // written by an earlier launch)
@@ -1431,6 +1485,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   // make it assume, at the loop head, that nothing younger can be outstanding, and wait for every store there
   __builtin_amdgcn_s_waitcnt(0x0F70);
   int status = 0;  // the previous row's sdt_body result: 1 = its outputs are all +Inf
+  int par = 0;     // the row's parity (sdt_body's LDS slots)
   bool stop = false;
 #pragma nounroll
   for (int i = nt - 2; i >= 0 && !stop; --i) {
@@ -1461,7 +1516,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, ein, pslot(i + 1), pslot(i),
                                  reg + (size_t)(i % NB) * R * L + (size_t)cp * L,
                                  UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L, sh,
-                                 sds, h, df_all, uo_all, h.raw.mask, h.raw.srank, xs);
+                                 sds, h, df_all, uo_all, par, h.raw.mask, h.raw.srank, xs);
+      par ^= 1;
       SD_TL(6);
       stop = sh.stop != 0;  // written before a barrier the row has passed since (every path has one)
     }
@@ -1469,6 +1525,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   if (tid == 0) {
     if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
     if (sh.cnt[1]) atomicAdd(&counters[1], sh.cnt[1]);
+    if (sh.cnt[2]) atomicAdd(&counters[4], sh.cnt[2]);
+    if (sh.cnt[3]) atomicAdd(&counters[5], sh.cnt[3]);
   }
   SD_FLUSH();
   SD_TL_FLUSH(h.g0);

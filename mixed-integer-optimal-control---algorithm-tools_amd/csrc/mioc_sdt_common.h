@@ -24,6 +24,12 @@ __device__ __forceinline__ double sd_min(double a, double b) {
   asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+// min(a, |b|) in one instruction (the abs is an operand modifier; fabs() on an asm operand would cost a v_and)
+__device__ __forceinline__ double sd_min_abs(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ double sd_max(double a, double b) {
   double r;
   asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));

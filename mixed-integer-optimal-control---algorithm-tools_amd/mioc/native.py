@@ -31,7 +31,6 @@ MIOC_ENONFINITE = -7
 MIOC_P_INF, MIOC_P_ONE, MIOC_P_INTLUT, MIOC_P_TABLE = 0, 1, 2, 3
 MIOC_OPT_ALGO, MIOC_OPT_TIMING, MIOC_OPT_PERSIST, MIOC_OPT_PRED_FMA = 1, 2, 3, 4
 MIOC_OPT_SPIN_LIMIT, MIOC_OPT_SDT_BUFFERS, MIOC_OPT_FSEP_SEGMENTS, MIOC_OPT_PINF_WALK = 5, 6, 7, 8
-MIOC_OPT_SDT_PAIR = 9
 MIOC_ALGO_AUTO, MIOC_ALGO_GENERIC, MIOC_ALGO_PINF, MIOC_ALGO_PYRAMID, MIOC_ALGO_SEPARABLE = 0, 1, 2, 3, 4
 MIOC_ALGO_FUSED, MIOC_ALGO_FUSED_SEPARABLE = 5, 6
 MIOC_ODE_FISHING, MIOC_ODE_DOUBLETANK, MIOC_ODE_VANDERPOL = 1, 2, 3

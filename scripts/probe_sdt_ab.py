@@ -1,8 +1,8 @@
 """A/B timing of k_sdt_run (C4 inputs at full L and B, truncated nt) across library builds, each in its own process.
 Prints per library: µs per DP step (HIP events, best of REPS calls) and a digest of u / Φ* at three budgets and of
 the argmin tables of a few steps, which must agree across builds.
-Usage: python scripts/probe_sdt_ab.py NT LIB [LIB ...]   (SDT_NB=n: staging buffers; LIB#0 / LIB#1: MIOC_OPT_SDT_PAIR
-off / on for that run, e.g. lib/libmioc.so#0 times the one-workgroup-per-row k_sdt_run)"""
+Usage: python scripts/probe_sdt_ab.py NT LIB [LIB ...]   (SDT_NB=n: staging buffers; a LIB may be repeated to
+interleave runs of the same build, LIB#tag only labels the run)"""
 import hashlib, json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mixed-integer-optimal-control---algorithm-tools_amd")
@@ -13,7 +13,7 @@ NB = int(os.environ.get("SDT_NB", "0"))  # staging buffers (MIOC_OPT_SDT_BUFFERS
 
 
 def one(nt, spec):
-    lib, _, pair = spec.partition("#")
+    lib = spec.partition("#")[0]
     os.environ["MIOC_LIB"] = lib
     sys.path.insert(0, PKG); sys.path.insert(0, ROOT)
     import numpy as np
@@ -27,8 +27,6 @@ def one(nt, spec):
         ctx.set_option(native.MIOC_OPT_TIMING, 1); ctx.set_option(native.MIOC_OPT_PERSIST, 1)
         if NB:
             ctx.set_option(native.MIOC_OPT_SDT_BUFFERS, NB)
-        if pair:
-            ctx.set_option(native.MIOC_OPT_SDT_PAIR, int(pair))
         best = None
         for _ in range(REPS):
             ctx.reset_stats()

@@ -1,10 +1,12 @@
 """GPU parity of the C4 (BASELINE roofline) shape on the code the bench times: k_sdt_run<4> (the persistent separable
-transform, one workgroup per budget row, 8^4 = 4096 levels, B = 256, p = 1) -- and the opt-in two-workgroups-per-row
-k_sdt_pair and the per-step k_sdt_step -- against the CPU oracle, never against another device algorithm.
+transform, one workgroup per budget row, 8^4 = 4096 levels, B = 256, p = 1) -- and the per-step k_sdt_step --
+against the CPU oracle, never against another device algorithm.
 
-  * a committed oracle fixture at the full L = 4096, B = 256 with nt = 64 (63 recursion steps: every rotation of
-    the four staging buffers and row B's two-step lag, many times): sha256 of every step's argmin table U in the
-    reference layout, and u / Φ* at B' = 256, 128, 7 (tests/golden/make_c4_fixture.py);
+  * a committed oracle fixture at the full L = 4096, B = 256 with nt = 64 (63 recursion steps and row B's two-step
+    lag): sha256 of every step's argmin table U in the reference layout, and u / Φ* at B' = 256, 128, 7
+    (tests/golden/make_c4_fixture.py).  At the default 256 staging buffers a 63-step DP never reuses one, so the
+    fixture also runs with 4, 5 and 12 buffers (MIOC_OPT_SDT_BUFFERS): the ring wraps 16, 12 and 5 times and every
+    row's write-after-read wait on the rows above is armed (diagnostics [4] counts the rows that armed it);
   * 4096-level tie-heavy steps (zero, integer, steep gradients): the exact-scan paths, including the overflow
     of the listed-target buffer (SD_LCAP), oracle computed here;
   * the chunked persistent branch (each workgroup several rows): a K = 2 batch and B = 300 > #CUs.
@@ -24,11 +26,12 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _ctx(lt, beta, algo, persist=1, pair=1):
+def _ctx(lt, beta, algo, persist=1, nb=None):
     ctx = native.Context(0)
     ctx.set_levels(lt)
     ctx.set_cost(1, beta)
-    ctx.set_option(native.MIOC_OPT_SDT_PAIR, pair)
+    if nb is not None:
+        ctx.set_option(native.MIOC_OPT_SDT_BUFFERS, nb)
     ctx.set_option(native.MIOC_OPT_TIMING, 1)
     ctx.set_option(native.MIOC_OPT_ALGO, algo)
     ctx.set_option(native.MIOC_OPT_PERSIST, persist)
@@ -39,35 +42,51 @@ def _hash(t):
     return np.frombuffer(hashlib.sha256(np.ascontiguousarray(t, dtype=np.int32).tobytes()).digest(), dtype=np.uint8)
 
 
-@pytest.mark.parametrize("variant", ["pair", "pair512", "persistent", "steps"])
-def test_c4_nt64_fixture(variant):
+# (variant, staging buffers): None = the default (256, no reuse at nt = 64); 4 / 5 / 12 wrap the ring (5 and 12 are
+# not powers of two, so an off-by-one in the buffer index that a power of two would hide cannot pass)
+C4_VARIANTS = [("persistent", None), ("persistent", 4), ("persistent", 5), ("persistent", 12), ("steps", None)]
+
+
+def _check_fixture(ctx, z, label):
+    nt = z["df"].shape[1]
+    bad = [i for i in range(nt - 1) if not np.array_equal(_hash(ctx.argmin_table(i)), z["u_hash"][i])]
+    assert not bad, f"{label}: U differs from the oracle at steps {bad[:10]}"
+    for q, Bp in enumerate(z["budgets"]):
+        u, ps, _ = ctx.backtrack(int(Bp))
+        assert np.array_equal(u, z["u"][q]), f"{label} B'={Bp}"
+        assert ps == z["phi_star"][q], f"{label} B'={Bp}: {ps!r} vs {z['phi_star'][q]!r}"
+
+
+@pytest.mark.parametrize("variant,nb", C4_VARIANTS, ids=[f"{v}-nb{n}" if n else v for v, n in C4_VARIANTS])
+def test_c4_nt64_fixture(variant, nb):
     """The separable transform writes U exactly like the reference: the rank where the reference writes it, and
     nothing (-1) elsewhere, so every step's table hashes to the oracle's.  persistent: k_sdt_run (the bench's kernel),
-    pair: k_sdt_pair (MIOC_OPT_SDT_PAIR), steps: one k_sdt_step launch per step."""
+    steps: one k_sdt_step launch per step.  With nb staging buffers the ring wraps and the WAR waits run."""
     z = np.load(os.path.join(HERE, "golden", "hashed", "c4_4096lv_p1_nt64_uhash.npz"), allow_pickle=False)
     cfg = CONFIGS["C4"]
     lt = cfg.levels()
     algo = native.MIOC_ALGO_SEPARABLE
-    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=int(variant != "steps"),
-               pair={"pair": 1, "pair512": 2}.get(variant, 0))
+    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=int(variant != "steps"), nb=nb)
     df, uo = z["df"], z["u_old"]
     B = int(z["B"][0])
     ctx.bellman(df, uo, B, float(z["dt"][0]))
     assert ctx.last_algo() == algo
     ctx.synchronize()
-    assert ctx.kernel_stats(0)[2] == {"pair": "k_sdt_pair", "pair512": "k_sdt_pair", "persistent": "k_sdt_run",
-                                      "steps": "k_sdt_step"}[variant]
-    nt = df.shape[1]
-    bad = [i for i in range(nt - 1) if not np.array_equal(_hash(ctx.argmin_table(i)), z["u_hash"][i])]
-    assert not bad, f"{variant}: U differs from the oracle at steps {bad[:10]}"
-    for q, Bp in enumerate(z["budgets"]):
-        u, ps, _ = ctx.backtrack(int(Bp))
-        assert np.array_equal(u, z["u"][q]), f"{variant} B'={Bp}"
-        assert ps == z["phi_star"][q], f"{variant} B'={Bp}: {ps!r} vs {z['phi_star'][q]!r}"
+    assert ctx.kernel_stats(0)[2] == {"persistent": "k_sdt_run", "steps": "k_sdt_step"}[variant]
+    diag = ctx.diagnostics()
+    assert diag[6] == 0, diag  # the persistent launch ran to the end (no per-step redo)
+    if variant == "persistent":
+        nt = df.shape[1]
+        if nb is None:
+            assert diag[4] == 0, diag  # 256 buffers, 63 steps: no buffer is reused
+        else:
+            # rows 1 .. B-1 arm the WAR wait at every step i < nt - nb (token(i + nb - 1) > 0)
+            assert diag[4] >= (B - 1) * (nt - 1 - nb), diag
+    _check_fixture(ctx, z, f"{variant} nb={nb}")
     ctx.close()
 
 
-@pytest.mark.parametrize("variant", ["pair", "pair512", "persistent", "steps"])
+@pytest.mark.parametrize("variant", ["persistent", "steps"])
 @pytest.mark.parametrize("mode", ["zero", "integer", "steep"])
 def test_c4_tie_heavy_vs_oracle(oracle_c, mode, variant):
     """4096 levels, B = 256: every target of a zero-gradient row ties (the listed-target buffer overflows and the
@@ -86,7 +105,7 @@ def test_c4_tie_heavy_vs_oracle(oracle_c, mode, variant):
         df = df * 1e3  # value spread ~1e12 beta: outside the transform's binade (2^36 units)
     beta = 1e-13 if mode == "steep" else cfg.beta
     phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_ONE, beta, cfg.dt)
-    ctx = _ctx(lt, beta, native.MIOC_ALGO_SEPARABLE, int(variant != "steps"), {"pair": 1, "pair512": 2}.get(variant, 0))
+    ctx = _ctx(lt, beta, native.MIOC_ALGO_SEPARABLE, int(variant != "steps"))
     ctx.bellman(df, uo, cfg.B, cfg.dt)
     diag = ctx.diagnostics()
     for i in range(n - 1):
@@ -122,6 +141,7 @@ def test_c4_chunked_rows_vs_oracle(oracle_c):
     ctx.bellman_batch_tensors(ddf, duo, cfg.B, cfg.dt)
     ctx.backtrack_batch_tensors(cfg.B, du, dphi, None)
     ctx.synchronize()
+    assert ctx.kernel_stats(0)[2] == "k_sdt_run"
     for k, (df, uo) in enumerate(subs):
         phi, U = oracle_c.bellman(lv, df, uo, cfg.B, P_ONE, cfg.beta, cfg.dt)
         ou, ops = oracle_c.backtrack(lv, uo, phi, U, cfg.B, cfg.B)
@@ -143,27 +163,21 @@ def test_c4_chunked_rows_vs_oracle(oracle_c):
     ctx.close()
 
 
-@pytest.mark.parametrize("pair", [1, 2, 0], ids=["pair", "pair512", "persistent"])
-def test_c4_nt64_fixture_wait_timeout_redoes_dp(pair):
-    """The headline kernels' timeout path: with a spin limit of one poll, the persistent k_sdt_pair / k_sdt_run gives
-    up at its first dependency wait that is not already satisfied, every workgroup leaves, and the host redoes the DP
-    with per-step launches (check_run, counted in diagnostics [6]) before anything reads the tables -- so every
-    step's U hash, u and Φ* still equal the oracle fixture."""
+@pytest.mark.parametrize("nb", [None, 5], ids=["nb-default", "nb5"])
+def test_c4_nt64_fixture_wait_timeout_redoes_dp(nb):
+    """The headline kernel's timeout path: with a spin limit of one poll, the persistent k_sdt_run gives up at its
+    first dependency wait that is not already satisfied (RAW, or with 5 staging buffers also WAR), every workgroup
+    leaves, and the host redoes the DP with per-step launches (check_run, counted in diagnostics [6]) before anything
+    reads the tables -- so every step's U hash, u and Φ* still equal the oracle fixture."""
     z = np.load(os.path.join(HERE, "golden", "hashed", "c4_4096lv_p1_nt64_uhash.npz"), allow_pickle=False)
     lt = CONFIGS["C4"].levels()
     algo = native.MIOC_ALGO_SEPARABLE
-    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=1, pair=pair)
+    ctx = _ctx(lt, float(z["beta"][0]), algo, persist=1, nb=nb)
     ctx.set_option(native.MIOC_OPT_SPIN_LIMIT, 1)
     df, uo = z["df"], z["u_old"]
     ctx.bellman(df, uo, int(z["B"][0]), float(z["dt"][0]))
     assert ctx.last_algo() == algo
-    nt = df.shape[1]
-    bad = [i for i in range(nt - 1) if not np.array_equal(_hash(ctx.argmin_table(i)), z["u_hash"][i])]
-    assert not bad, f"U differs from the oracle at steps {bad[:10]}"
-    for q, Bp in enumerate(z["budgets"]):
-        u, ps, _ = ctx.backtrack(int(Bp))
-        assert np.array_equal(u, z["u"][q]), f"B'={Bp}"
-        assert ps == z["phi_star"][q], f"B'={Bp}: {ps!r} vs {z['phi_star'][q]!r}"
+    _check_fixture(ctx, z, f"timeout redo nb={nb}")
     diag = ctx.diagnostics()
     assert diag[6] >= 1, diag  # the persistent launch was abandoned and redone
     ctx.close()
