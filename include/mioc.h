@@ -72,7 +72,10 @@ extern "C" {
                                  (default 2^24; a tiny value forces that fallback, for tests) */
 #define MIOC_OPT_SDT_BUFFERS 6 /* persistent separable transform: staging buffers (4..256, default 256; more
                                   buffers let rows run further apart, which hides the row hand-off; cut to
-                                  the most that keep a subproblem's staging region under 4 GiB) */
+                                  the most that keep a subproblem's staging region under 4 GiB; raised to
+                                  7·M + 1 (29 on 8^4 grids): with fewer, a row's write-after-read wait can
+                                  close a cycle with the one-row-ahead waits of the rows below it, so the DP
+                                  would deadlock -- a problem where 7·M + 1 do not fit runs per step) */
 #define MIOC_OPT_FSEP_SEGMENTS 7 /* fused separable DP: row segments per subproblem, each on its own workgroup
                                     (0, default: chosen from the batch size -- more than one only when the
                                     batch alone cannot fill the GPU; 1..8: forced; -1: the one-lane-per-row

@@ -298,12 +298,18 @@ int run_bellman(mioc_ctx *ctx) {
     }
     // persistent layout: per subproblem NB staging buffers of (B+1)·L, then row 0 of every step (nt·L), one region
     // addressed by one buffer resource (< 4 GiB); per-step layout: two buffers of K blocks of (B+1)·L
-    int nbuf = persist ? ctx->opt_nb : 2;
+    // at least 7·M + 1 buffers: item (c', i) waits (write-after-read) for the rows up to 7·M above it to have loaded
+    // S_{i+NB}, and (one item ahead) for the rows below it to have finished step i; with NB <= 7·M those waits close a
+    // cycle -- (c', i) <- (c'-1, i-1) <- ... <- (c'-NB, i-NB), whose WAR wait needs row c' to have loaded S_i, i.e.
+    // item (c', i-1) -- and the DP deadlocks until the spin limit (tests/test_gpu_c4.py runs 29, 32 and 37)
+    const int nb_min = 7 * ctx->pyr.M + 1;
+    int nbuf = persist ? std::max(ctx->opt_nb, nb_min) : 2;
     // one buffer resource addresses a subproblem's whole region (32-bit offsets): as many buffers as fit under 4 GiB
     if (persist) {
       const size_t cap = (1ull << 32) / sizeof(double);
       const size_t fit = cap > nt * L ? (cap - nt * L - 1) / s_stride : 0;
-      if ((size_t)nbuf > fit) nbuf = (int)std::max<size_t>(fit, 4);
+      if ((size_t)nbuf > fit) nbuf = (int)fit;
+      if (nbuf < nb_min) persist = false, nbuf = 2;  // too few fit to be deadlock-free: per-step launches
     }
     const size_t kstride = persist ? (size_t)nbuf * s_stride + nt * L : s_stride;
     if (persist && kstride * sizeof(double) >= (1ull << 32)) persist = false;  // (then also kstride = s_stride)

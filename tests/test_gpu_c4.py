@@ -5,8 +5,9 @@ against the CPU oracle, never against another device algorithm.
   * a committed oracle fixture at the full L = 4096, B = 256 with nt = 64 (63 recursion steps and row B's two-step
     lag): sha256 of every step's argmin table U in the reference layout, and u / Φ* at B' = 256, 128, 7
     (tests/golden/make_c4_fixture.py).  At the default 256 staging buffers a 63-step DP never reuses one, so the
-    fixture also runs with 4, 5 and 12 buffers (MIOC_OPT_SDT_BUFFERS): the ring wraps 16, 12 and 5 times and every
-    row's write-after-read wait on the rows above is armed (diagnostics [4] counts the rows that armed it);
+    fixture also runs with 29 (the fewest that cannot deadlock: 7·M + 1), 32 and 37 buffers (MIOC_OPT_SDT_BUFFERS):
+    the ring wraps and every row below B arms its write-after-read wait on the rows above for nt - NB steps
+    (diagnostics [4] counts those rows); 4 is raised to 29;
   * 4096-level tie-heavy steps (zero, integer, steep gradients): the exact-scan paths, including the overflow
     of the listed-target buffer (SD_LCAP), oracle computed here;
   * the chunked persistent branch (each workgroup several rows): a K = 2 batch and B = 300 > #CUs.
@@ -42,9 +43,12 @@ def _hash(t):
     return np.frombuffer(hashlib.sha256(np.ascontiguousarray(t, dtype=np.int32).tobytes()).digest(), dtype=np.uint8)
 
 
-# (variant, staging buffers): None = the default (256, no reuse at nt = 64); 4 / 5 / 12 wrap the ring (5 and 12 are
-# not powers of two, so an off-by-one in the buffer index that a power of two would hide cannot pass)
-C4_VARIANTS = [("persistent", None), ("persistent", 4), ("persistent", 5), ("persistent", 12), ("steps", None)]
+# (variant, staging buffers): None = the default (256, no reuse at nt = 64); 29 / 32 / 37 wrap the ring (29 and 37 are
+# not powers of two, so an off-by-one in the buffer index that a power of two would hide cannot pass); 4 is below the
+# deadlock-free minimum 7·M + 1 = 29 and must be raised to it
+C4_VARIANTS = [("persistent", None), ("persistent", 29), ("persistent", 32), ("persistent", 37), ("persistent", 4),
+               ("steps", None)]
+NB_MIN = 29
 
 
 def _check_fixture(ctx, z, label):
@@ -80,8 +84,8 @@ def test_c4_nt64_fixture(variant, nb):
         if nb is None:
             assert diag[4] == 0, diag  # 256 buffers, 63 steps: no buffer is reused
         else:
-            # rows 1 .. B-1 arm the WAR wait at every step i < nt - nb (token(i + nb - 1) > 0)
-            assert diag[4] >= (B - 1) * (nt - 1 - nb), diag
+            # one row per workgroup: rows 1 .. B-1 arm the WAR wait at every step i < nt - NB (token(i + NB - 1) > 0)
+            assert diag[4] == (B - 1) * (nt - max(nb, NB_MIN)), diag
     _check_fixture(ctx, z, f"{variant} nb={nb}")
     ctx.close()
 
@@ -163,10 +167,10 @@ def test_c4_chunked_rows_vs_oracle(oracle_c):
     ctx.close()
 
 
-@pytest.mark.parametrize("nb", [None, 5], ids=["nb-default", "nb5"])
+@pytest.mark.parametrize("nb", [None, 31], ids=["nb-default", "nb31"])
 def test_c4_nt64_fixture_wait_timeout_redoes_dp(nb):
     """The headline kernel's timeout path: with a spin limit of one poll, the persistent k_sdt_run gives up at its
-    first dependency wait that is not already satisfied (RAW, or with 5 staging buffers also WAR), every workgroup
+    first dependency wait that is not already satisfied (RAW, or with 31 staging buffers also WAR), every workgroup
     leaves, and the host redoes the DP with per-step launches (check_run, counted in diagnostics [6]) before anything
     reads the tables -- so every step's U hash, u and Φ* still equal the oracle fixture."""
     z = np.load(os.path.join(HERE, "golden", "hashed", "c4_4096lv_p1_nt64_uhash.npz"), allow_pickle=False)
