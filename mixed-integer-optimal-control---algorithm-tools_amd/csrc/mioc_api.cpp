@@ -223,6 +223,22 @@ void ev_end(mioc_ctx *ctx, int which, int64_t launches) {
 int run_bellman(mioc_ctx *ctx) {
   ProblemDev P = problem_dev(ctx);
   LevelsDev Lv = levels_dev(ctx);
+  // fills queued before the validation's host sync below, so that they overlap the previous call's device work: the
+  // DP counters, and (p = Inf, the likely algorithm) the segmented recursion's flags
+  if (!ctx->d_counters) {
+    size_t cc = 0;
+    int rc0 = grow(ctx, &ctx->d_counters, &cc, 8 * sizeof(int32_t), "counters");
+    if (rc0) return rc0;
+  }
+  HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(int32_t), ctx->stream));
+  bool pinf_flags_zeroed = false;
+  if (ctx->p_kind == MIOC_P_INF && !ctx->force_steps) {
+    const size_t fbytes = ((size_t)ctx->K * pinf_recur_segments(P) + 1) * sizeof(int32_t);
+    int rcf = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, fbytes, "p=Inf segment flags");
+    if (rcf) return rcf;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, fbytes, ctx->stream));
+    pinf_flags_zeroed = true;
+  }
   // validation pass: finite df, integral u_old, max budget class
   HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int32_t), ctx->stream));
   HIP_TRY(ctx, launch_validate(ctx->stream, P, ctx->d_numin, ctx->d_numax, ctx->d_flags));
@@ -265,12 +281,6 @@ int run_bellman(mioc_ctx *ctx) {
   if (algo == MIOC_ALGO_SEPARABLE && !sdt_ok)
     return fail(ctx, MIOC_EINVAL, "the separable L1 transform needs p = 1, beta > 0 and an 8^3 or 8^4 product grid "
                                   "of consecutive integer levels");
-  if (!ctx->d_counters) {
-    size_t cc = 0;
-    int rc0 = grow(ctx, &ctx->d_counters, &cc, 8 * sizeof(int32_t), "counters");
-    if (rc0) return rc0;
-  }
-  HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(int32_t), ctx->stream));
   ctx->algo = algo;
   const size_t K = (size_t)ctx->K, nt = (size_t)ctx->nt, L = (size_t)ctx->L, RP = (size_t)ctx->RP;
 
@@ -491,10 +501,12 @@ int run_bellman(mioc_ctx *ctx) {
     // row segments on several CUs need their hand-off flags (and a timed-out wait redoes the DP in one workgroup)
     int32_t *pflags = nullptr;
     if (!ctx->force_steps) {
-      const size_t fbytes = ((size_t)K * pinf_recur_segments(P) + 1) * sizeof(int32_t);
-      rc = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, fbytes, "p=Inf segment flags");
-      if (rc) return rc;
-      HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, fbytes, ctx->stream));
+      if (!pinf_flags_zeroed) {
+        const size_t fbytes = ((size_t)K * pinf_recur_segments(P) + 1) * sizeof(int32_t);
+        rc = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, fbytes, "p=Inf segment flags");
+        if (rc) return rc;
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, fbytes, ctx->stream));
+      }
       if (!ctx->h_run_err) HIP_TRY(ctx, hipHostMalloc(&ctx->h_run_err, 16, 0));
       *ctx->h_run_err = 0;
       pflags = ctx->d_runflags;
@@ -506,9 +518,19 @@ int run_bellman(mioc_ctx *ctx) {
     ctx->stat_name[0] = variant;  // the timing window is named after the recursion kernel that ran
     if (segmented) {
       const int nseg = pinf_recur_segments(P);
-      HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + (size_t)K * nseg, sizeof(int32_t),
-                                  hipMemcpyDeviceToHost, ctx->stream));
-      ctx->run_pending = true;
+      if (!P.gate) {
+        // a wait past the spin limit: the one-workgroup recursion redoes the DP on the device, gated by the error word
+        // (no host round trip between the DP and the backtrack); diagnostics [6] reads its count (d_counters[6])
+        ProblemDev Pr = P;
+        Pr.redo_gate = ctx->d_runflags + (size_t)K * nseg;
+        Pr.redo_count = ctx->d_counters + 6;
+        HIP_TRY(ctx, launch_pinf_recur(ctx->stream, Pr, D, ctx->ncu, nullptr, ctx->spin_limit, nullptr, nullptr));
+      } else {
+        // under the device TRM control the backtrack kernels are gated already: the host checks and redoes (check_run)
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + (size_t)K * nseg, sizeof(int32_t),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        ctx->run_pending = true;
+      }
     }
   }
   ctx->have_dp = true;
@@ -541,7 +563,8 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
   if (rc) return rc;
   int32_t *d_urank = ctx->d_ranks + K * nt;
   if (ctx->algo != MIOC_ALGO_PINF) HIP_TRY(ctx, launch_uold_rank(ctx->stream, P, Lv, d_urank));
-  HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags + 2, 0, 2 * sizeof(int32_t), ctx->stream));
+  // (p = Inf: k_pinf_start zeroes them, one fill fewer on the stream)
+  if (ctx->algo != MIOC_ALGO_PINF) HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags + 2, 0, 2 * sizeof(int32_t), ctx->stream));
   if (ctx->algo == MIOC_ALGO_PYRAMID || ctx->algo == MIOC_ALGO_SEPARABLE) {
     const size_t s_stride = (size_t)(ctx->B + 1) * ctx->L;
     const size_t uu_stride_k = (nt > 1 ? nt - 1 : 1) * s_stride;
@@ -561,7 +584,6 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
                                      d_urank, ctx->d_ranks, ctx->d_flags + 2));
     ev_end(ctx, 1, 1);
   } else {
-    HIP_TRY(ctx, launch_pinf_start(ctx->stream, P, Lv, ctx->pinf, (int)B_use, ctx->d_start));
     // the segmented walk spreads one subproblem's path over many workgroups: for batches too small to fill the GPU
     // with one serial walk each (auto: K <= 64 and at least 512 steps)
     const bool fwalk = ctx->opt_pinf_walk > 0 || (ctx->opt_pinf_walk == 0 && K <= 64 && nt >= 512);
@@ -575,7 +597,11 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
                          "segmented walk segment maps");
       if (!rc) rc = grow(ctx, &D.fneed, &ctx->pinf_cap_fneed, (K + 1) * sizeof(int32_t), "segmented walk flags");
       if (rc) return rc;
-      HIP_TRY(ctx, hipMemsetAsync(D.fneed, 0, (K + 1) * sizeof(int32_t), ctx->stream));
+    }
+    // k_pinf_start also zeroes the walk's fallback counters (d_flags[2..3]) and, for the segmented walk, fneed
+    HIP_TRY(ctx, launch_pinf_start(ctx->stream, P, Lv, D, (int)B_use, ctx->d_start, ctx->d_flags + 2,
+                                   fwalk ? D.fneed : nullptr));
+    if (fwalk) {
       ev_begin(ctx, 1, "k_pinf_fwalk");
       HIP_TRY(ctx, launch_pinf_fwalk(ctx->stream, P, Lv, D, ctx->d_start, ctx->d_ranks));
       // subproblems whose chain met a state-dependent row: the serial walk (the others return at once)
@@ -1277,10 +1303,10 @@ int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
   // slot 6: the separable transform's persistent DPs redone with per-step launches (cooperative launch refused or a
   // dependency wait timed out) -- its kernels write no c[6]; the pyramid's value-collision count otherwise
   // slot 8: row segments per subproblem of the last fused separable DP (0: the one-lane-per-row kernel)
-  const int64_t c6 = ctx->algo == MIOC_ALGO_SEPARABLE || ctx->algo == MIOC_ALGO_FUSED_SEPARABLE ||
-                             ctx->algo == MIOC_ALGO_PINF
+  // (p = Inf: plus the device-side redo of the last DP, counted by the gated one-workgroup recursion in c[6])
+  const int64_t c6 = ctx->algo == MIOC_ALGO_SEPARABLE || ctx->algo == MIOC_ALGO_FUSED_SEPARABLE
                          ? ctx->n_persist_fallbacks
-                         : c[6];
+                         : ctx->algo == MIOC_ALGO_PINF ? ctx->n_persist_fallbacks + c[6] : c[6];
   // slot 9: after a p=Inf segmented walk, its subproblems left to the serial walk (-1: the serial walk ran alone)
   int32_t fserial = -1;
   if (ctx->algo == MIOC_ALGO_PINF && ctx->last_pinf_fwalk && ctx->pinf.fneed)

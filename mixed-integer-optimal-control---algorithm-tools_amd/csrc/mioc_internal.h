@@ -45,9 +45,20 @@ struct ProblemDev {
   const double *uold = nullptr;    // [K][nt][M]
   const int32_t *Bvec = nullptr;   // backtrack: per-subproblem budget B'_k (null: one B' for the batch)
   const int32_t *gate = nullptr;   // device TRM control (mioc_trm_attach): backtrack kernels return at once while *gate == 0
+  // the one-workgroup p = Inf recursion as the device-side redo of a segmented one: it runs only if the segmented
+  // launch's error word (a timed-out wait) is set, and then counts itself in *redo_count (null: an ordinary launch)
+  const int32_t *redo_gate = nullptr;
+  int32_t *redo_count = nullptr;
 };
 // the kernels of a gated call return at once (uniformly) while the device TRM control's gate word is 0
 __device__ __forceinline__ bool gate_closed(const int32_t *gate) { return gate && *gate == 0; }
+// a redo launch (ProblemDev::redo_gate) returns at once unless the launch it backs up timed out
+__device__ __forceinline__ bool redo_skip(const ProblemDev &P) {
+  if (!P.redo_gate) return false;
+  if (*P.redo_gate == 0) return true;
+  if (P.redo_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(P.redo_count, 1);
+  return false;
+}
 
 // Product grid with consecutive integer levels per dimension (the L1-ball pyramid's domain).
 struct PyrGeom {
@@ -195,7 +206,7 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
                              unsigned spin_limit, bool *segmented, const char **variant = nullptr);
 int pinf_recur_segments(const ProblemDev &P);  // row segments of k_pinf_recur_mc per subproblem (its error word's offset)
 hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D, int Bu,
-                             Start *start);
+                             Start *start, int32_t *zero2 = nullptr, int32_t *fneed = nullptr);
 hipError_t launch_pinf_walk(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D,
                             const Start *start, int32_t *ranks, int32_t *nfallback, const int32_t *need);
 // segmented walk: steps per segment and segment count for nt steps

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <algorithm>
 #include <cstdint>
 
 #include "mioc_internal.h"
@@ -377,6 +378,7 @@ __device__ unsigned long long g_pinf_stamps[16][8];
 
 template <int BWP, int G>
 __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P, PinfDev D, int CH) {
+  if (redo_skip(P)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int CB = BWP / G;     // classes per lane
   constexpr int NP = CB / 2 + 1;  // 16-byte pieces of a lane's window
@@ -495,6 +497,7 @@ __global__ __launch_bounds__(G == 1 ? 512 : 1024) void k_pinf_recur(ProblemDev P
 // partials into R_i[E] (min is exact: the same value as one lane's fold over all classes) while the next step runs.
 template <int BWP, int NW>
 __global__ __launch_bounds__(NW * 64) void k_pinf_recur_xr(ProblemDev P, PinfDev D, int CH) {
+  if (redo_skip(P)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int G = 4, CB = BWP / G, NP = CB / 2 + 1, CW = BWP / NW, E = 32 * NW;
   static_assert(CB % 2 == 0 && CW * NW == BWP, "k_pinf_recur_xr shape");
@@ -1152,6 +1155,7 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
 
 // rows c_from .. RP-1 of R (beyond the rows k_pinf_recur_xr / _mc compute, all above B): +Inf for every step
 __global__ void k_pinf_rfill(ProblemDev P, PinfDev D, int c_from) {
+  if (P.redo_gate && *P.redo_gate == 0) return;
   const int k = blockIdx.y, RP = P.RP, nt = P.nt, n = RP - c_from;
   double *R = D.R + (size_t)k * nt * RP;
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)nt * n; e += (size_t)gridDim.x * blockDim.x)
@@ -1282,7 +1286,17 @@ __device__ __forceinline__ bool pkey_less(const PKey &a, const PKey &b) {
   return a.v < b.v || (a.v == b.v && a.pos < b.pos);
 }
 
-__global__ __launch_bounds__(1024) void k_pinf_start(ProblemDev P, LevelsDev Lv, PinfDev D, int Bu, Start *start) {
+// zero2 (nullable): two words zeroed by block 0 (the walk's fallback counters); fneed (nullable): the segmented walk's
+// flags, fneed[k] by block k and the count fneed[K] by block 0 (fills folded into this launch)
+__global__ __launch_bounds__(1024) void k_pinf_start(ProblemDev P, LevelsDev Lv, PinfDev D, int Bu, Start *start,
+                                                     int32_t *zero2, int32_t *fneed) {
+  if (threadIdx.x == 0) {
+    if (fneed) fneed[blockIdx.x] = 0;
+    if (blockIdx.x == 0) {
+      if (fneed) fneed[P.K] = 0;
+      if (zero2) zero2[0] = zero2[1] = 0;
+    }
+  }
   if (gate_closed(P.gate)) return;
   extern __shared__ __attribute__((aligned(16))) double sR1[];
   __shared__ PKey red[16];
@@ -1301,7 +1315,14 @@ __global__ __launch_bounds__(1024) void k_pinf_start(ProblemDev P, LevelsDev Lv,
   best.val = INFINITY;
   best.r = -1;
   best.c = 0;
-  for (int r = threadIdx.x; r < Lv.L; r += blockDim.x) {
+  // work items (level r, chunk q of the budget range 0..Bu): with few levels (the SOS1 shapes: 2-3 levels, B' ~ 800)
+  // one thread per level would scan the whole range alone.  Per level the reference takes the first minimum over c
+  // (strict <), then compares (value, grid index, c) across levels: one lexicographic minimum of (key, grid index, c)
+  // over every (r, c) is the same cell, so the chunks of a level need no order among themselves.
+  const int nq = nt == 1 ? 1 : max(1, min(Bu + 1, (int)blockDim.x / max(1, Lv.L)));
+  const int span = (Bu + nq) / nq;  // ceil((Bu + 1) / nq)
+  for (int w = threadIdx.x; w < Lv.L * nq; w += blockDim.x) {
+    const int r = w / nq, q = w - r * nq;
     const double *nuv = Lv.nuval + (size_t)r * M;
     const int b = p_bt(nuv, uo0, M);
     if (b > Bu) continue;
@@ -1313,11 +1334,12 @@ __global__ __launch_bounds__(1024) void k_pinf_start(ProblemDev P, LevelsDev Lv,
       continue;
     }
     const double K = t1 + Lv.beta;
-    // first minimum over c for this l (strict), then compare (value, grid index, c)
+    // first minimum over this chunk's c for this l (strict), then compare (value, grid index, c)
     double bv = INFINITY;
     uint64_t bkey = ~0ull;
     int bc = -1;
-    for (int c = b; c <= Bu; ++c) {
+    const int c0 = max(b, q * span), c1 = min(Bu, q * span + span - 1);
+    for (int c = c0; c <= c1; ++c) {
       const double v = K + sR1[c - b];
       const uint64_t kv = jl_key2(v);
       if (kv < bkey) {
@@ -1356,9 +1378,9 @@ __global__ __launch_bounds__(1024) void k_pinf_start(ProblemDev P, LevelsDev Lv,
 }
 
 hipError_t launch_pinf_start(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const PinfDev &D, int Bu,
-                             Start *start) {
+                             Start *start, int32_t *zero2, int32_t *fneed) {
   size_t lds = (size_t)(Bu + 1) * sizeof(double);
-  hipLaunchKernelGGL(k_pinf_start, dim3(P.K), dim3(1024), lds, s, P, Lv, D, Bu, start);
+  hipLaunchKernelGGL(k_pinf_start, dim3(P.K), dim3(1024), lds, s, P, Lv, D, Bu, start, zero2, fneed);
   return hipGetLastError();
 }
 
@@ -1591,43 +1613,53 @@ __global__ __launch_bounds__(256) void k_pinf_walk(ProblemDev P, LevelsDev Lv, P
 // expanded per segment (k_pinf_fexpand).  A chain that meets a state-dependent row leaves its subproblem to
 // the serial walk (k_pinf_walk gated by fneed), so the ranks equal the serial walk's always.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pinf_ftab(ProblemDev P, PinfDev D) {
+// fts steps per workgroup (ftab_steps): rows R_j .. R_{j+fts} staged once (consecutive steps share them).  The row
+// minimum R_j[c'] = min_b fl(Kmin_j[b] + R_{j+1}[c' - b]) is the recursion's own output, read instead of recomputed
+// (the same candidates and an exact min: the same double).
+int ftab_steps(int RP) { return std::max(1, std::min(8, 65536 / (RP * 8) - 1)); }
+size_t ftab_lds(int RP, int BWP) {
+  const int f = ftab_steps(RP);
+  return ((size_t)(f + 1) * RP + 2 * (size_t)f * BWP) * sizeof(double) + (size_t)f * BWP * sizeof(int);
+}
+__global__ __launch_bounds__(256) void k_pinf_ftab(ProblemDev P, PinfDev D, int fts) {
   if (gate_closed(P.gate)) return;
   extern __shared__ __attribute__((aligned(16))) double fsm[];
-  const int j = blockIdx.x + 1, k = blockIdx.y, nt = P.nt, RP = P.RP, B = P.B, BWP = D.BWP;
-  const bool term = (j == nt - 1);
-  double *Rn = fsm, *km = Rn + RP, *k2 = km + BWP;  // R_{j+1} row, class minima / second values of step j
-  int *kf = reinterpret_cast<int *>(k2 + BWP);
-  const size_t crow = ((size_t)k * nt + j) * BWP;
-  for (int q = threadIdx.x; q < BWP; q += blockDim.x) {
-    km[q] = D.kmin[crow + q];
-    k2[q] = D.k2[crow + q];
-    kf[q] = D.kfirst[crow + q];
+  const int k = blockIdx.y, nt = P.nt, RP = P.RP, B = P.B, BWP = D.BWP, BW = D.BW;
+  const int j0 = 1 + (int)blockIdx.x * fts, n = min(fts, nt - j0);  // steps j0 .. j0 + n - 1
+  double *Rs = fsm;                                                // rows j0 .. j0 + n (the last if < nt)
+  double *km = Rs + (size_t)(fts + 1) * RP, *k2 = km + fts * BWP;
+  int *kf = reinterpret_cast<int *>(k2 + fts * BWP);
+  const int nrow = j0 + n <= nt - 1 ? n + 1 : n;
+  const double *Rk = D.R + (size_t)k * nt * RP;
+  for (int e = threadIdx.x; e < nrow * RP; e += blockDim.x) Rs[e] = Rk[(size_t)j0 * RP + e];
+  const size_t crow = ((size_t)k * nt + j0) * BWP;
+  for (int e = threadIdx.x; e < n * BWP; e += blockDim.x) {
+    km[e] = D.kmin[crow + e];
+    k2[e] = D.k2[crow + e];
+    kf[e] = D.kfirst[crow + e];
   }
-  if (!term)
-    for (int c = threadIdx.x; c < RP; c += blockDim.x) Rn[c] = D.R[((size_t)k * nt + j + 1) * RP + c];
-  const double kab = D.kabs[(size_t)k * nt + j - 1];
   __syncthreads();
-  uint8_t *out = D.ftab + ((size_t)k * nt + j) * RP;
-  for (int cp = threadIdx.x; cp < RP; cp += blockDim.x) {
-    unsigned res = 0xFFu;
-    if (cp <= B) {
-      double R = INFINITY;
-      for (int b = 0; b < BWP; ++b) {
-        const double x = term ? (b == cp ? 0.0 : INFINITY) : (cp - b >= 0 ? Rn[cp - b] : INFINITY);
-        if (km[b] < INFINITY && x < INFINITY) R = fmin(R, term ? km[b] : km[b] + x);
-      }
+  for (int s = 0; s < n; ++s) {
+    const int j = j0 + s;
+    const bool term = (j == nt - 1);
+    const double *Rj = Rs + (size_t)s * RP, *Rn = Rj + RP, *kmj = km + s * BWP, *k2j = k2 + s * BWP;
+    const int *kfj = kf + s * BWP;
+    const double kab = D.kabs[(size_t)k * nt + j - 1];
+    uint8_t *out = D.ftab + ((size_t)k * nt + j) * RP;
+    for (int cp = threadIdx.x; cp < RP; cp += blockDim.x) {
+      unsigned res = 0xFFu;
+      const double R = cp <= B ? Rj[cp] : INFINITY;
       if (R < INFINITY) {
         bool safe = true;
         int best = INT_MAX, bb = -1;
-        for (int b = 0; b < BWP; ++b) {
+        for (int b = 0; b < BW; ++b) {
           const double x = term ? (b == cp ? 0.0 : INFINITY) : (cp - b >= 0 ? Rn[cp - b] : INFINITY);
-          if (!(km[b] < INFINITY && x < INFINITY)) continue;
-          const double V = term ? km[b] : km[b] + x;
+          if (!(kmj[b] < INFINITY && x < INFINITY)) continue;
+          const double V = term ? kmj[b] : kmj[b] + x;
           if (V == R) {
-            if (kf[b] < best) best = kf[b], bb = b;
-            if (k2[b] < INFINITY) {  // a level of the class with a larger K must not round onto the target
-              const double V2 = term ? k2[b] : k2[b] + x;
+            if (kfj[b] < best) best = kfj[b], bb = b;
+            if (k2j[b] < INFINITY) {  // a level of the class with a larger K must not round onto the target
+              const double V2 = term ? k2j[b] : k2j[b] + x;
               if (!(V2 - R > (kab + fmax(fabs(R), fabs(V2))) * 0x1p-50)) safe = false;
             }
           } else if (!(V - R > (kab + fmax(fabs(R), fabs(V))) * 0x1p-50)) {
@@ -1636,42 +1668,78 @@ __global__ __launch_bounds__(256) void k_pinf_ftab(ProblemDev P, PinfDev D) {
         }
         if (safe && bb >= 0 && best >= 0) res = (unsigned)bb;
       }
+      out[cp] = (uint8_t)res;
     }
-    out[cp] = (uint8_t)res;
   }
 }
 
-// composed map of segment g: the row after steps j0 .. j1 for every entry row (one thread per entry row)
-__global__ __launch_bounds__(256) void k_pinf_fseg(ProblemDev P, PinfDev D, int G, int nseg) {
+// The chains of the segmented walk are dependent reads of ftab, one byte per step; read from global memory each step is
+// a round trip (≈0.3 µs).  So a segment's class rows are staged into the LDS, FCH rows at a time (coalesced 16-byte
+// copies), and the chains step through the LDS.
+constexpr int kFwalkLds = 64 * 1024;  // LDS bytes of staged class rows per workgroup
+__device__ __forceinline__ int fwalk_rows(int RP) { return kFwalkLds / RP; }
+// rows j0 .. j0 + n - 1 of subproblem k's class table into `dst` (RP bytes each; RP is a multiple of 64)
+__device__ __forceinline__ void fwalk_stage(const uint8_t *tab, int RP, int j0, int n, uint8_t *dst) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(tab + (size_t)j0 * RP);
+  uint4 *d = reinterpret_cast<uint4 *>(dst);
+  const int n16 = n * RP / 16;
+  for (int e = threadIdx.x; e < n16; e += blockDim.x) d[e] = src[e];
+}
+
+// composed map of segment g: the row after steps j0 .. j1 for every entry row (one thread per entry row; B + 1 <= 8192)
+__global__ __launch_bounds__(1024) void k_pinf_fseg(ProblemDev P, PinfDev D, int G, int nseg) {
   if (gate_closed(P.gate)) return;
-  const int g = blockIdx.x, k = blockIdx.z, nt = P.nt, RP = P.RP;
-  const int cp0 = blockIdx.y * blockDim.x + threadIdx.x;
-  if (cp0 > P.B) return;
+  extern __shared__ __attribute__((aligned(16))) uint8_t frow[];
+  const int g = blockIdx.x, k = blockIdx.y, nt = P.nt, RP = P.RP, B = P.B, FCH = fwalk_rows(RP);
   const int j0 = 1 + g * G, j1 = (j0 + G - 1 < nt - 1 ? j0 + G - 1 : nt - 1);
   const uint8_t *tab = D.ftab + (size_t)k * nt * RP;
-  int c = cp0;
-  for (int j = j0; j <= j1; ++j) {
-    const unsigned b = tab[(size_t)j * RP + c];
-    if (b == 0xFFu) {
-      c = -1;
-      break;
+  constexpr int PER = 8;
+  int cs[PER];
+#pragma unroll
+  for (int e = 0; e < PER; ++e) cs[e] = (int)threadIdx.x + e * (int)blockDim.x;
+  for (int jb = j0; jb <= j1; jb += FCH) {
+    const int n = min(FCH, j1 - jb + 1);
+    __syncthreads();  // every chain is past the previous chunk
+    fwalk_stage(tab, RP, jb, n, frow);
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      int cc = cs[e];
+      if ((int)threadIdx.x + e * (int)blockDim.x > B || cc < 0) continue;
+      for (int j = jb; j < jb + n; ++j) {
+        const unsigned bb = frow[(size_t)(j - jb) * RP + cc];
+        if (bb == 0xFFu) {
+          cc = -1;
+          break;
+        }
+        if (j < nt - 1) cc -= (int)bb;
+      }
+      cs[e] = cc;
     }
-    if (j < nt - 1) c -= (int)b;
   }
-  D.fseg[((size_t)k * nseg + g) * RP + cp0] = c;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int cp0 = (int)threadIdx.x + e * (int)blockDim.x;
+    if (cp0 <= B) D.fseg[((size_t)k * nseg + g) * RP + cp0] = cs[e];
+  }
 }
 
-// one workgroup per subproblem: thread 0 chains the segment maps from the start cell, then every thread expands
-// its segments into ranks; fneed[k] = 1 hands the subproblem to the serial walk
-__global__ __launch_bounds__(1024) void k_pinf_fexpand(ProblemDev P, LevelsDev Lv, PinfDev D, const Start *start,
-                                                       int32_t *ranks, int G, int nseg) {
+// one workgroup per (segment g, subproblem): thread 0 chains the segment maps from the start cell through segment g
+// (the chain must exist through this segment's own steps; the last segment's workgroup thereby checks the whole chain
+// and owns the verdict: fneed[k] = 1 hands the subproblem to the serial walk), then walks the segment's steps through
+// its staged class rows, and every thread writes the ranks of the steps
+constexpr int kFexpandSteps = 512;  // steps staged per round (the classes of a round in s_b)
+__global__ __launch_bounds__(256) void k_pinf_fexpand(ProblemDev P, LevelsDev Lv, PinfDev D, const Start *start,
+                                                      int32_t *ranks, int G, int nseg) {
   if (gate_closed(P.gate)) return;
-  extern __shared__ int sent[];  // [nseg] entry row of each segment
-  __shared__ int s_ok;
-  const int k = blockIdx.x, nt = P.nt, RP = P.RP, M = P.M;
+  extern __shared__ __attribute__((aligned(16))) uint8_t frow[];
+  __shared__ int s_ok, s_c;
+  __shared__ uint8_t s_b[kFexpandSteps];
+  const int g = blockIdx.x, k = blockIdx.y, nt = P.nt, RP = P.RP, M = P.M;
+  const int FCH = min(fwalk_rows(RP), kFexpandSteps);
   const Start st = start[k];
   if (st.status != MIOC_OK || nt == 1) {  // nothing to walk: the serial walk returns at once as well
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && g == nseg - 1) {
       D.fneed[k] = 0;
       if (st.status == MIOC_OK) ranks[(size_t)k * nt] = st.r;
     }
@@ -1679,36 +1747,50 @@ __global__ __launch_bounds__(1024) void k_pinf_fexpand(ProblemDev P, LevelsDev L
   }
   if (threadIdx.x == 0) {
     int cp = st.c - p_bt(Lv.nuval + (size_t)st.r * M, P.uold + (size_t)k * nt * M, M);
-    int ok = cp >= 0 && cp <= P.B;
-    for (int g = 0; ok && g < nseg; ++g) {
-      sent[g] = cp;
-      cp = D.fseg[((size_t)k * nseg + g) * RP + cp];
+    int ok = cp >= 0 && cp <= P.B, entry = -1;
+    for (int h = 0; ok && h <= g; ++h) {
+      if (h == g) entry = cp;
+      cp = D.fseg[((size_t)k * nseg + h) * RP + cp];
       ok = cp >= 0;
     }
+    if (g == nseg - 1) {
+      D.fneed[k] = !ok;
+      if (!ok) atomicAdd(D.fneed + P.K, 1);
+      else ranks[(size_t)k * nt] = st.r;
+    }
     s_ok = ok;
-    D.fneed[k] = !ok;
-    if (!ok) atomicAdd(D.fneed + P.K, 1);
-    else ranks[(size_t)k * nt] = st.r;
+    s_c = entry;
   }
   __syncthreads();
   if (!s_ok) return;
+  const int j0 = 1 + g * G, j1 = (j0 + G - 1 < nt - 1 ? j0 + G - 1 : nt - 1);
   const uint8_t *tab = D.ftab + (size_t)k * nt * RP;
   const int32_t *kfk = D.kfirst + (size_t)k * nt * D.BWP;
   int32_t *rk = ranks + (size_t)k * nt;
-  for (int g = threadIdx.x; g < nseg; g += blockDim.x) {
-    const int j0 = 1 + g * G, j1 = (j0 + G - 1 < nt - 1 ? j0 + G - 1 : nt - 1);
-    int c = sent[g];
-    for (int j = j0; j <= j1; ++j) {
-      const int b = (int)tab[(size_t)j * RP + c];  // not 0xFF: the chain through this segment exists
-      rk[j] = kfk[(size_t)j * D.BWP + b];
-      c -= b;
+  int c = s_c;
+  for (int jb = j0; jb <= j1; jb += FCH) {
+    const int n = min(FCH, j1 - jb + 1);
+    __syncthreads();
+    fwalk_stage(tab, RP, jb, n, frow);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int j = jb; j < jb + n; ++j) {
+        const int b = (int)frow[(size_t)(j - jb) * RP + c];  // not 0xFF: the chain through this segment exists
+        s_b[j - jb] = (uint8_t)b;
+        c -= b;
+      }
     }
+    __syncthreads();
+    for (int j = jb + (int)threadIdx.x; j < jb + n; j += blockDim.x) rk[j] = kfk[(size_t)j * D.BWP + s_b[j - jb]];
   }
 }
 
+// G: steps per segment, about 2·sqrt(nt) (the chain over the segment maps is a global read per segment, a segment's
+// own steps are LDS reads), a power of two in [64, 4096], and at most 4096 segments
 void pinf_fplan(int nt, int *G, int *nseg) {
   const int steps = nt > 1 ? nt - 1 : 1;
-  int g = 256;
+  int g = 64;
+  while (g < 4096 && (double)g * g < 4.0 * steps) g *= 2;
   while ((steps + g - 1) / g > 4096) g *= 2;
   *G = g;
   *nseg = (steps + g - 1) / g;
@@ -1720,12 +1802,15 @@ hipError_t launch_pinf_fwalk(hipStream_t s, const ProblemDev &P, const LevelsDev
   int G, nseg;
   pinf_fplan(P.nt, &G, &nseg);
   if (P.nt > 1) {
-    const size_t lds = ((size_t)P.RP + 2 * D.BWP) * sizeof(double) + (size_t)D.BWP * sizeof(int);
-    hipLaunchKernelGGL(k_pinf_ftab, dim3(P.nt - 1, P.K), dim3(256), lds, s, P, D);
-    hipLaunchKernelGGL(k_pinf_fseg, dim3(nseg, (P.B + 256) / 256, P.K), dim3(256), 0, s, P, D, G, nseg);
+    const int fts = ftab_steps(P.RP);
+    hipLaunchKernelGGL(k_pinf_ftab, dim3((P.nt - 1 + fts - 1) / fts, P.K), dim3(256), ftab_lds(P.RP, D.BWP), s, P, D,
+                       fts);
+    const size_t flds = (size_t)(kFwalkLds / P.RP) * P.RP;  // fwalk_rows(RP) staged class rows
+    hipLaunchKernelGGL(k_pinf_fseg, dim3(nseg, P.K), dim3(1024), flds, s, P, D, G, nseg);
+    hipLaunchKernelGGL(k_pinf_fexpand, dim3(nseg, P.K), dim3(256), flds, s, P, Lv, D, start, ranks, G, nseg);
+  } else {
+    hipLaunchKernelGGL(k_pinf_fexpand, dim3(1, P.K), dim3(256), 0, s, P, Lv, D, start, ranks, G, nseg);
   }
-  hipLaunchKernelGGL(k_pinf_fexpand, dim3(P.K), dim3(1024), (size_t)nseg * sizeof(int), s, P, Lv, D, start, ranks,
-                     G, nseg);
   return hipGetLastError();
 }
 

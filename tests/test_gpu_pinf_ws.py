@@ -46,7 +46,8 @@ def _check(oracle_c, lv, lt, df, uo, B, beta, dt, budgets, spin=0):
 @pytest.mark.parametrize("key", ["C1", "C2", "C3"])
 def test_ws_sos1_full_size_vs_oracle(oracle_c, key, spin):
     """C1-C3 at full size (B + 1 = 86 / 820 / 820 rows: 2 / 13 / 13 segments).  spin = 1: the first unmet wait
-    abandons the launch and the host redoes the DP in one workgroup before anything reads R."""
+    abandons the launch and the one-workgroup recursion launched behind it (gated by the error word) redoes the DP on
+    the device before anything reads R."""
     cfg = CONFIGS[key]
     lt, df, uo = make_inputs(cfg)
     lv = Levels(lt.nu, [tuple(int(x) for x in t) for t in lt.tuples])
