@@ -38,6 +38,7 @@ template <typename T>
 int grow(mioc_ctx *ctx, T **p, size_t *cap_bytes, size_t need_bytes, const char *what) {
   if (*p && *cap_bytes >= need_bytes) return MIOC_OK;
   if (*p) {
+    (void)hipDeviceSynchronize();  // the old buffer may still be read by a backtrack in flight on the other stream
     hipFree(*p);
     *p = nullptr;
     *cap_bytes = 0;
@@ -91,6 +92,28 @@ ProblemDev problem_dev(const mioc_ctx *ctx) {
 
 void ev_collect(mioc_ctx *ctx);
 
+// the context's current inputs and p = Inf tables <-> its DP slots
+void slot_save(mioc_ctx *ctx) {
+  mioc_ctx::Slot &q = ctx->slots[ctx->slot];
+  q.df = ctx->d_df, q.uold = ctx->d_uold, q.in_cap = ctx->in_cap;
+  q.kmin = ctx->pinf.kmin, q.k2 = ctx->pinf.k2, q.kfirst = ctx->pinf.kfirst, q.R = ctx->pinf.R, q.kabs = ctx->pinf.kabs;
+  q.cap_k = ctx->pinf_cap_k, q.cap_R = ctx->pinf_cap_R, q.cap_kabs = ctx->pinf_cap_kabs;
+}
+void slot_load(mioc_ctx *ctx) {
+  const mioc_ctx::Slot &q = ctx->slots[ctx->slot];
+  ctx->d_df = q.df, ctx->d_uold = q.uold, ctx->in_cap = q.in_cap;
+  ctx->pinf.kmin = q.kmin, ctx->pinf.k2 = q.k2, ctx->pinf.kfirst = q.kfirst, ctx->pinf.R = q.R, ctx->pinf.kabs = q.kabs;
+  ctx->pinf_cap_k = q.cap_k, ctx->pinf_cap_R = q.cap_R, ctx->pinf_cap_kabs = q.cap_kabs;
+}
+// a new DP: the other slot, once the backtracks that read it are done (on the device: the stream waits)
+int begin_dp(mioc_ctx *ctx) {
+  slot_save(ctx);
+  ctx->slot ^= 1;
+  slot_load(ctx);
+  if (ctx->bt_rec[ctx->slot]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_bt[ctx->slot], 0));
+  return MIOC_OK;
+}
+
 void free_all(mioc_ctx *ctx) {
   if (ctx->d_runflags) hipFree(ctx->d_runflags);
   if (ctx->d_chain) hipFree(ctx->d_chain);
@@ -98,10 +121,17 @@ void free_all(mioc_ctx *ctx) {
   if (ctx->d_segflags) hipFree(ctx->d_segflags);
   if (ctx->h_run_err) hipHostFree(ctx->h_run_err);
   if (ctx->h_trm_poll) hipHostFree(ctx->h_trm_poll);
+  if (ctx->bstream) hipStreamSynchronize(ctx->bstream);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  slot_save(ctx);  // the current inputs and p = Inf tables are one of the slots
+  for (auto &q : ctx->slots) {
+    void *sp[] = {q.df, q.uold, q.kmin, q.k2, q.kfirst, q.R, q.kabs};
+    for (void *p : sp)
+      if (p) hipFree(p);
+  }
   void *ptrs[] = {ctx->d_nuval, ctx->d_nuint,  ctx->d_gidx,      ctx->d_numin,       ctx->d_numax,
-                  ctx->d_costlut, ctx->d_costtab, ctx->d_df,       ctx->d_uold,        ctx->d_front,
-                  ctx->d_U,     ctx->pinf.kmin, ctx->pinf.k2,      ctx->pinf.kfirst,   ctx->pinf.R,
-                  ctx->pinf.kabs, ctx->pinf.ftab, ctx->pinf.fseg, ctx->pinf.fneed,
+                  ctx->d_costlut, ctx->d_costtab, ctx->d_front,
+                  ctx->d_U,     ctx->pinf.ftab, ctx->pinf.fseg, ctx->pinf.fneed,
                   ctx->d_start, ctx->d_ranks,   ctx->d_flags,      ctx->d_uout_own,    ctx->d_phistar_own,
                   ctx->d_status_own, ctx->d_stage,    ctx->d_counters, ctx->d_perm, ctx->d_same2, ctx->d_strad,
                   ctx->d_vals,  ctx->d_voff,    ctx->d_g2r,   ctx->d_tvw,        ctx->d_pred_own, ctx->d_ode_state};
@@ -112,6 +142,10 @@ void free_all(mioc_ctx *ctx) {
   ctx->heat = nullptr;
   ev_collect(ctx);
   for (auto &pr : ctx->ev_pool) hipEventDestroy(pr.begin), hipEventDestroy(pr.end);
+  if (ctx->ev_dp) hipEventDestroy(ctx->ev_dp);
+  for (hipEvent_t e : ctx->ev_bt)
+    if (e) hipEventDestroy(e);
+  if (ctx->bstream) hipStreamDestroy(ctx->bstream);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
 }
 
@@ -194,7 +228,7 @@ void ev_collect(mioc_ctx *ctx) {
     ctx->ev_pending[w].clear();
   }
 }
-void ev_begin(mioc_ctx *ctx, int which, const char *name) {
+void ev_begin(mioc_ctx *ctx, int which, const char *name, hipStream_t st = nullptr) {
   if (!ctx->timing) return;
   if (ctx->ev_pending[which].size() >= 256) ev_collect(ctx);
   mioc_ctx::EvPair pr;
@@ -205,14 +239,14 @@ void ev_begin(mioc_ctx *ctx, int which, const char *name) {
     hipEventCreate(&pr.begin);
     hipEventCreate(&pr.end);
   }
-  hipEventRecord(pr.begin, ctx->stream);
+  hipEventRecord(pr.begin, st ? st : ctx->stream);
   ctx->ev_open[which] = pr;
   ctx->stat_name[which] = name;
 }
-void ev_end(mioc_ctx *ctx, int which, int64_t launches) {
+void ev_end(mioc_ctx *ctx, int which, int64_t launches, hipStream_t st = nullptr) {
   if (!ctx->timing) return;
   mioc_ctx::EvPair pr = ctx->ev_open[which];
-  hipEventRecord(pr.end, ctx->stream);
+  hipEventRecord(pr.end, st ? st : ctx->stream);
   pr.launches = launches;
   ctx->ev_pending[which].push_back(pr);
 }
@@ -240,9 +274,10 @@ int run_bellman(mioc_ctx *ctx) {
     pinf_flags_zeroed = true;
   }
   // validation pass: finite df, integral u_old, max budget class
-  HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int32_t), ctx->stream));
+  // (words 0, 1 only: 2, 3 are a backtrack's, which may still run on the other stream)
+  HIP_TRY(ctx, hipMemsetAsync(ctx->d_flags, 0, 2 * sizeof(int32_t), ctx->stream));
   HIP_TRY(ctx, launch_validate(ctx->stream, P, ctx->d_numin, ctx->d_numax, ctx->d_flags));
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->h_flags, ctx->d_flags, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->h_flags, ctx->d_flags, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->h_flags[0] & 2)
     return fail(ctx, MIOC_EINEXACT, "u_old has a non-integral entry: convert(Int64, abs(nu - u_old)) "
@@ -550,6 +585,18 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
   if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "backtrack called before bellman");
   if (B_use < 0 || B_use > ctx->B)
     return fail(ctx, MIOC_ESTATE, "B_use must satisfy 0 <= B_use <= B of the last bellman call");
+  // p = Inf (outside the device TRM control): on the second stream, after this DP, so that the next bellman's kernels
+  // overlap it; the other algorithms run on the context's stream after any such backtrack in flight
+  const bool async_bt = ctx->algo == MIOC_ALGO_PINF && !ctx->gate;
+  if (!async_bt) {
+    const int rcj = join_bt(ctx);
+    if (rcj) return rcj;
+  }
+  hipStream_t bs = async_bt ? ctx->bstream : ctx->stream;
+  if (async_bt) {
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_dp, ctx->stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(bs, ctx->ev_dp, 0));
+  }
   ProblemDev P = problem_dev(ctx);
   LevelsDev Lv = levels_dev(ctx);
   const size_t K = (size_t)ctx->K, nt = (size_t)ctx->nt;
@@ -599,21 +646,26 @@ int run_backtrack(mioc_ctx *ctx, int64_t B_use, double *d_u_out, double *d_phi_s
       if (rc) return rc;
     }
     // k_pinf_start also zeroes the walk's fallback counters (d_flags[2..3]) and, for the segmented walk, fneed
-    HIP_TRY(ctx, launch_pinf_start(ctx->stream, P, Lv, D, (int)B_use, ctx->d_start, ctx->d_flags + 2,
-                                   fwalk ? D.fneed : nullptr));
+    HIP_TRY(ctx, launch_pinf_start(bs, P, Lv, D, (int)B_use, ctx->d_start, ctx->d_flags + 2, fwalk ? D.fneed : nullptr));
     if (fwalk) {
-      ev_begin(ctx, 1, "k_pinf_fwalk");
-      HIP_TRY(ctx, launch_pinf_fwalk(ctx->stream, P, Lv, D, ctx->d_start, ctx->d_ranks));
+      ev_begin(ctx, 1, "k_pinf_fwalk", bs);
+      HIP_TRY(ctx, launch_pinf_fwalk(bs, P, Lv, D, ctx->d_start, ctx->d_ranks));
       // subproblems whose chain met a state-dependent row: the serial walk (the others return at once)
-      HIP_TRY(ctx, launch_pinf_walk(ctx->stream, P, Lv, D, ctx->d_start, ctx->d_ranks, ctx->d_flags + 2, D.fneed));
-      ev_end(ctx, 1, 1);
+      HIP_TRY(ctx, launch_pinf_walk(bs, P, Lv, D, ctx->d_start, ctx->d_ranks, ctx->d_flags + 2, D.fneed));
+      ev_end(ctx, 1, 1, bs);
     } else {
-      ev_begin(ctx, 1, "k_pinf_walk");
-      HIP_TRY(ctx, launch_pinf_walk(ctx->stream, P, Lv, D, ctx->d_start, ctx->d_ranks, ctx->d_flags + 2, nullptr));
-      ev_end(ctx, 1, 1);
+      ev_begin(ctx, 1, "k_pinf_walk", bs);
+      HIP_TRY(ctx, launch_pinf_walk(bs, P, Lv, D, ctx->d_start, ctx->d_ranks, ctx->d_flags + 2, nullptr));
+      ev_end(ctx, 1, 1, bs);
     }
   }
-  HIP_TRY(ctx, launch_expand(ctx->stream, P, Lv, ctx->d_start, ctx->d_ranks, d_u_out, d_phi_star, d_status));
+  HIP_TRY(ctx, launch_expand(bs, P, Lv, ctx->d_start, ctx->d_ranks, d_u_out, d_phi_star, d_status));
+  if (async_bt) {
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_bt[ctx->slot], bs));
+    ctx->bt_rec[ctx->slot] = true;
+    ctx->bt_pending = true;
+    ctx->bt_last = ctx->slot;
+  }
   ctx->have_path = true;
   return MIOC_OK;
 }
@@ -668,6 +720,15 @@ int set_problem(mioc_ctx *ctx, int64_t K, int64_t nx, int64_t nt, int64_t B, dou
 
 }  // namespace
 
+int mioc::join_bt(mioc_ctx *ctx) {
+  if (!ctx->bt_pending) return MIOC_OK;
+  (void)hipSetDevice(ctx->device);
+  ctx->bt_pending = false;
+  if (hipStreamWaitEvent(ctx->stream, ctx->ev_bt[ctx->bt_last], 0) != hipSuccess)
+    return fail(ctx, MIOC_EHIP, "hipStreamWaitEvent failed");
+  return MIOC_OK;
+}
+
 // ==================================================================================================
 // C ABI
 // ==================================================================================================
@@ -687,6 +748,10 @@ int32_t mioc_create(int32_t device, mioc_ctx **out) {
     return MIOC_EHIP;
   }
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->bstream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_dp, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_bt[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_bt[1], hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&ctx->d_flags, 16) != hipSuccess || hipMalloc(&ctx->d_pred_own, 64) != hipSuccess || hipHostMalloc(&ctx->h_flags, 16, 0) != hipSuccess) {
     free_all(ctx);
     delete ctx;
@@ -752,6 +817,7 @@ int32_t mioc_set_option(mioc_ctx *ctx, int32_t option, int64_t value) {
 int32_t mioc_set_levels(mioc_ctx *ctx, int64_t M, const int64_t *counts, const int64_t *values, int64_t L,
                         const int32_t *tuples) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   if (M < 1 || M > kMaxM) return fail(ctx, MIOC_EINVAL, "number of controls must be in [1, 8]");
   if (!counts || !values || !tuples) return fail(ctx, MIOC_EINVAL, "null level arrays");
   if (L < 1 || L > 65535) return fail(ctx, MIOC_EINVAL, "number of admissible tuples must be in [1, 65535]");
@@ -863,6 +929,7 @@ int32_t mioc_set_levels(mioc_ctx *ctx, int64_t M, const int64_t *counts, const i
 int32_t mioc_set_cost(mioc_ctx *ctx, int32_t p_kind, int64_t p_int, double beta, int64_t table_len,
                       const double *table) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   if (p_kind < MIOC_P_INF || p_kind > MIOC_P_TABLE) return fail(ctx, MIOC_EINVAL, "unknown p_kind");
   if (!std::isfinite(beta)) return fail(ctx, MIOC_EINVAL, "beta must be finite");
   if (p_kind == MIOC_P_INTLUT && (p_int < 2 || p_int > 8))
@@ -887,6 +954,8 @@ int32_t mioc_bellman_batch_device(mioc_ctx *ctx, int64_t K, const double *d_df, 
   int rc = check_ready(ctx);
   if (rc) return rc;
   if (!d_df || !d_u_old) return fail(ctx, MIOC_EINVAL, "null input pointer");
+  rc = begin_dp(ctx);
+  if (rc) return rc;
   rc = set_problem(ctx, K, nx, nt, B, dt);
   if (rc) return rc;
   const size_t bytes = (size_t)K * nx * nt * sizeof(double);
@@ -900,6 +969,8 @@ int32_t mioc_bellman(mioc_ctx *ctx, const double *df, const double *u_old, int64
   int rc = check_ready(ctx);
   if (rc) return rc;
   if (!df || !u_old) return fail(ctx, MIOC_EINVAL, "null input pointer");
+  rc = begin_dp(ctx);
+  if (rc) return rc;
   rc = set_problem(ctx, 1, nx, nt, B, dt);
   if (rc) return rc;
   const size_t bytes = (size_t)nx * nt * sizeof(double);
@@ -952,6 +1023,7 @@ int32_t mioc_backtrack(mioc_ctx *ctx, int64_t B_use, double *u_out, double *phi_
   if (!rc && !ctx->d_status_own) rc = grow(ctx, &ctx->d_status_own, &c2, 16, "status staging");
   if (rc) return rc;
   rc = run_backtrack(ctx, B_use, ctx->d_uout_own, ctx->d_phistar_own, ctx->d_status_own);
+  if (!rc) rc = join_bt(ctx);  // the copies below run on the context's stream
   if (rc) return rc;
   double ps = 0.0;
   int32_t st = 0;
@@ -979,6 +1051,8 @@ static int32_t batch_host(mioc_ctx *ctx, int64_t K, const double *df, const doub
                           int64_t B, double dt, int64_t B_use, double *u_out, double *phi_star, int32_t *status) {
   int rc = check_ready(ctx);
   if (rc) return rc;
+  rc = begin_dp(ctx);
+  if (rc) return rc;
   rc = set_problem(ctx, K, nx, nt, B, dt);
   if (rc) return rc;
   const size_t n = (size_t)K * nx * nt;
@@ -993,6 +1067,7 @@ static int32_t batch_host(mioc_ctx *ctx, int64_t K, const double *df, const doub
   if (!rc) rc = grow(ctx, &d_phi, &c1, (size_t)K * sizeof(double), "multi-device phi staging");
   if (!rc) rc = grow(ctx, &d_st, &c2, (size_t)K * sizeof(int32_t), "multi-device status staging");
   if (!rc) rc = run_backtrack(ctx, B_use, d_u, d_phi, d_st);
+  if (!rc) rc = join_bt(ctx);  // the copies below run on the context's stream
   if (!rc && hipMemcpyAsync(u_out, d_u, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
     rc = fail(ctx, MIOC_EHIP, "u copy-out failed");
   if (!rc && phi_star &&
@@ -1012,6 +1087,7 @@ static int32_t batch_host(mioc_ctx *ctx, int64_t K, const double *df, const doub
 int32_t mioc_ode_eval_device(mioc_ctx *ctx, int32_t problem, int64_t K, const double *d_x, int64_t nx, int64_t nt,
                              double T0, double T1, const double *params, int32_t nparams, double *d_J, double *d_df) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   // the examples' constants (example_fishing.jl, example_doubletank.jl, example_vanderpol.jl)
   static const double fishing[14] = {1, 1, 1, 1, 1, 1, 0.2, 0.4, 0.01, 0.1, 0.2, 0.1, 0.5, 0.7};
   static const double tank[7] = {2, 3, 1, 0.5, 2, 2, 2};
@@ -1038,6 +1114,7 @@ int32_t mioc_ode_eval_device(mioc_ctx *ctx, int32_t problem, int64_t K, const do
 
 int32_t mioc_rand_start_device(mioc_ctx *ctx, int64_t K, int64_t nt, int64_t jumps, uint64_t seed, double *d_u_out) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   if (!ctx->have_levels) return fail(ctx, MIOC_ESTATE, "levels must be set first");
   if (K < 1 || K > INT32_MAX || nt < 1 || nt > (1 << 24) || !d_u_out) return fail(ctx, MIOC_EINVAL, "bad K / nt / u");
   if (jumps < 0) jumps = nt / 10;
@@ -1085,6 +1162,7 @@ int trm_check_err(mioc_ctx *ctx);
 
 int32_t mioc_synchronize(mioc_ctx *ctx) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   ev_collect(ctx);
@@ -1096,10 +1174,15 @@ int32_t mioc_synchronize(mioc_ctx *ctx) {
   return check_run(ctx);
 }
 
-void *mioc_stream(mioc_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+void *mioc_stream(mioc_ctx *ctx) {
+  if (!ctx) return nullptr;
+  (void)join_bt(ctx);  // ordered after the backtracks in flight on the second stream
+  return (void *)ctx->stream;
+}
 
 int32_t mioc_get_ranks_device(mioc_ctx *ctx, int32_t *d_ranks_out) {
   if (!ctx || !d_ranks_out) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   if (!ctx->have_path) return fail(ctx, MIOC_ESTATE, "no backtrack result to read");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipMemcpyAsync(d_ranks_out, ctx->d_ranks, (size_t)ctx->K * ctx->nt * sizeof(int32_t),
@@ -1139,6 +1222,7 @@ TrmDev trm_dev(const mioc_ctx *ctx, int mode, int64_t K, int64_t nt) {
 
 int trm_ready(mioc_ctx *ctx) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   if (!ctx->have_levels || !ctx->have_cost) return fail(ctx, MIOC_ESTATE, "levels and cost must be set first");
   if (ctx->p_kind == MIOC_P_TABLE && !ctx->d_g2r)
     return fail(ctx, MIOC_EINVAL, "TV_p with MIOC_P_TABLE needs the level grid lookup (grid too large)");
@@ -1232,6 +1316,7 @@ int64_t mioc_trm_state_bytes(int64_t K) { return K < 1 || K > 4096 ? -1 : (int64
 
 int32_t mioc_trm_attach(mioc_ctx *ctx, void *d_state) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   ctx->gate = static_cast<const int32_t *>(d_state);
   return MIOC_OK;
 }
@@ -1239,6 +1324,7 @@ int32_t mioc_trm_attach(mioc_ctx *ctx, void *d_state) {
 int32_t mioc_trm_outer_begin_device(mioc_ctx *ctx, int64_t K, void *d_state, const double *d_tv_u, double D0,
                                     int64_t B, int32_t *d_budgets) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   if (K < 1 || K > 4096 || !d_state || !d_tv_u || !d_budgets) return fail(ctx, MIOC_EINVAL, "bad TRM state arguments");
   if (B < 0 || B > (1 << 20) || !std::isfinite(D0)) return fail(ctx, MIOC_EINVAL, "bad budget");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1252,6 +1338,7 @@ int32_t mioc_trm_inner_end_device(mioc_ctx *ctx, int64_t K, void *d_state, doubl
                                   int32_t *d_decision, int64_t n_per_restart, const double *d_trial, double *d_u,
                                   double *d_u_old) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   if (!ctx->have_cost) return fail(ctx, MIOC_ESTATE, "mioc_set_cost has not been called");
   if (K < 1 || K > 4096 || !d_state || !d_int_val || !d_tv_new || !d_J_new || !d_J_old || !d_J || !d_tv_u ||
       !d_budgets || !d_trial || !d_u || !d_u_old || n_per_restart < 1)
@@ -1266,6 +1353,7 @@ int32_t mioc_trm_inner_end_device(mioc_ctx *ctx, int64_t K, void *d_state, doubl
 
 int32_t mioc_trm_poll(mioc_ctx *ctx, const void *d_state, int32_t *out) {
   if (!ctx || !d_state || !out) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   if (!ctx->h_trm_poll) HIP_TRY(ctx, hipHostMalloc(&ctx->h_trm_poll, 16, 0));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->h_trm_poll, d_state, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
@@ -1295,6 +1383,7 @@ int32_t mioc_last_algo(mioc_ctx *ctx) { return ctx ? ctx->algo : MIOC_EINVAL; }
 
 int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
   if (!ctx || !counters || n < 0) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   int32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f[4] = {0, 0, 0, 0};
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1320,6 +1409,7 @@ int32_t mioc_diagnostics(mioc_ctx *ctx, int64_t *counters, int32_t n) {
 
 int32_t mioc_get_argmin_table(mioc_ctx *ctx, int64_t k, int64_t step, int32_t *U_out) {
   if (!ctx || !U_out) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   if (!ctx->have_dp) return fail(ctx, MIOC_ESTATE, "no bellman result to read");
   if (k < 0 || k >= ctx->K || step < 0 || step + 1 >= ctx->nt)
     return fail(ctx, MIOC_EINVAL, "subproblem or step out of range (0 <= step < nt-1)");

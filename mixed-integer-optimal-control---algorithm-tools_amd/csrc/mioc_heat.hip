@@ -380,6 +380,7 @@ int32_t mioc_heat_setup(mioc_ctx *ctx, int64_t N, int64_t nx, int64_t nt, double
                         const double *M_invA, const double *M_invF, const double *mass, const double *state0,
                         const double *yd) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   if (N < 1 || N > HMAXN)
     return heat_fail(ctx, MIOC_EINVAL, "heat: need 1 <= Nglobal_dofs <= " + std::to_string(HMAXN));
   if (nx < 1 || nx > HMAXNX) return heat_fail(ctx, MIOC_EINVAL, "heat: need 1 <= nx <= 4 controls");
@@ -452,6 +453,7 @@ int32_t mioc_heat_setup(mioc_ctx *ctx, int64_t N, int64_t nx, int64_t nt, double
 
 int32_t mioc_heat_eval_device(mioc_ctx *ctx, int64_t K, const double *d_x, double *d_J, double *d_df) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   HeatState *h = ctx->heat;
   if (!h || !h->ready) return heat_fail(ctx, MIOC_ESTATE, "heat: no successful mioc_heat_setup");
   if (K < 1 || K > INT32_MAX || !d_x) return heat_fail(ctx, MIOC_EINVAL, "heat: bad K / x");
@@ -498,6 +500,7 @@ int32_t mioc_heat_eval_device(mioc_ctx *ctx, int64_t K, const double *d_x, doubl
 
 int32_t mioc_heat_eval(mioc_ctx *ctx, int64_t K, const double *x, double *J, double *df) {
   if (!ctx) return MIOC_EINVAL;
+  MIOC_JOIN_BT(ctx);
   HeatState *h = ctx->heat;
   if (!h || !h->ready) return heat_fail(ctx, MIOC_ESTATE, "heat: no successful mioc_heat_setup");
   if (K < 1 || K > INT32_MAX || !x || (!J && !df)) return heat_fail(ctx, MIOC_EINVAL, "heat: bad K / x / outputs");

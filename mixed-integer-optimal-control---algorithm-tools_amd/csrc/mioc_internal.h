@@ -251,6 +251,15 @@ hipError_t launch_trm_inner_end(hipStream_t s, int K, void *state, double beta, 
 hipError_t launch_ode_eval(hipStream_t s, const int32_t *gate, int problem, int K, int nt, double tau, const double *params, int y0off,
                            const double *X, double *J, double *DF, double *ST);
 
+// orders the context's stream after its in-flight p = Inf backtracks (mioc_api.cpp); every C ABI call that is not a
+// bellman or a backtrack calls it first
+int join_bt(mioc_ctx *ctx);
+#define MIOC_JOIN_BT(ctx)                         \
+  do {                                            \
+    const int rcj_ = mioc::join_bt(ctx);          \
+    if (rcj_) return rcj_;                        \
+  } while (0)
+
 struct HeatState;  // mioc_heat.hip: the PDE heat objective's device matrices (mioc_heat_setup)
 void heat_free(HeatState *h);
 
@@ -367,6 +376,24 @@ struct mioc_ctx {
   double *d_phistar_own = nullptr;
   int32_t *d_status_own = nullptr;
   size_t uout_cap = 0;
+
+  // p = Inf backtrack overlapping the next DP: it runs on bstream (the next bellman's kernels on `stream` meanwhile),
+  // so every DP owns one of two slots of its inputs and p = Inf tables (the backtrack of DP n reads slot n % 2 while
+  // DP n + 1 writes the other).  ev_bt[s]: the last backtrack that read slot s (the bellman that reuses s waits on it);
+  // join_bt orders `stream` after the backtracks before any other call reads their outputs.
+  hipStream_t bstream = nullptr;
+  hipEvent_t ev_dp = nullptr, ev_bt[2] = {nullptr, nullptr};
+  bool bt_rec[2] = {false, false};
+  bool bt_pending = false;
+  int bt_last = 0;
+  int slot = 0;  // the last bellman's slot
+  struct Slot {
+    double *df = nullptr, *uold = nullptr;
+    size_t in_cap = 0;
+    double *kmin = nullptr, *k2 = nullptr, *R = nullptr, *kabs = nullptr;
+    int32_t *kfirst = nullptr;
+    size_t cap_k = 0, cap_R = 0, cap_kabs = 0;
+  } slots[2];
 
   // timing
   struct EvPair {
