@@ -361,72 +361,38 @@ __device__ __forceinline__ void sd_perm_load(SdPerm &pm, const uint32_t *__restr
   pm.hout = pout[pm.pout_h];
 }
 
-// One source row c' of step i for subproblem k (the row body shared by both drivers).
-//   v      : Ψ at this thread's eight positions 2(tid + T·q) + {0, 1} of the sphere order of u_old(i+1), i.e.
-//            S_{i+1}[c' - b̃_j(i+1)][pos_{i+1}(j)] (+Inf where that row is below 0); loaded by the caller (the
-//            persistent driver issues these loads one row ahead, so they may still be in flight on entry).
-//   pin    : LDS copy of the sphere order of step i+1 (rank | b̃ << 16 by position), pout: of step i.
-//   h      : the driver's pipeline hooks (no-ops for one launch per step): h.early() once every wave has consumed `v`
-//            (publish `loaded`, issue the polls); h.go() after the first barrier (check the polls, issue the next row's
-//            loads, the next step's sphere order and df / u_old); h.late_drain() before the barrier after the winners
-//            (this wave's stores of the previous row have landed), h.publish() after it (the previous row is done).  A
-//            timed-out wait sets sh.stop, which the driver reads after the row.
-//   smask, srank, xs: (sd_strad) the pairs q whose second element straddles a sphere seam (bit 3q+2 of smask: not
-//            this lane's to store), and this lane's straddle element (rank srank, value xs; srank < 0: none)
-// Returns 1 if the row is all +Inf (no target in the trust region or no finite source), else 0.
-// Writes row c' of S_i (sphere order of u_old(i)) and of UU_i: exactly five 16-byte vector-memory stores per
-// thread on every path, the last vector-memory instructions of the row (the persistent driver's counted wait
-// for the next row's loads relies on it).  Every barrier is LDS-only (sd_bar): nothing here waits for the
-// caller's outstanding loads or stores.
-template <int M, bool PERSIST, class Hooks>
-__device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int k, int cp,
-                                         int i, double (&v)[8], const uint2 (&ein_in)[4], const uint32_t *pin,
-                                         const uint32_t *pout,
-                                         double *Sout, uint16_t *UU, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
-                                         unsigned char *sds, Hooks &h, const double *__restrict__ df_all,
-                                         const double *__restrict__ uo_all, int par, unsigned smask = 0,
-                                         int srank = -1, double xs = 0.0) {
-  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
-  double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
-  double *dtv = psi + L;                                // [L] transform values (swizzled)
-  uint16_t *uu = reinterpret_cast<uint16_t *>(dtv + L);  // [L] the U row (natural order)
-  // [L] the outputs (natural order): a buffer of their own, so that the winners of one wave need not wait for every
-  // other wave's last pass
-  double *outv = reinterpret_cast<double *>(sds + sd_out_offset<M>());
-  uint16_t *list = uu + L;                              // [SD_LCAP] targets for the exact scan
+// The first phase of row c' of step i: its loaded Ψ (v: this thread's eight positions, + the straddle element srank / xs)
+// into the LDS by rank (psi, for the winners and exact scans) and raw into the transform buffer (stamped by pass 0); the
+// wave's min and max of Ψ and its counts (targets in the trust region, low 16 bits; finite sources, high 16 bits) into
+// sh.rmn / rmx / rnv[w].  Returns this lane's trust-region targets (bit x: target tid | x << 3(M-1) has c' + b̃ <= B).
+// The persistent driver runs it for the NEXT row at the end of a row (the next row's loads have landed by then: the
+// row's late drain waited for them), where the row's stores leave the SIMDs idle; the row body then starts at the
+// barrier that publishes these statistics.
+template <int M, bool PERSIST>
+__device__ __forceinline__ unsigned sdt_stats(const ProblemDev &P, const PyrGeom &G, int k, int cp, int i,
+                                              const double (&v)[8], const uint2 (&ein)[4],
+                                              SdtShared<(1 << (3 * M - 3)) / 64> &sh, unsigned char *sds,
+                                              const double *__restrict__ df_all, const double *__restrict__ uo_all,
+                                              int srank = -1, double xs = 0.0) {
+  constexpr int L = 1 << (3 * M);
+  double *psi = reinterpret_cast<double *>(sds);  // [L] Ψ_j by rank
+  double *dtv = psi + L;                          // [L] transform values (swizzled)
   const int tid = sd_tid(), lane = tid & 63, w = tid >> 6;
   const int B = P.B;
-  const double beta = Lv.beta;
-  // df / u_old of this step: the persistent driver has copied them into this wave's LDS words (LDS-DMA issued one
-  // row ahead: a global load here would cost a memory round trip per row); the per-step driver reads them directly
-  const double *dfi = PERSIST ? reinterpret_cast<const double *>(sds + sd_dfuo_offset<M>()) + (2 * M + 2) * (threadIdx.x >> 6)
-                              : df_all + ((size_t)k * P.nt + i) * M;
-  const double *uoi = PERSIST ? dfi + M : uo_all + ((size_t)k * P.nt + i) * M;
-  SD_RSTAMP(13);
-  SD_STAMP(0);
-  // this thread's sphere-order entries (rank | b̃ << 16 at its eight positions of step i+1): read by the caller (the
-  // persistent driver kept them from issuing this row's loads, so no LDS round trip starts the row)
-  uint2 ein[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) ein[q] = ein_in[q];
-  // ---- this thread's targets: ranks tid | x << 3(M-1) (the lines of the last pass) -----------------
-  double a[M];
+  const double *uoi = PERSIST ? reinterpret_cast<const double *>(sds + sd_dfuo_offset<M>()) +
+                                    (2 * M + 2) * (threadIdx.x >> 6) + M
+                              : uo_all + ((size_t)k * P.nt + i) * M;
+  (void)df_all;
   int lb[M], uo[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-    a[m] = P.dt * dfi[m];
     lb[m] = G.base[m];
     // u_old(:, i) is the same for every lane: as a scalar, the trust-region thresholds below are scalar arithmetic
     uo[m] = __builtin_amdgcn_readfirstlane((int)uoi[m]);
   }
-  double pre = 0.0;
   int bpre = 0;
 #pragma unroll
-  for (int m = 0; m < M - 1; ++m) {
-    const int nu = lb[m] + ((tid >> (3 * m)) & 7);
-    pre = pre + a[m] * (double)nu;  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
-    bpre += abs(nu - uo[m]);
-  }
+  for (int m = 0; m < M - 1; ++m) bpre += abs(lb[m] + ((tid >> (3 * m)) & 7) - uo[m]);
   unsigned valid = 0;  // target inside the trust region: c' + b̃_l(i) <= B
   // targets in the trust region (low 16 bits) + finite sources (high 16 bits) of the wave: ballots counted on the
   // scalar unit
@@ -436,6 +402,103 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     const bool in = bpre <= B - cp - abs(lb[M - 1] + x - uo[M - 1]);  // right side wave-uniform
     valid |= (unsigned)in << x;
     nv += __popcll(__ballot(in));
+  }
+  double pmn = INFINITY, pmx = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const double x = v[2 * q + hh];  // (sd_strad: +Inf for a straddling second element, written by its loader)
+      // written anyway: the straddle lane is in this wave and writes after it (in-wave LDS order)
+      const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
+      psi[j] = x;
+      dtv[sd_swz(j)] = x;  // raw, stamped by pass 0
+      const bool fin = x < INFINITY;
+      nv += __popcll(__ballot(fin)) << 16;
+      pmn = sd_min(pmn, x);  // +Inf is neutral
+      pmx = sd_max(pmx, __hiloint2double(fin ? __double2hiint(x) : (int)0xFFF00000, __double2loint(x)));  // +Inf -> -Inf
+    }
+  if constexpr (sd_strad<M>()) {  // this lane's straddle element
+    const double x = (srank & 0x10000) ? INFINITY : xs;
+    const bool fin = srank >= 0 && x < INFINITY;
+    nv += __popcll(__ballot(fin)) << 16;
+    if (srank >= 0) {
+      psi[srank & 0xFFFF] = x;
+      dtv[sd_swz(srank & 0xFFFF)] = x;
+    }
+    pmn = sd_min(pmn, fin ? x : INFINITY);
+    pmx = sd_max(pmx, fin ? x : -INFINITY);
+  }
+  sd_wave_stats(pmn, pmx);
+  if (lane == 0) {
+    sh.rmn[w] = pmn;
+    sh.rmx[w] = pmx;
+    sh.rnv[w] = nv;
+  }
+  return valid;
+}
+
+// One source row c' of step i for subproblem k (the row body shared by both drivers), after its statistics phase
+// (sdt_stats: Ψ in the LDS, each wave's statistics in sh):
+//   valid  : sdt_stats' result for this row (this lane's targets inside the trust region).
+//   ein_in : this thread's sphere-order entries of step i+1 at its eight positions (rank | b̃ << 16).
+//   pin    : LDS copy of the sphere order of step i+1 (rank | b̃ << 16 by position), pout: of step i.
+//   h      : the driver's pipeline hooks (no-ops for one launch per step): h.early() once every wave has consumed its Ψ
+//            (publish `loaded`, issue the polls); h.go() after the first barrier (check the polls, issue the next row's
+//            loads, the next step's sphere order and df / u_old); h.late_drain() before the barrier after the winners
+//            (this wave's stores of the previous row have landed), h.publish() after it (the previous row is done).  A
+//            timed-out wait sets sh.stop, which the driver reads after the row; h.tail(empty, outv) once the row's
+//            outputs are final, before its stores (the persistent driver runs the next row's sdt_stats there).
+//   smask, srank: (sd_strad) the pairs q whose second element straddles a sphere seam (bit 3q+2 of smask: not
+//            this lane's to store), and the rank of this lane's straddle element (srank < 0: none)
+// Returns 1 if the row is all +Inf (no target in the trust region or no finite source), else 0.
+// Writes row c' of S_i (sphere order of u_old(i)) and of UU_i: exactly five 16-byte vector-memory stores per
+// thread on every path, the last vector-memory instructions of the row (the persistent driver's counted wait
+// for the next row's loads relies on it).  Every barrier is LDS-only (sd_bar): nothing here waits for the
+// caller's outstanding loads or stores.
+template <int M, bool PERSIST, class Hooks>
+__device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv, const PyrGeom &G, int k, int cp,
+                                         int i, unsigned valid, const uint2 (&ein_in)[4], const uint32_t *pin,
+                                         const uint32_t *pout,
+                                         double *Sout, uint16_t *UU, SdtShared<(1 << (3 * M - 3)) / 64> &sh,
+                                         unsigned char *sds, Hooks &h, const double *__restrict__ df_all,
+                                         const double *__restrict__ uo_all, int par, unsigned smask = 0,
+                                         int srank = -1) {
+  constexpr int L = 1 << (3 * M), T = L / 8, NW = T / 64, Smax = 7 * M;
+  double *psi = reinterpret_cast<double *>(sds);        // [L] Ψ_j by rank
+  double *dtv = psi + L;                                // [L] transform values (swizzled)
+  uint16_t *uu = reinterpret_cast<uint16_t *>(dtv + L);  // [L] the U row (natural order)
+  // [L] the outputs (natural order): a buffer of their own, so that the winners of one wave need not wait for every
+  // other wave's last pass
+  double *outv = reinterpret_cast<double *>(sds + sd_out_offset<M>());
+  uint16_t *list = uu + L;                              // [SD_LCAP] targets for the exact scan
+  const int tid = sd_tid(), lane = tid & 63;
+  const double beta = Lv.beta;
+  // df / u_old of this step: the persistent driver has copied them into this wave's LDS words (LDS-DMA issued one
+  // row ahead: a global load here would cost a memory round trip per row); the per-step driver reads them directly
+  const double *dfi = PERSIST ? reinterpret_cast<const double *>(sds + sd_dfuo_offset<M>()) + (2 * M + 2) * (threadIdx.x >> 6)
+                              : df_all + ((size_t)k * P.nt + i) * M;
+  (void)uo_all;
+  SD_RSTAMP(13);
+  SD_STAMP(0);
+  // this thread's sphere-order entries (rank | b̃ << 16 at its eight positions of step i+1): read by the caller (the
+  // persistent driver kept them from issuing this row's loads, so no LDS round trip starts the row)
+  uint2 ein[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ein[q] = ein_in[q];
+  // ---- this thread's targets: ranks tid | x << 3(M-1) (the lines of the last pass) -----------------
+  double a[M];
+  int lb[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    a[m] = P.dt * dfi[m];
+    lb[m] = G.base[m];
+  }
+  double pre = 0.0;
+#pragma unroll
+  for (int m = 0; m < M - 1; ++m) {
+    const int nu = lb[m] + ((tid >> (3 * m)) & 7);
+    pre = pre + a[m] * (double)nu;  // ((0 + (Δt·df_1)·ν_1) + ...), HelpFunctions.jl:52-57
   }
 
   // ---- the binade: values base + (Ψ - ref)/β + d lie in [base, 2·base), grid g = 2^18 ulp ----------------
@@ -565,42 +628,11 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
         }
     }
   };
-  int nf;
+  int nf, nv;
   bool empty;
   {
-    double pmn = INFINITY, pmx = -INFINITY;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const double x = v[2 * q + hh];  // (sd_strad: +Inf for a straddling second element, written by its loader)
-        // written anyway: the straddle lane is in this wave and writes after it (in-wave LDS order)
-        const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
-        psi[j] = x;
-        dtv[sd_swz(j)] = x;  // raw, stamped by pass 0
-        const bool fin = x < INFINITY;
-        nv += __popcll(__ballot(fin)) << 16;
-        pmn = sd_min(pmn, x);  // +Inf is neutral
-        pmx = sd_max(pmx, __hiloint2double(fin ? __double2hiint(x) : (int)0xFFF00000, __double2loint(x)));  // +Inf -> -Inf
-      }
-    if constexpr (sd_strad<M>()) {  // this lane's straddle element
-      const double x = (srank & 0x10000) ? INFINITY : xs;
-      const bool fin = srank >= 0 && x < INFINITY;
-      nv += __popcll(__ballot(fin)) << 16;
-      if (srank >= 0) {
-        psi[srank & 0xFFFF] = x;
-        dtv[sd_swz(srank & 0xFFFF)] = x;
-      }
-      pmn = sd_min(pmn, fin ? x : INFINITY);
-      pmx = sd_max(pmx, fin ? x : -INFINITY);
-    }
-    sd_wave_stats(pmn, pmx);
-    if (lane == 0) {
-      sh.rmn[w] = pmn;
-      sh.rmx[w] = pmx;
-      sh.rnv[w] = nv;
-    }
-    sd_bar();  // every wave has consumed its loads of S_{i+1} (their values are in LDS)
+    double pmn, pmx;
+    sd_bar();  // every wave's row statistics (sdt_stats) are in sh, its Ψ in the LDS: the loads of S_{i+1} are consumed
     if (tid == 0) sh.nlist[par ^ 1] = sh.redo[par ^ 1] = 0;  // the next row's slots
     h.early();
     {
@@ -643,19 +675,23 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   if (sparse) {
     if (tid == 0) sh.nsp = 0;
     sd_bar();
+    // this lane's finite sources, from Ψ by rank (a straddling second element is its straddle lane's to add)
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-        if (v[2 * q + hh] < INFINITY) {
+      for (int hh = 0; hh < 2; ++hh) {
+        const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
+        const double x = psi[j];
+        if (x < INFINITY && !(hh && (smask >> (3 * q + 2) & 1))) {
           const int e = atomicAdd(&sh.nsp, 1);
-          sh.spj[e] = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
-          sh.spv[e] = v[2 * q + hh];
+          sh.spj[e] = j;
+          sh.spv[e] = x;
         }
-    if (sd_strad<M>() && srank >= 0 && !(srank & 0x10000) && xs < INFINITY) {
+      }
+    if (sd_strad<M>() && srank >= 0 && !(srank & 0x10000) && psi[srank & 0xFFFF] < INFINITY) {
       const int e = atomicAdd(&sh.nsp, 1);
       sh.spj[e] = srank & 0xFFFF;
-      sh.spv[e] = xs;
+      sh.spv[e] = psi[srank & 0xFFFF];
     }
     sd_bar();
 #pragma unroll
@@ -741,6 +777,8 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     h.publish();
   }
   SD_STAMP(8);
+  // the persistent driver's next row: its statistics phase (LDS writes and VALU only), with this row's outputs final
+  h.tail(empty, outv);
   // ---- Φ_i row c' in the sphere order of u_old(i), and the U row, both 16 bytes per lane ------------
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -960,6 +998,7 @@ struct SdHooksNone {
   __device__ __forceinline__ void go() {}
   __device__ __forceinline__ void late_drain() {}
   __device__ __forceinline__ void publish() {}
+  __device__ __forceinline__ void tail(bool, const double *) {}
 };
 
 // LDS bytes of the row body: Ψ by rank, the transform / output values, the U row, the scan list, and two
@@ -1074,7 +1113,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3)) void k_sdt_step(ProblemDev P, Lev
     uint2 ein[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) ein[q] = *reinterpret_cast<const uint2 *>(slot + sd_p2<M>(tid, q));
-    sdt_body<M, false>(P, Lv, G, k, cp, i, v, ein, slot, slot + L, Sout_all + (size_t)k * s_stride + (size_t)cp * L,
+    const unsigned valid = sdt_stats<M, false>(P, G, k, cp, i, v, ein, sh, sds, P.df, P.uold);
+    sdt_body<M, false>(P, Lv, G, k, cp, i, valid, ein, slot, slot + L, Sout_all + (size_t)k * s_stride + (size_t)cp * L,
                        UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)(P.B + 1) * L) + (size_t)cp * L, sh,
                        sds, hooks, P.df, P.uold, 0);
     if (tid == 0) {
@@ -1339,6 +1379,11 @@ struct SdPipe {
   int need, val;
   SdRaw raw;
   SdNext nx;  // the next row's sphere-order entries and seam (sd_read_next)
+  // the next row's statistics phase, run at the end of this row (tail): its result for the next sdt_body
+  const ProblemDev *Pp;
+  const PyrGeom *Gp;
+  unsigned valid_next;
+  int whole;  // one row per workgroup (hi - lo == 1)
 
   // every wave polls its own dependency flags (lanes 0-31 RAW for the next row, 32-63 WAR for this row's stores; a
   // lane without one polls a flag that always passes -- every lane loads, no branch), once every wave has consumed
@@ -1422,6 +1467,18 @@ struct SdPipe {
     pcp = cp;
     pi = i;
   }
+  // the next row's statistics phase (its loads landed at this row's late drain): after this row's outputs are final,
+  // before its stores.  A one-row workgroup's next row reads its own row of this step, whose stores are not issued yet:
+  // the sphere-0 source at distance 0 (u_old(i) on the level grid: position 0 with b̃ = 0, lane 0 of wave 0) is this
+  // row's output, from the LDS (an off-grid u_old has b̃ >= 1 everywhere and no such source).
+  __device__ __forceinline__ void tail(bool empty, const double *outv) {
+    if (!has_next) return;
+    double v[8];
+    sd_take<M>(v, raw);
+    if (whole && (threadIdx.x & 63) == 0 && (raw.e[0].x >> 16) == 0) v[0] = empty ? INFINITY : outv[raw.e[0].x & 0xFFFFu];
+    const double xs = __hiloint2double((int)raw.sv.y, (int)raw.sv.x);
+    valid_next = sdt_stats<M, true>(*Pp, *Gp, k, ncp, ni, v, raw.e, *sh, sds, dfa, uoa, raw.srank, xs);
+  }
 };
 
 template <int M>
@@ -1445,8 +1502,6 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   const int base = B / W, extra = B - base * W;  // rows 1..B, the longer chunks highest
   const int lo = 1 + wl * base + max(0, wl - (W - extra)), hi = lo + base + (wl >= W - extra ? 1 : 0);
   uint32_t *slot = reinterpret_cast<uint32_t *>(sds + sd_slot_offset<M>());
-  // the row body's outputs (natural order) after a row
-  double *dtv = reinterpret_cast<double *>(sds + sd_out_offset<M>());
   auto pslot = [&](int step) { return slot + (step & 1) * L; };  // sphere order of `step`
   // this subproblem's region: NB staging buffers of R rows, then row 0 of every step (k_sdt_row0); one buffer
   // resource over all of it (the host checks it is below 4 GiB)
@@ -1484,7 +1539,13 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   // a wait the compiler sees (vmcnt(0), other counters untouched): entering the loop with these loads pending would
   // make it assume, at the loop head, that nothing younger can be outstanding, and wait for every store there
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  int status = 0;  // the previous row's sdt_body result: 1 = its outputs are all +Inf
+  h.Pp = &P, h.Gp = &G, h.whole = hi - lo == 1;
+  {  // the first row's statistics phase (later rows': the previous row's tail)
+    double v[8];
+    sd_take<M>(v, h.raw);
+    const double xs = __hiloint2double((int)h.raw.sv.y, (int)h.raw.sv.x);
+    h.valid_next = sdt_stats<M, true>(P, G, k, lo, nt - 2, v, h.raw.e, sh, sds, df_all, uo_all, h.raw.srank, xs);
+  }
   int par = 0;     // the row's parity (sdt_body's LDS slots)
   bool stop = false;
 #pragma nounroll
@@ -1498,25 +1559,18 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       const int g = cp == lo ? h.g0 : 1 << 30;  // timeline stamps: the chunk's first row
       (void)g;
       SD_TL(0);
-      // this row's loads, sphere order and df / u_old (everything but the previous row's five stores) have landed;
-      // the memory clobber keeps the LDS reads of what the DMA wrote below this point
+      // this row's loads, sphere order and df / u_old (everything but the previous row's five stores) have landed (at
+      // the previous row's late drain already: its tail ran this row's statistics phase); the memory clobber keeps the
+      // LDS reads of what the DMA wrote below this point
       asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      double v[8];
-      sd_take<M>(v, h.raw);
       SD_TL(7);
-      // one row per workgroup: a sphere-0 source at distance 0 (u_old(i+1) on the level grid: position 0 with b̃ = 0)
-      // is this workgroup's own output of the previous row, still in LDS (the loaded copy predates it); an off-grid
-      // u_old(i+1) has b̃ >= 1 everywhere and no such source (position 0 is lane 0 of wave 0)
-      if (hi - lo == 1 && h.pcp >= 0 && (tid & 63) == 0 && (h.raw.e[0].x >> 16) == 0)
-        v[0] = status == 1 ? INFINITY : dtv[h.raw.e[0].x & 0xFFFFu];
       uint2 ein[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) ein[q] = h.raw.e[q];
-      const double xs = __hiloint2double((int)h.raw.sv.y, (int)h.raw.sv.x);
-      status = sdt_body<M, true>(P, Lv, G, k, cp, i, v, ein, pslot(i + 1), pslot(i),
-                                 reg + (size_t)(i % NB) * R * L + (size_t)cp * L,
-                                 UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L, sh,
-                                 sds, h, df_all, uo_all, par, h.raw.mask, h.raw.srank, xs);
+      sdt_body<M, true>(P, Lv, G, k, cp, i, h.valid_next, ein, pslot(i + 1), pslot(i),
+                        reg + (size_t)(i % NB) * R * L + (size_t)cp * L,
+                        UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L, sh, sds, h,
+                        df_all, uo_all, par, h.raw.mask, h.raw.srank);
       par ^= 1;
       SD_TL(6);
       stop = sh.stop != 0;  // written before a barrier the row has passed since (every path has one)
