@@ -675,14 +675,15 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
   if (sparse) {
     if (tid == 0) sh.nsp = 0;
     sd_bar();
-    // this lane's finite sources, from Ψ by rank (a straddling second element is its straddle lane's to add)
+    // this lane's finite sources, from Ψ by rank (sd_strad: a straddling second element is its straddle lane's to add;
+    // otherwise this lane loaded it itself)
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int j = (int)((hh ? ein[q].y : ein[q].x) & 0xFFFFu);
         const double x = psi[j];
-        if (x < INFINITY && !(hh && (smask >> (3 * q + 2) & 1))) {
+        if (x < INFINITY && !(sd_strad<M>() && hh && (smask >> (3 * q + 2) & 1))) {
           const int e = atomicAdd(&sh.nsp, 1);
           sh.spj[e] = j;
           sh.spv[e] = x;
