@@ -446,9 +446,13 @@ int run_bellman(mioc_ctx *ctx) {
         // segments with at most one workgroup per CU to go round: reserve more than half a CU's LDS, so that the
         // dispatcher cannot put two segments on one CU while another CU idles (the segments run as one pipeline,
         // and a shared CU slows all of them: the 128-restart shard ran 17 - 28 ms from run to run)
-        int ncu = 0;
+        int ncu = 0, cu_lds = 0, wg_lds = 0;
         HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-        if ((size_t)K * (size_t)S <= (size_t)ncu) plan.lds = std::max<size_t>(plan.lds, 82 * 1024);
+        HIP_TRY(ctx, hipDeviceGetAttribute(&cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, ctx->device));
+        HIP_TRY(ctx, hipDeviceGetAttribute(&wg_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device));
+        // half a CU's LDS plus one 2 KiB allocation granule (gfx950: 82 KiB of 160), capped at a workgroup's maximum
+        const size_t half = std::min<size_t>((size_t)cu_lds / 2 + 2048, (size_t)wg_lds);
+        if ((size_t)K * (size_t)S <= (size_t)ncu) plan.lds = std::max<size_t>(plan.lds, half);
       }
       if (v2) ctx->occupancy = fsep2_blocks_per_cu(ctx->pyr, plan);
       if (v2 && S > 1) {

@@ -118,3 +118,16 @@ def test_ws_batch_vs_oracle(oracle_c):
         assert st[k] == 0
         assert np.array_equal(ub[k].T, ou) and pb[k] == ops, f"k={k}"
     ctx.close()
+
+
+@pytest.mark.parametrize("nt", [65, 129])
+def test_ws_full_first_chunk_vs_oracle(oracle_c, nt):
+    """nt = 65 and 129 (65 * k: the first, top chunk is full -- (nt - 2) % 64 == 63 -- so the counted-wait path with
+    no previous chunk (mid() with prev_lo = -1, then vmcnt(56)) runs from the first chunk on), C2's shape (13
+    segments), Gaussian gradients, against the oracle at three budgets."""
+    cfg = CONFIGS["C2"]
+    lt, df, uo = make_inputs(cfg, nt=nt, k=11)
+    lv = Levels(lt.nu, [tuple(int(x) for x in t) for t in lt.tuples])
+    name, diag = _check(oracle_c, lv, lt, df, uo, cfg.B, cfg.beta, cfg.dt, (cfg.B, cfg.B // 3, 5))
+    assert name == "k_pinf_recur_ws", name
+    assert diag[6] == 0, diag
