@@ -778,19 +778,25 @@ __device__ __forceinline__ int sdt_body(const ProblemDev &P, const LevelsDev &Lv
     h.publish();
   }
   SD_STAMP(8);
-  // the persistent driver's next row: its statistics phase (LDS writes and VALU only), with this row's outputs final
-  h.tail(empty, outv);
-  // ---- Φ_i row c' in the sphere order of u_old(i), and the U row, both 16 bytes per lane ------------
+  // ---- Φ_i row c' in the sphere order of u_old(i), and the U row, both 16 bytes per lane: gathered from the LDS
+  // before the tail, so that the two dependent LDS round trips (order entries, then values) run under its VALU work
+  uint2 eo[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) eo[q] = *reinterpret_cast<const uint2 *>(pout + sd_p2<M>(tid, q));
+  double go[8];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint2 e = *reinterpret_cast<const uint2 *>(pout + sd_p2<M>(tid, q));
-    sd_store16<PERSIST>(Sout, L * 8, sd_p2<M>(tid, q), __double_as_longlong(outv[e.x & 0xFFFFu]),
-                        __double_as_longlong(outv[e.y & 0xFFFFu]));
+    go[2 * q] = outv[eo[q].x & 0xFFFFu];
+    go[2 * q + 1] = outv[eo[q].y & 0xFFFFu];
   }
-  {
-    const ulonglong2 t = reinterpret_cast<const ulonglong2 *>(uu)[tid];
-    *reinterpret_cast<ulonglong2 *>(UU + 8 * tid) = t;  // read by later launches only (backtrack)
-  }
+  const ulonglong2 ut = reinterpret_cast<const ulonglong2 *>(uu)[tid];
+  // the persistent driver's next row: its statistics phase (LDS writes and VALU only), with this row's outputs final
+  h.tail(empty, outv);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    sd_store16<PERSIST>(Sout, L * 8, sd_p2<M>(tid, q), __double_as_longlong(go[2 * q]),
+                        __double_as_longlong(go[2 * q + 1]));
+  *reinterpret_cast<ulonglong2 *>(UU + 8 * tid) = ut;  // read by later launches only (backtrack)
   SD_STAMP(9);
   SD_RSTAMP(14);
   return empty ? 1 : 0;
@@ -1459,6 +1465,9 @@ struct SdPipe {
   // late in the row, before the barrier after the winners: this wave's stores of the previous row have landed (they
   // have had the whole row: no wait), so after that barrier the previous row can be published
   __device__ __forceinline__ void late_drain() {
+#ifdef SD_TL_DRAIN  // timeline builds: stamp 7 = the drain's start (instead of "loads taken" at the row start)
+    SD_TL_AT(g0, i, nt, 7);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     SD_TL_AT(g0, i, nt, 5);
   }
@@ -1564,7 +1573,9 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       // the previous row's late drain already: its tail ran this row's statistics phase); the memory clobber keeps the
       // LDS reads of what the DMA wrote below this point
       asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+#ifndef SD_TL_DRAIN
       SD_TL(7);
+#endif
       uint2 ein[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) ein[q] = h.raw.e[q];

@@ -66,6 +66,10 @@ for q, nm in enumerate(names):
 per = (T[:, 1:, 0] - T[:, :-1, 0])
 print(f"step period per row: median {np.median(per):.3f}  p10 {np.percentile(per, 10):.3f}  p90 "
       f"{np.percentile(per, 90):.3f} us")
+if os.environ.get("TL_DRAIN"):  # a -DSD_TL_DRAIN build: stamp 7 is the late drain's start
+    for nm, a, b in (("  passes + winners (4->7)", 4, 7), ("  late drain wait (7->5)", 7, 5)):
+        d = (T[:, :, b] - T[:, :, a])[ok]
+        print(f"{nm:36s} median {np.median(d):6.3f}  p10 {np.percentile(d, 10):6.3f}  p90 {np.percentile(d, 90):6.3f} us")
 d = (T[:, :, 7] - T[:, :, 0])[ok]
 print(f"{'  of it: waiting for the loads (0->7)':36s} median {np.median(d):6.3f}  p10 {np.percentile(d, 10):6.3f}  p90 {np.percentile(d, 90):6.3f} us")
 rest = (T[:, 1:, 0] - T[:, :-1, 6])
