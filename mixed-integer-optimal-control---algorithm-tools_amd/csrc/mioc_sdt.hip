@@ -1391,6 +1391,8 @@ struct SdPipe {
   const PyrGeom *Gp;
   unsigned valid_next;
   int whole;  // one row per workgroup (hi - lo == 1)
+  unsigned nbo;     // byte offset of the next row's input buffer, (ni + 1) % NB (kept by the driver: no division)
+  bool stop_seen;   // sh.stop as read after the row's barrier 3 (publish)
 
   // every wave polls its own dependency flags (lanes 0-31 RAW for the next row, 32-63 WAR for this row's stores; a
   // lane without one polls a flag that always passes -- every lane loads, no branch), once every wave has consumed
@@ -1452,7 +1454,7 @@ struct SdPipe {
       const int same = *(const volatile __attribute__((address_space(3))) int32_t *)(
           sds + sd_dfuo_offset<M>() + (threadIdx.x >> 6) * sd_dfuo_stride<M>() + 16 * M);
       sd_read_next<M>(nx, slot + ((ni + 1) & 1) * L, sslot + ((ni + 1) & 1) * 8 * SD_STRAD_N);
-      sd_issue_pipe<M>(raw, rs, nx, ncp, (unsigned)((ni + 1) % NB) * bufb, r0b + (unsigned)(ni + 1) * rowb, rowb);
+      sd_issue_pipe<M>(raw, rs, nx, ncp, nbo, r0b + (unsigned)(ni + 1) * rowb, rowb);
       if (ni != i && !same) {
         sd_perm_dma_asm<M>(pk + (size_t)ni * L, slot + (ni & 1) * L);
         if constexpr (sd_strad<M>()) sd_strad_dma(sk + (size_t)ni * 8 * SD_STRAD_N, sslot + (ni & 1) * 8 * SD_STRAD_N);
@@ -1474,6 +1476,9 @@ struct SdPipe {
   __device__ __forceinline__ void publish() {
     if (threadIdx.x == 0 && pcp >= 0)
       __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a timed-out wait of this row (go(), before this barrier) set sh.stop: read here, where every wave reads the same
+    // value, so that the driver's exit test after the row needs no LDS round trip of its own
+    stop_seen = sh->stop != 0;
     pcp = cp;
     pi = i;
   }
@@ -1558,6 +1563,8 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   }
   int par = 0;     // the row's parity (sdt_body's LDS slots)
   bool stop = false;
+  // the staging buffers of steps i and i + 1 (i % NB, (i + 1) % NB), stepped down with i instead of divided per row
+  int bi = (nt - 2) % NB, bi1 = (nt - 1) % NB;
 #pragma nounroll
   for (int i = nt - 2; i >= 0 && !stop; --i) {
 #pragma nounroll
@@ -1566,6 +1573,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
       h.cp = cp, h.i = i;
       h.ncp = last_row ? lo : cp + 1, h.ni = last_row ? i - 1 : i;  // the next row
       h.has_next = h.ni >= 0;
+      h.nbo = (unsigned)(last_row ? bi : bi1) * h.bufb;  // buffer (ni + 1) % NB
       const int g = cp == lo ? h.g0 : 1 << 30;  // timeline stamps: the chunk's first row
       (void)g;
       SD_TL(0);
@@ -1580,13 +1588,15 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
 #pragma unroll
       for (int q = 0; q < 4; ++q) ein[q] = h.raw.e[q];
       sdt_body<M, true>(P, Lv, G, k, cp, i, h.valid_next, ein, pslot(i + 1), pslot(i),
-                        reg + (size_t)(i % NB) * R * L + (size_t)cp * L,
+                        reg + (size_t)bi * R * L + (size_t)cp * L,
                         UU_all + (size_t)k * uu_stride_k + (size_t)i * ((size_t)R * L) + (size_t)cp * L, sh, sds, h,
                         df_all, uo_all, par, h.raw.mask, h.raw.srank);
       par ^= 1;
       SD_TL(6);
-      stop = sh.stop != 0;  // written before a barrier the row has passed since (every path has one)
+      stop = h.stop_seen;  // read after the row's barrier 3 (every path has one)
     }
+    bi1 = bi;
+    bi = bi == 0 ? NB - 1 : bi - 1;
   }
   if (tid == 0) {
     if (sh.cnt[0]) atomicAdd(&counters[0], sh.cnt[0]);
