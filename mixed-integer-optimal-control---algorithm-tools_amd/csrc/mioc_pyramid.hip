@@ -820,11 +820,15 @@ __global__ __launch_bounds__(PY_T) void k_pyr_step(ProblemDev P, LevelsDev Lv, P
 // row c' - s of S_i (the sphere s) form one contiguous run per sphere.  Inside a sphere the ranks ascend (a
 // stable counting sort), so the order is a function of u_old(i) alone: steps with equal u_old share one table,
 // which the persistent separable-transform driver uses to skip reloading it.
+constexpr int kOrderMaxL = 4096;
 __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint32_t *perm_all, int32_t *same2,
                                                    uint16_t *strad, int32_t *counters) {
   constexpr int NK = 64;            // bucket keys: min(distance, 63)
   __shared__ int start[NK];         // the next free position of each bucket
   __shared__ int wcnt[4][NK + 1];   // ranks of the current chunk per wave and bucket (NK: the inactive lanes)
+  // the order is built here and stored coalesced at the end: scattered 4-byte stores straight to HBM cost a
+  // read-modify-write of every 128-byte line at the memory side (the launch checks L <= kOrderMaxL)
+  __shared__ uint32_t sperm[kOrderMaxL];
   const int i = blockIdx.x, k = blockIdx.y, L = G.ncol * G.n[0], M = G.M;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const double *uo = P.uold + ((size_t)k * P.nt + i) * M;
@@ -879,7 +883,7 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
     if (act) {
       int pos = start[b] + below;
       for (int q = 0; q < w; ++q) pos += wcnt[q][b];
-      perm[pos] = (uint32_t)j | ((uint32_t)d << 16);
+      sperm[pos] = (uint32_t)j | ((uint32_t)d << 16);
     }
     __syncthreads();
     for (int e = tid; e < NK; e += blockDim.x) {
@@ -888,6 +892,12 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
     }
     if (tid == 0) wcnt[0][NK] = wcnt[1][NK] = wcnt[2][NK] = wcnt[3][NK] = 0;
     __syncthreads();
+  }
+  if ((L & 3) == 0) {  // 16 bytes per lane (perm rows are 16-byte aligned when L is a multiple of 4)
+    for (int e = 4 * tid; e < L; e += 4 * blockDim.x)
+      *reinterpret_cast<uint4 *>(perm + e) = *reinterpret_cast<const uint4 *>(sperm + e);
+  } else {
+    for (int e = tid; e < L; e += blockDim.x) perm[e] = sperm[e];
   }
   // strad (the persistent separable driver at 8^4, 8 waves of 512 positions): per wave, the in-wave offsets of the odd
   // positions whose distance differs from position p-1's -- the second elements of the 16-byte position pairs that
@@ -900,7 +910,7 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
     if (tid < 8) start[tid] = 0;  // per-wave counts
     __syncthreads();
     for (int p = 2 * tid + 1; p < L; p += 2 * blockDim.x)
-      if ((perm[p] >> 16) != (perm[p - 1] >> 16)) {
+      if ((sperm[p] >> 16) != (sperm[p - 1] >> 16)) {
         const int u = (p - 1) >> 1, t = u % T;
         const int wv = t >> 6;
         const int o = 128 * (u / T) + 2 * (t & 63) + 1;
@@ -915,6 +925,7 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
 
 hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm, int32_t *same2,
                             uint16_t *strad, int32_t *counters) {
+  if (G.ncol * G.n[0] > kOrderMaxL) return hipErrorInvalidValue;  // (the pyramid paths need L <= 4096 anyway)
   hipLaunchKernelGGL(k_pyr_order, dim3(P.nt, P.K), dim3(256), 0, s, P, G, perm, same2, strad, counters);
   return hipGetLastError();
 }
