@@ -737,9 +737,9 @@ def main():
             variant["walk_serial_fallbacks"] = max(0, int(r2["diag"][9]))
         if rank == 0 and world == 1 and not args.no_cpu_baseline and args.solver == "native":
             variant["cpu_baseline"] = cpu_baseline(args.config, "inf", args.cpu_steps)
-    def batch_line(cfg_name, total=None, p_over=None):
+    def batch_line(cfg_name, total=None, p_over=None, min_steps=3):
         r3 = run(args, cfg_name, args.batch_size, p_over, None, rank, world, device, dist, torch,
-                 max(args.steps, 3), args.warmup, total=total)
+                 max(args.steps, min_steps), args.warmup, total=total)
         line = {"config": {"workload": workload(r3), "parallelism": f"dp{world} (independent restarts)",
                            "global_batch": r3["G"], "per_rank": r3["K"]},
                 "value": round(r3["G"] * r3["steps"] / r3["elapsed"], 3), "unit": "subproblems/s",
@@ -791,12 +791,14 @@ def main():
         batch_pinf = batch_line(args.pinf_batch_config)
     singles = {}
     if args.single_configs not in ("", "none") and args.nt is None:
-        # one subproblem per GPU per step of the reference's own main() presets (doubletank, vanderpol at p = Inf)
+        # one subproblem per GPU per step of the reference's own main() presets (doubletank, vanderpol at p = Inf); a
+        # stream of 20 subproblems (0.5-1.7 ms each), so that the end of the timed region -- the last backtrack, which
+        # nothing overlaps, and the synchronisation -- weighs as in a stream rather than a third of the total (3 steps)
         for cname in args.single_configs.split(","):
             saved = args.batch_size
             args.batch_size = 1
             try:
-                singles[cname] = batch_line(cname)
+                singles[cname] = batch_line(cname, min_steps=20)
             finally:
                 args.batch_size = saved
     if rank == 0:
