@@ -829,6 +829,7 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
   // the order is built here and stored coalesced at the end: scattered 4-byte stores straight to HBM cost a
   // read-modify-write of every 128-byte line at the memory side (the launch checks L <= kOrderMaxL)
   __shared__ uint32_t sperm[kOrderMaxL];
+  __shared__ uint16_t sdist[kOrderMaxL];  // each rank's distance (computed once)
   const int i = blockIdx.x, k = blockIdx.y, L = G.ncol * G.n[0], M = G.M;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const double *uo = P.uold + ((size_t)k * P.nt + i) * M;
@@ -844,17 +845,29 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
   for (int e = tid; e < NK; e += blockDim.x) start[e] = 0;
   for (int e = tid; e < 4 * (NK + 1); e += blockDim.x) (&wcnt[0][0])[e] = 0;
   __syncthreads();
+  // every dimension of 8 levels (the 8^M grids of the separable paths): coordinates by shifts, not divisions
+  bool oct = true;
+  for (int m = 0; m < M; ++m) oct = oct && G.n[m] == 8;
   auto dist = [&](int j) {
     int d = 0;
-    for (int m = 0; m < M; ++m) {
-      const int x = j % G.n[m];
-      j /= G.n[m];
-      d += abs(G.base[m] + x - u[m]);
+    if (oct) {
+      for (int m = 0; m < M; ++m) d += abs(G.base[m] + ((j >> (3 * m)) & 7) - u[m]);
+    } else {
+      for (int m = 0; m < M; ++m) {
+        const int x = j % G.n[m];
+        j /= G.n[m];
+        d += abs(G.base[m] + x - u[m]);
+      }
     }
     return min(d, 0xFFFF);
   };
   auto key = [&](int j, int d) { return min(d, 63); };
-  for (int j = tid; j < L; j += blockDim.x) atomicAdd(&start[key(j, dist(j))], 1);
+  // each rank's distance, computed once (the placement below reads it back)
+  for (int j = tid; j < L; j += blockDim.x) {
+    const int d = dist(j);
+    sdist[j] = (uint16_t)d;
+    atomicAdd(&start[key(j, d)], 1);
+  }
   __syncthreads();
   if (tid == 0) {
     int run = 0;
@@ -870,7 +883,7 @@ __global__ __launch_bounds__(256) void k_pyr_order(ProblemDev P, PyrGeom G, uint
   for (int c = 0; c < L; c += 256) {
     const int j = c + tid;
     const bool act = j < L;
-    const int d = act ? dist(j) : 0, b = act ? key(j, d) : NK;
+    const int d = act ? (int)sdist[j] : 0, b = act ? key(j, d) : NK;
     unsigned long long same = ~0ull;
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
