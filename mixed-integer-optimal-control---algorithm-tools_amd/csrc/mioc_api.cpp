@@ -267,7 +267,7 @@ int run_bellman(mioc_ctx *ctx) {
   HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(int32_t), ctx->stream));
   bool pinf_flags_zeroed = false;
   if (ctx->p_kind == MIOC_P_INF && !ctx->force_steps) {
-    const size_t fbytes = ((size_t)ctx->K * pinf_recur_segments(P) + 1) * sizeof(int32_t);
+    const size_t fbytes = ((size_t)ctx->K * pinf_recur_segments(P) * PINF_WS_FLAG_STRIDE + 1) * sizeof(int32_t);
     int rcf = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, fbytes, "p=Inf segment flags");
     if (rcf) return rcf;
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, fbytes, ctx->stream));
@@ -360,7 +360,7 @@ int run_bellman(mioc_ctx *ctx) {
     if (persist && kstride * sizeof(double) >= (1ull << 32)) persist = false;  // (then also kstride = s_stride)
     const size_t ks = persist ? kstride : s_stride;
     // flags: done and loaded per row, then the error word
-    const size_t nflag = 2 * K * (size_t)(ctx->B + 1);
+    const size_t nflag = 2 * K * (size_t)(ctx->B + 1) * SDT_FLAG_STRIDE;
     const size_t runflag_bytes = ((nflag + 1) * sizeof(int32_t) + 15) / 16 * 16;
     if (persist) {
       int rcf = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, runflag_bytes, "persistent row flags");
@@ -459,12 +459,12 @@ int run_bellman(mioc_ctx *ctx) {
         const int NB = 8, SM = ctx->pyr.n[0] + ctx->pyr.n[1] - 2;
         (void)SM;
         rc = grow(ctx, &ctx->d_ring, &ctx->ring_cap, K * (size_t)S * NB * (size_t)plan.slot_bytes, "segment rings");
-        if (!rc) rc = grow(ctx, &ctx->d_segflags, &ctx->segflag_cap, (2 * K * (size_t)S + 1) * sizeof(int32_t),
+        if (!rc) rc = grow(ctx, &ctx->d_segflags, &ctx->segflag_cap, (FSEP_FLAG_STRIDE * K * (size_t)S + 1) * sizeof(int32_t),
                            "segment flags");
         if (rc) return rc;
         if (!ctx->h_run_err) HIP_TRY(ctx, hipHostMalloc(&ctx->h_run_err, 16, 0));
         *ctx->h_run_err = 0;
-        HIP_TRY(ctx, hipMemsetAsync(ctx->d_segflags, 0, (2 * K * (size_t)S + 1) * sizeof(int32_t), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_segflags, 0, (FSEP_FLAG_STRIDE * K * (size_t)S + 1) * sizeof(int32_t), ctx->stream));
         ev_begin(ctx, 0, "k_fsep2");
         int ncu = 0;
         HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
@@ -484,7 +484,7 @@ int run_bellman(mioc_ctx *ctx) {
         }
         HIP_TRY(ctx, le);
         ev_end(ctx, 0, 1);
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_segflags + 2 * K * (size_t)S, sizeof(int32_t),
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_segflags + FSEP_FLAG_STRIDE * K * (size_t)S, sizeof(int32_t),
                                     hipMemcpyDeviceToHost, ctx->stream));
         ctx->run_pending = true;
         ctx->have_dp = true;
@@ -541,7 +541,7 @@ int run_bellman(mioc_ctx *ctx) {
     int32_t *pflags = nullptr;
     if (!ctx->force_steps) {
       if (!pinf_flags_zeroed) {
-        const size_t fbytes = ((size_t)K * pinf_recur_segments(P) + 1) * sizeof(int32_t);
+        const size_t fbytes = ((size_t)K * pinf_recur_segments(P) * PINF_WS_FLAG_STRIDE + 1) * sizeof(int32_t);
         rc = grow(ctx, &ctx->d_runflags, &ctx->runflag_cap, fbytes, "p=Inf segment flags");
         if (rc) return rc;
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_runflags, 0, fbytes, ctx->stream));
@@ -561,12 +561,12 @@ int run_bellman(mioc_ctx *ctx) {
         // a wait past the spin limit: the one-workgroup recursion redoes the DP on the device, gated by the error word
         // (no host round trip between the DP and the backtrack); diagnostics [6] reads its count (d_counters[6])
         ProblemDev Pr = P;
-        Pr.redo_gate = ctx->d_runflags + (size_t)K * nseg;
+        Pr.redo_gate = ctx->d_runflags + (size_t)K * nseg * PINF_WS_FLAG_STRIDE;
         Pr.redo_count = ctx->d_counters + 6;
         HIP_TRY(ctx, launch_pinf_recur(ctx->stream, Pr, D, ctx->ncu, nullptr, ctx->spin_limit, nullptr, nullptr));
       } else {
         // under the device TRM control the backtrack kernels are gated already: the host checks and redoes (check_run)
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + (size_t)K * nseg, sizeof(int32_t),
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_run_err, ctx->d_runflags + (size_t)K * nseg * PINF_WS_FLAG_STRIDE, sizeof(int32_t),
                                     hipMemcpyDeviceToHost, ctx->stream));
         ctx->run_pending = true;
       }

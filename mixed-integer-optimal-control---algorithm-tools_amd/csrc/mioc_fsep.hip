@@ -171,8 +171,10 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
   const double beta = Lv.beta, inv = Lv.inv_beta;
   const double numx0 = (double)max(abs(A.base0), abs(A.base0 + N0 - 1)),
                numx1 = (double)max(abs(A.base1), abs(A.base1 + N1 - 1));
-  int32_t *const fl = A.flags + 2 * ((size_t)k * S + q);
-  int32_t *const err = A.flags + 2 * (size_t)P.K * S;
+  // this segment's record {outbox token, consumed token}, FSEP_FLAG_STRIDE words apart from its neighbours'
+  constexpr int FW = FSEP_FLAG_STRIDE;
+  int32_t *const fl = A.flags + FW * ((size_t)k * S + q);
+  int32_t *const err = A.flags + FW * (size_t)P.K * S;
   // rings through buffer resources (32-bit offsets, sc1 accesses); the inbox slot is copied into the LDS staging
   // rows by LDS-DMA (no registers held across the read phase)
   const size_t ring_seg = SEG ? (size_t)NB * A.slot_bytes : 0;
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
   // the inbox flag of the segment below, polled one step ahead: the value a step checks was loaded during the step
   // before, so the inbox copy issues at the start of the read phase and its latency hides behind the transform
   int vin_next = 0;
-  if (SEG && q > 0) vin_next = __hip_atomic_load(fl - 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (SEG && q > 0) vin_next = __hip_atomic_load(fl - FW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if defined(MIOC_STAMPS)
   unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -281,13 +283,13 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
     const int need_in = SEG && q > 0 ? nt - 1 - i : INT_MIN;
     const int need_cons = SEG && q < S - 1 && i + NB <= nt - 2 ? nt - 1 - (i + NB) : INT_MIN;
     int vin = vin_next, vcons = 0;
-    if (SEG && need_cons != INT_MIN) vcons = __hip_atomic_load(fl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (SEG && need_cons != INT_MIN) vcons = __hip_atomic_load(fl + FW + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // ================= read phase: Φ_{i+1} rows into registers, the transform, results into registers ========
     FS_T(q0);
     // ---- the segment below has published this step's outbox: load it (consumed in the write phase) --------
-    if (SEG && q > 0 && wait_flag(fl - 2, vin, need_in)) {
-      if (i >= 1) vin_next = vin >= need_in + 1 ? vin : __hip_atomic_load(fl - 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (SEG && q > 0 && wait_flag(fl - FW, vin, need_in)) {
+      if (i >= 1) vin_next = vin >= need_in + 1 ? vin : __hip_atomic_load(fl - FW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // LDS-DMA of the slot, 1 KiB chunks by wave (inline asm: the compiler does not make later LDS accesses
       // wait for it; the drain before barrier 1 completes it, the barrier publishes it)
       const char *slot = ring_in + (size_t)(i % NB) * A.slot_bytes;
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(FS2_MAXT) __attribute__((amdgpu_waves_per_eu(!SEG &
       if (q > 0) __hip_atomic_store(fl + 1, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // inbox i read
     }
     // ================= write phase: Φ_i ======================================================================
-    if (SEG && need_cons != INT_MIN) wait_flag(fl + 3, vcons, need_cons);
+    if (SEG && need_cons != INT_MIN) wait_flag(fl + FW + 1, vcons, need_cons);
     // the write offsets from a second opaque copy of the thread index, taken after the barrier: computed before
     // it, they would stay live through the whole read phase
     int tidw = tid;

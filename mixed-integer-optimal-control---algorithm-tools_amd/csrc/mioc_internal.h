@@ -120,6 +120,23 @@ hipError_t launch_expand(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv
 // [K][nt][8 waves][32] uint16, per wave of the persistent separable driver the in-wave offsets of the second elements
 // of seam-straddling position pairs
 // counters (nullable): [3] += seams a wave's list could not hold (an internal-consistency failure, must stay 0)
+// k_pinf_recur_ws's segment flags: this many 32-bit words apart (packed, one line held all 13 segments' flags of
+// C2 / C3; 128 bytes apart the single-subproblem recursion is 2-3 % faster, profiles/round6_flag_stride.txt); the
+// segmented p = Inf kernels' error word sits at K · pinf_recur_segments · this (k_pinf_recur_mc / _mcw keep their
+// flags packed: spaced out, _mcw was 6 % slower)
+#ifndef PINF_WS_FLAG_STRIDE
+#define PINF_WS_FLAG_STRIDE 32
+#endif
+// k_fsep2's segment records {outbox token, consumed token}: this many 32-bit words apart (>= 2)
+#ifndef FSEP_FLAG_STRIDE
+#define FSEP_FLAG_STRIDE 2
+#endif
+// k_sdt_run's row flags (done, loaded): this many 32-bit words apart.  Packed (1), one 128-byte line carried the flags
+// of 32 rows, each stored every item by its own row and polled by the 28 rows around it; 32-byte spacing is 2 % faster
+// at full C4 and cuts the run-to-run spread (7.02-7.28 -> 6.94-7.03 us per DP step, profiles/round6_flag_stride.txt)
+#ifndef SDT_FLAG_STRIDE
+#define SDT_FLAG_STRIDE 8
+#endif
 hipError_t launch_pyr_order(hipStream_t s, const ProblemDev &P, const PyrGeom &G, uint32_t *perm,
                             int32_t *same2 = nullptr, uint16_t *strad = nullptr, int32_t *counters = nullptr);
 hipError_t launch_pyr_terminal(hipStream_t s, const ProblemDev &P, const LevelsDev &Lv, const uint32_t *perm, double *S,

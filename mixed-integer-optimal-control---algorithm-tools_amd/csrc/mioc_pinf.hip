@@ -632,7 +632,9 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
   double *A = sm, *Kbuf = sm + (size_t)NS * AS;  // Kbuf: [2][CH][BWP]
   const double *kmin = D.kmin + (size_t)k * nt * BWP;
   double *R = D.R + (size_t)k * nt * RP;
-  int32_t *done = flags + (size_t)k * nseg, *err = flags + (size_t)K * nseg;
+  // segments' flags packed; the error word where every segmented p = Inf kernel keeps it
+  constexpr int FS = 1;
+  int32_t *done = flags + (size_t)k * nseg * FS, *err = flags + (size_t)K * nseg * PINF_WS_FLAG_STRIDE;
   const __amdgpu_buffer_rsrc_t Rr = __builtin_amdgcn_make_buffer_rsrc(R, 0, (int)((size_t)nt * RP * 8), 0x00020000);
   auto slot = [&](int s) { return A + (size_t)(s % NS) * AS; };
   // terminal row R_{n-1}[c'] = Kmin_{n-1}[c'] (c' < BWP), the rows below included (a function of kmin: no hand-off)
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
     const int need = nt - 1 - s;
     for (int d = 1; d * RPS <= 32 && q - d >= 0; ++d) {
       unsigned spins = 0;
-      while (__hip_atomic_load(done + q - d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+      while (__hip_atomic_load(done + (q - d) * FS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
           __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return false;
@@ -806,7 +808,7 @@ __global__ __launch_bounds__(64) void k_pinf_recur_mc(ProblemDev P, PinfDev D, i
     }
     // this chunk's rows have landed: publish its last step for the segments above
     vm_drain();
-    if (lane == 0) __hip_atomic_store(done + q, nt - 1 - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(done + q * FS, nt - 1 - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     hi = nhi;
     lo = nlo;
   }
@@ -834,7 +836,9 @@ __global__ __launch_bounds__(256) void k_pinf_recur_mcw(ProblemDev P, PinfDev D,
   double *A = sm, *Kbuf = sm + (size_t)NS * AS, *Pbuf = Kbuf + (size_t)2 * CH * BWP;  // Pbuf: [2][CH][RPS]
   const double *kmin = D.kmin + (size_t)k * nt * BWP;
   double *R = D.R + (size_t)k * nt * RP;
-  int32_t *done = flags + (size_t)k * nseg, *err = flags + (size_t)K * nseg;
+  // segments' flags packed; the error word where every segmented p = Inf kernel keeps it
+  constexpr int FS = 1;
+  int32_t *done = flags + (size_t)k * nseg * FS, *err = flags + (size_t)K * nseg * PINF_WS_FLAG_STRIDE;
   const __amdgpu_buffer_rsrc_t Rr = __builtin_amdgcn_make_buffer_rsrc(R, 0, (int)((size_t)nt * RP * 8), 0x00020000);
   auto slot = [&](int s) { return A + (size_t)(s % NS) * AS; };
   // terminal row R_{n-1}[c'] = Kmin_{n-1}[c'] (c' < BWP), the rows below included (a function of kmin: no hand-off)
@@ -873,7 +877,7 @@ __global__ __launch_bounds__(256) void k_pinf_recur_mcw(ProblemDev P, PinfDev D,
       const int need = nt - 1 - (clo + 1);
       for (int d = 1; d * RPS <= 32 && q - d >= 0 && ok; ++d) {
         unsigned spins = 0;
-        while (__hip_atomic_load(done + q - d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        while (__hip_atomic_load(done + (q - d) * FS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
           if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
             __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (lane == 0) s_stop = 1;
@@ -957,7 +961,7 @@ __global__ __launch_bounds__(256) void k_pinf_recur_mcw(ProblemDev P, PinfDev D,
       }
       // this chunk's rows have landed: publish its last step for the segments above
       vm_drain();
-      if (lane == 0) __hip_atomic_store(done + q, nt - 1 - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(done + q * FS, nt - 1 - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (nhi >= 0) {
       prepare(nlo, nhi, (qq + 1) & 1);
     }
@@ -999,7 +1003,9 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
   double *Hbuf = sm, *Kbuf = sm + (size_t)2 * CE * HB;
   const double *kmin = D.kmin + (size_t)k * nt * BWP;
   double *R = D.R + (size_t)k * nt * RP;
-  int32_t *done = flags + (size_t)k * nseg, *err = flags + errw;
+  // segments' flags PINF_WS_FLAG_STRIDE words apart (mioc_internal.h)
+  constexpr int FS = PINF_WS_FLAG_STRIDE;
+  int32_t *done = flags + (size_t)k * nseg * FS, *err = flags + errw;
   const __amdgpu_buffer_rsrc_t Rr = __builtin_amdgcn_make_buffer_rsrc(R, 0, (int)((size_t)nt * RP * 8), 0x00020000);
   for (int e = lane; e < 2 * CE * HB; e += 64) Hbuf[e] = INFINITY;  // (segment 0: rows below 0 stay +Inf)
   for (int e = lane; e < 2 * CE * BWP; e += 64) Kbuf[e] = INFINITY;
@@ -1011,7 +1017,7 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
     if (q == 0) return true;
     const int need = nt - 1 - s;
     unsigned spins = 0;
-    while (__hip_atomic_load(done + q - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+    while (__hip_atomic_load(done + (q - 1) * FS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
       if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return false;
@@ -1069,7 +1075,7 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
           asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // S: every store but this chunk's first S
         else
           vm_drain();
-        if (lane == 0) __hip_atomic_store(done + q, nt - 1 - prev_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(done + q * FS, nt - 1 - prev_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (nhi >= 0) {  // (the poll first: its wait would otherwise also wait for the DMAs)
         if (!wait_below(nlo + 1)) {
@@ -1150,7 +1156,7 @@ __global__ __launch_bounds__(64) void k_pinf_recur_ws(ProblemDev P, PinfDev D, i
   // the last chunk's rows have landed: publish it (segments above wait for it)
   vm_drain();
   if (!stop && prev_lo >= 0 && lane == 0)
-    __hip_atomic_store(done + q, nt - 1 - prev_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(done + q * FS, nt - 1 - prev_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // rows c_from .. RP-1 of R (beyond the rows k_pinf_recur_xr / _mc compute, all above B): +Inf for every step
@@ -1190,7 +1196,7 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
     const int nseg = (P.B + 1 + 63) / 64;
     if (PINF_RECUR_WS && flags && segmented && D.BW >= 1 && D.BW <= 8 && D.BWP == 8 && nseg >= 2 &&
         P.K * nseg <= ncu && 64 * nseg <= P.RP && (size_t)P.nt * P.RP * 8 < (1ull << 31)) {
-      const int errw = P.K * pinf_recur_segments(P);
+      const int errw = P.K * pinf_recur_segments(P) * PINF_WS_FLAG_STRIDE;
       const size_t lds = (size_t)2 * (PINF_WS_CHUNK + 4) * (8 + D.BWP) * sizeof(double);  // Hbuf, Kbuf
       const dim3 grid(P.K * nseg);
       switch (D.BW < 2 ? 2 : D.BW) {

@@ -1400,18 +1400,18 @@ struct SdPipe {
   __device__ __forceinline__ void early() {
     SD_TL_AT(g0, i, nt, 1);
     const int tid = threadIdx.x, lane = tid & 63, s = lane < 32 ? lane + 1 : lane - 31;
-    fp = lk + cp;
+    fp = lk + cp * SDT_FLAG_STRIDE;
     need = INT32_MIN;
     if (lane < 32) {
       const int r = ncp - s;
       if (has_next && s <= 7 * M && r >= 1 && r < lo && nt - 2 - ni > 0) {
-        fp = dk + r;
+        fp = dk + r * SDT_FLAG_STRIDE;
         need = nt - 2 - ni;  // token(ni + 1)
       }
     } else {
       const int r = cp + s;
       if (s <= 7 * M && r <= B && r >= hi && nt - i - NB > 0) {
-        fp = lk + r;
+        fp = lk + r * SDT_FLAG_STRIDE;
         need = nt - i - NB;  // token(i + NB - 1)
       }
     }
@@ -1427,7 +1427,7 @@ struct SdPipe {
     const int tid = threadIdx.x;
     // evaluated before the flag store below: the compiler's wait for `val` would otherwise cover that store
     bool ready = __all(val >= need);
-    if (tid == 0) __hip_atomic_store(lk + cp, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(lk + cp * SDT_FLAG_STRIDE, nt - 1 - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     while (!ready) {
       if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > spin_limit) {
@@ -1475,7 +1475,7 @@ struct SdPipe {
   }
   __device__ __forceinline__ void publish() {
     if (threadIdx.x == 0 && pcp >= 0)
-      __hip_atomic_store(dk + pcp, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dk + pcp * SDT_FLAG_STRIDE, nt - 1 - pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // a timed-out wait of this row (go(), before this barrier) set sh.stop: read here, where every wave reads the same
     // value, so that the driver's exit test after the row needs no LDS round trip of its own
     stop_seen = sh->stop != 0;
@@ -1510,7 +1510,9 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   extern __shared__ __attribute__((aligned(16))) unsigned char sds[];
   __shared__ SdtShared<(1 << (3 * M - 3)) / 64> sh;
   const int B = P.B, R = B + 1, nt = P.nt, tid = threadIdx.x;
-  int32_t *done = flags, *loaded = flags + P.K * R, *err = flags + 2 * P.K * R;
+  // (each flag SDT_FLAG_STRIDE words apart)
+  const int FR = R * SDT_FLAG_STRIDE;
+  int32_t *done = flags, *loaded = flags + P.K * FR, *err = flags + 2 * P.K * FR;
   const int W = nwg / P.K;  // workgroups per subproblem (the host guarantees 1 <= W <= B)
   const int k = (int)blockIdx.x / W, wl = (int)blockIdx.x - k * W;
   if (k >= P.K) return;
@@ -1524,7 +1526,7 @@ __global__ __launch_bounds__(1 << (3 * M - 3), 2) void k_sdt_run(ProblemDev P, L
   SdPipe<M> h;
   h.lo = lo, h.hi = hi, h.B = B, h.NB = NB, h.nt = nt, h.k = k, h.g0 = k * R + lo;
   h.spin_limit = spin_limit, h.rowb = (unsigned)L * 8u, h.bufb = (unsigned)R * h.rowb, h.r0b = (unsigned)NB * h.bufb;
-  h.dk = done + (size_t)k * R, h.lk = loaded + (size_t)k * R, h.err = err;
+  h.dk = done + (size_t)k * FR, h.lk = loaded + (size_t)k * FR, h.err = err;
   h.pk = perm_all + (size_t)k * nt * L, h.slot = slot;
   h.rs = __builtin_amdgcn_make_buffer_rsrc(reg, 0, (int)(h.r0b + (unsigned)nt * h.rowb), 0x00020000);
   h.dfa = df_all, h.uoa = uo_all, h.sm = same2, h.sds = sds, h.sh = &sh;
