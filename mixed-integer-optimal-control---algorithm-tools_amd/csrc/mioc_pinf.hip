@@ -1216,7 +1216,7 @@ hipError_t launch_pinf_recur(hipStream_t s, const ProblemDev &P, const PinfDev &
     }
   }
   // few subproblems, classes <= 32, tall enough: row segments of 32 on several CUs (k_pinf_recur_mc); the flags
-  // (K·nseg + 1 words, zeroed by the caller) carry the hand-off and the error word
+  // (K·nseg·PINF_WS_FLAG_STRIDE + 1 words, zeroed by the caller) carry the hand-off (packed) and, last, the error word
   {
     constexpr int LPR = PINF_RECUR_MC_LANES, RPS = 64 / LPR;  // lanes per row, rows per segment
     const int nseg = (P.B + 1 + RPS - 1) / RPS;
